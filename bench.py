@@ -1,0 +1,197 @@
+"""Headline benchmark: sorted 31-mers/s on a 3.1 Gb synthetic genome (BASELINE.json config C3).
+
+One step = the hot path over the whole genome with the sequence byte array already in HBM:
+enumerate -> encode (2-bit keys) -> stable LSD radix sort -> unique k-mers + multiplicities.
+Timed with a barrier + device synchronisation on both sides, max over ranks.
+
+N = 1: the genome on one MI355X.  N > 1 (torch.distributed, one rank per GPU): the same genome is
+split into N contiguous position ranges (a (k-1)-base halo each); every rank encodes its range,
+the ranks exchange k-mers by top key bits in ONE all-to-all over RCCL, and each rank sorts and
+counts its key range -- total work fixed, "scaling": "strong".
+
+Also reported: the dominant kernel's roofline (HIP events on the engine's stream) and the CPU
+baseline -- the reference algorithm (numba-quicksort restatement, oracle/) on a bounded sample.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "genome-kmers_amd"))
+sys.path.insert(0, str(ROOT))
+
+METRIC = "sorted 31-mers/sec end-to-end on 3.1 Gb synthetic genome; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--genome-len", type=int, default=3_100_000_000)
+    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-sample", type=int, default=4_000_000, help="k-mers in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", type=str, default=str(ROOT / "profiles" / "traffic_latest.json"),
+                    help="per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc (if present)")
+    return ap.parse_args()
+
+
+def make_genome(L: int, seed: int) -> np.ndarray:
+    """Uniform i.i.d. random bases over the reference's alphabet order (profiling.py:12-24)."""
+    lut = np.frombuffer(b"ATGC", dtype=np.uint8)
+    out = np.empty(L, dtype=np.uint8)
+    rng = np.random.default_rng(seed)
+    chunk = 1 << 28
+    for at in range(0, L, chunk):
+        m = min(chunk, L - at)
+        out[at:at + m] = lut[rng.integers(0, 4, m, dtype=np.uint8)]
+    return out
+
+
+def cpu_baseline(sba: np.ndarray, k: int, sample: int) -> dict:
+    """Reference algorithm (Kmers.sort: numba quicksort + byte comparator with validation,
+    kmers.py:1624-1731) restated in C (oracle/gk_oracle.c), 1 thread, on the first `sample` k-mers."""
+    from oracle import oracle
+
+    sub = np.ascontiguousarray(sba[: sample + k - 1])
+    starts = np.arange(sample, dtype=np.uint32)
+    t0 = time.perf_counter()
+    oracle.quicksort(sub, starts, k, k)
+    dt = time.perf_counter() - t0
+    return {"value": sample / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample:,} {k}-mers of the same genome (single contig), numba-quicksort "
+                      f"restatement with validate_kmers, gcc -O3, 1 thread; {dt:.1f} s"}
+
+
+def load_traffic(path: str, kernel: str):
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+        return t.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from genome_kmers import _native
+
+    k = args.k
+    L = args.genome_len
+    sba = make_genome(L, args.seed)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if world == 1:
+        eng = _native.Engine(local)
+        t0 = time.perf_counter()
+        eng.set_sequence(sba, np.zeros(1, dtype=np.uint32))
+        eng.sync()
+        h2d_ms = (time.perf_counter() - t0) * 1e3
+        n_units = L - k + 1
+
+        def step():
+            eng.enumerate(k)
+            eng.sort(k)
+            return eng.unique_count_only()
+    else:
+        from genome_kmers import distributed
+
+        job = distributed.ShardedKmerSort(sba, np.zeros(1, dtype=np.uint32), k, rank, world, device=local)
+        eng = job.engine
+        h2d_ms = job.h2d_ms
+        n_units = job.total_kmers
+
+        def step():
+            return job.run()
+
+    n_unique = None
+    for _ in range(args.warmup):
+        n_unique = step()
+    barrier()
+    eng.profile_enable(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_unique = step()
+    eng.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    report = eng.profile_report()
+    eng.profile_enable(False)
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        u = torch.tensor([n_unique], dtype=torch.int64, device="cuda")
+        dist.all_reduce(u)
+        n_unique = int(u.item())
+
+    ms_per_step = dt / args.steps * 1e3
+    value = n_units * args.steps / dt
+
+    # dominant kernel: one radix scatter pass; algorithmic bytes = read (key 8 B + start 4 B) +
+    # write (8 B + 4 B) per k-mer of the launch
+    rp = report.get("radix_pass", {"count": 0, "total_ms": 0.0})
+    local_n = eng.n if world == 1 else job.local_kmers
+    bytes_per_launch = local_n * 24
+    avg_ms = rp["total_ms"] / max(rp["count"], 1)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
+    traffic = load_traffic(args.traffic, "onesweep_kernel")
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "onesweep_kernel<1> (one 8-bit LSD radix pass)", "avg_launch_ms": round(avg_ms, 4),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "pipeline_read_frac": round(n_units * 105 / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(sba, k, args.cpu_sample)
+            cpu["cores_on_box"] = os.cpu_count()
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": f"synthetic: uniform random ACGT, numpy PCG64 seed {args.seed}",
+            "config": {"workload": f"C3: {L:,}-base synthetic single-contig genome, k={k} (min=max={k})",
+                       "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
+                       "parallelism": f"position-range shards x{world} + 1 RCCL all-to-all" if world > 1 else "1 GPU",
+                       "h2d_sba_ms": round(h2d_ms, 2), "stages_ms_per_step": stages},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

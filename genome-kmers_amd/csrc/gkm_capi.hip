@@ -1,0 +1,686 @@
+// gkm_capi.hip -- the extern "C" boundary of libgkm.so and the sort orchestration.
+//
+// Sort strategies:
+//   direct   max_kmer_len given and the padded key fits 256 bits: encode once, LSD radix sort.
+//   doubling max_kmer_len None (suffix order up to '$', the Kmers default) or a very long bound:
+//            prefix doubling over every sba position -- seed keys of 21 (ACGT) / 16 (IUPAC)
+//            symbols, then rounds of (rank[p], rank[p + h]) 64-bit keys, each a stable radix sort --
+//            and finally the starts with >= min_kmer_len bases are kept, in order.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+
+#include "gkm_internal.h"
+
+namespace gkm {
+
+hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (*p && *cap >= bytes) return hipSuccess;
+    if (*p) {
+        hipError_t e = hipFree(*p);
+        if (e != hipSuccess) return e;
+        *p = nullptr;
+        *cap = 0;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
+    *cap = bytes;
+    return hipSuccess;
+}
+
+int fail(gk_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(gk_ctx *c, hipError_t e, const char *where) {
+    std::string m = std::string(hipGetErrorString(e)) + " at " + where;
+    return fail(c, e == hipErrorOutOfMemory ? GK_E_OOM : GK_E_HIP, m);
+}
+
+void timer_begin(gk_ctx *c, const char *name, int *slot) {
+    *slot = -1;
+    if (!c->profile) return;
+    Timer t;
+    t.name = name;
+    if (hipEventCreate(&t.start) != hipSuccess || hipEventCreate(&t.stop) != hipSuccess) return;
+    hipEventRecord(t.start, c->stream);
+    c->timers.push_back(t);
+    *slot = (int)c->timers.size() - 1;
+}
+
+void timer_end(gk_ctx *c, int slot) {
+    if (slot < 0 || !c->profile) return;
+    hipEventRecord(c->timers[slot].stop, c->stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// prefix-doubling kernels
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t seg_end_of(const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
+                                               uint64_t p) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)seg[mid] <= p) lo = mid; else hi = mid;
+    }
+    return (lo + 1 == nseg) ? L - 1 : (uint64_t)seg[lo + 1] - 2;
+}
+
+// R[vals[i]] = gstart[gid[i] - 1] + 1   (rank = 1 + index of the group's first element)
+__global__ __launch_bounds__(256) void rank_scatter_kernel(const uint32_t *__restrict__ vals,
+                                                           const uint32_t *__restrict__ gid,
+                                                           const uint32_t *__restrict__ gstart, uint64_t n,
+                                                           uint32_t *__restrict__ R) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        R[vals[i]] = gstart[gid[i] - 1] + 1;
+}
+
+// key = rank[p] << 32 | (p + o <= seg_end(p) ? rank[p + o] : 0)
+__global__ __launch_bounds__(256) void pair_keys_kernel(const uint32_t *__restrict__ vals,
+                                                        const uint32_t *__restrict__ R,
+                                                        const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
+                                                        uint64_t o, uint64_t n, uint64_t *__restrict__ keys) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = vals[i];
+        const uint64_t q = p + o;
+        const uint32_t r2 = (q <= seg_end_of(seg, nseg, L, p)) ? R[q] : 0u;
+        keys[i] = ((uint64_t)R[p] << 32) | r2;
+    }
+}
+
+// keep starts with >= m bases before the end of their segment
+__global__ __launch_bounds__(256) void len_flags_kernel(const uint32_t *__restrict__ vals,
+                                                        const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
+                                                        uint64_t m, uint64_t n, uint8_t *__restrict__ flags) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = vals[i];
+        flags[i] = (p + m - 1 <= seg_end_of(seg, nseg, L, p)) ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void gather_pairs_kernel(const uint32_t *__restrict__ idx, uint64_t count,
+                                                           const uint32_t *__restrict__ vin,
+                                                           const uint64_t *__restrict__ kin,
+                                                           uint32_t *__restrict__ vout, uint64_t *__restrict__ kout) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = idx[i];
+        vout[i] = vin[j];
+        kout[i] = kin[j];
+    }
+}
+
+// keys[i] = R[starts[i]] (final rank of a user-provided start)
+__global__ __launch_bounds__(256) void rank_gather_kernel(const uint32_t *__restrict__ starts,
+                                                          const uint32_t *__restrict__ R, uint64_t n,
+                                                          uint64_t *__restrict__ keys) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        keys[i] = R[starts[i]];
+}
+
+__global__ __launch_bounds__(256) void u32_to_key_kernel(const uint32_t *__restrict__ v, uint64_t n,
+                                                         uint64_t *__restrict__ keys) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        keys[i] = v[i];
+}
+
+__global__ __launch_bounds__(256) void full_key_heads_kernel(const uint64_t *__restrict__ keys, uint64_t n,
+                                                             uint8_t *__restrict__ head) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+static int grid_of(uint64_t n, int cap = 8192) {
+    uint64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    return (int)std::min<uint64_t>(g, (uint64_t)cap);
+}
+
+hipError_t launch_rank_scatter(gk_ctx *c, const uint32_t *vals, const uint32_t *gid, const uint32_t *gstart,
+                               uint64_t n, uint32_t *R) {
+    hipLaunchKernelGGL(rank_scatter_kernel, dim3(grid_of(n)), dim3(256), 0, c->stream, vals, gid, gstart, n, R);
+    return hipGetLastError();
+}
+
+}  // namespace gkm
+
+using namespace gkm;
+
+// ---------------------------------------------------------------------------------------------
+// buffers
+// ---------------------------------------------------------------------------------------------
+static int ensure_elems(gk_ctx *c, uint64_t n, int words) {
+    // vals[0] / vals[1] hold data that must survive when only keys grow; grow both together
+    if (n > c->elem_cap) {
+        uint32_t *nv[2] = {nullptr, nullptr};
+        for (int b = 0; b < 2; ++b) GK_TRY_HIP(c, hipMalloc(&nv[b], 4 * (n + 64)));
+        if (c->have_starts && c->elem_cap > 0)
+            GK_TRY_HIP(c, hipMemcpyAsync(nv[c->cur], c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToDevice, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (int b = 0; b < 2; ++b) {
+            if (c->vals[b]) hipFree(c->vals[b]);
+            c->vals[b] = nv[b];
+            if (c->keys[b]) hipFree(c->keys[b]);
+            c->keys[b] = nullptr;
+        }
+        c->elem_cap = n;
+        c->key_words_cap = 0;
+        c->keys_valid = false;
+    }
+    if (words > c->key_words_cap) {
+        for (int b = 0; b < 2; ++b) {
+            if (c->keys[b]) hipFree(c->keys[b]);
+            c->keys[b] = nullptr;
+            GK_TRY_HIP(c, hipMalloc(&c->keys[b], 8 * (uint64_t)words * (c->elem_cap + 64)));
+        }
+        c->key_words_cap = words;
+        c->keys_valid = false;
+    }
+    const uint64_t tiles = (n + kSortTile - 1) / kSortTile + 1;
+    if (tiles * 256 > c->status_cap) {
+        if (c->status) hipFree(c->status);
+        c->status = nullptr;
+        GK_TRY_HIP(c, hipMalloc(&c->status, 8 * tiles * 256));
+        GK_TRY_HIP(c, hipMemsetAsync(c->status, 0, 8 * tiles * 256, c->stream));
+        c->status_cap = tiles * 256;
+    }
+    return GK_OK;
+}
+
+namespace gkm {
+int materialize_starts(gk_ctx *c) {
+    if (!c->have_starts || c->starts_materialized) return GK_OK;
+    int slot;
+    timer_begin(c, "enumerate", &slot);
+    GK_TRY_HIP(c, launch_enumerate(c, c->min_k, c->vals[c->cur]));
+    timer_end(c, slot);
+    c->starts_materialized = true;
+    return GK_OK;
+}
+}  // namespace gkm
+
+// ---------------------------------------------------------------------------------------------
+// lifetime
+// ---------------------------------------------------------------------------------------------
+extern "C" int gk_device_count(int *count) {
+    if (!count) return GK_E_ARG;
+    hipError_t e = hipGetDeviceCount(count);
+    return e == hipSuccess ? GK_OK : GK_E_HIP;
+}
+
+extern "C" int gk_create(gk_ctx **out, int device) {
+    if (!out) return GK_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GK_E_HIP;
+    if (device < 0 || device >= ndev) return GK_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return GK_E_HIP;
+    gk_ctx *c = new gk_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->counters, 4 * 64) != hipSuccess || hipMalloc(&c->hist, 4 * 256 * kMaxWords * 8) != hipSuccess ||
+        hipMalloc(&c->offsets, 4 * 256 * kMaxWords * 8) != hipSuccess || hipMalloc(&c->scalars, 8 * 64) != hipSuccess) {
+        gk_destroy(c);
+        return GK_E_HIP;
+    }
+    *out = c;
+    return GK_OK;
+}
+
+extern "C" void gk_destroy(gk_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
+                    c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->cumk, c->tile_sums, c->scalars,
+                    c->dhist, c->mask, c->ranks};
+    for (void *b : bufs)
+        if (b) hipFree(b);
+    for (auto &t : c->timers) {
+        hipEventDestroy(t.start);
+        hipEventDestroy(t.stop);
+    }
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char *gk_last_error(gk_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int gk_sync(gk_ctx *c) {
+    if (!c) return GK_E_ARG;
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
+extern "C" int gk_stream(gk_ctx *c, void **stream) {
+    if (!c || !stream) return GK_E_ARG;
+    *stream = (void *)c->stream;
+    return GK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// input
+// ---------------------------------------------------------------------------------------------
+extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, const uint32_t *seg_starts, uint64_t nseg) {
+    if (!c) return GK_E_ARG;
+    if (!sba || len == 0) return fail(c, GK_E_ARG, "sequence byte array is empty");
+    if (!seg_starts || nseg == 0) return fail(c, GK_E_ARG, "sequence_collection is empty");
+    if (len > 0xFFFFFFFFull) return fail(c, GK_E_LIMIT, "sequence byte array longer than 2^32-1");
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (seg_starts[0] != 0) return fail(c, GK_E_ARG, "first segment must start at 0");
+    uint64_t max_len = 0;
+    bool internal = false;
+    for (uint64_t s = 0; s < nseg; ++s) {
+        const uint64_t b = seg_starts[s];
+        const uint64_t e = (s + 1 == nseg) ? len - 1 : (uint64_t)seg_starts[s + 1] - 2;
+        if (s + 1 < nseg && ((uint64_t)seg_starts[s + 1] < b + 2 || (uint64_t)seg_starts[s + 1] > len))
+            return fail(c, GK_E_ARG, "segment starts are not strictly increasing by >= 2");
+        if (s > 0 && sba[b - 1] != GK_DOLLAR) internal = true;  // separator missing
+        if (e < b) return fail(c, GK_E_ARG, "empty segment");
+        max_len = std::max<uint64_t>(max_len, e - b + 1);
+    }
+    const uint64_t padded = ((len + kEncodeTile - 1) / kEncodeTile) * kEncodeTile + kSbaPad;
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->sba), &c->sba_cap, padded));
+    GK_TRY_HIP(c, hipMemsetAsync(c->sba + len, GK_DOLLAR, c->sba_cap - len, c->stream));
+    GK_TRY_HIP(c, hipMemcpyAsync(c->sba, sba, len, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->seg), &c->seg_cap, 4 * nseg));
+    GK_TRY_HIP(c, hipMemcpyAsync(c->seg, seg_starts, 4 * nseg, hipMemcpyHostToDevice, c->stream));
+    c->sba_len = len;
+    c->nseg = nseg;
+    c->hseg.assign(seg_starts, seg_starts + nseg);
+    c->max_seg_len = max_len;
+    uint32_t *d_flags = reinterpret_cast<uint32_t *>(c->scalars + 8);
+    GK_TRY_HIP(c, launch_alphabet(c, d_flags));
+    uint32_t h[2] = {0, 0};
+    GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = false;
+    c->n = 0;
+    if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
+    c->acgt = (h[0] & 2u) ? 0 : 1;
+    c->internal_dollar = internal || (uint64_t)h[1] != nseg - 1;
+    return GK_OK;
+}
+
+extern "C" int gk_alphabet_is_acgt(gk_ctx *c, int *is_acgt) {
+    if (!c || !is_acgt) return GK_E_ARG;
+    *is_acgt = c->acgt;
+    return GK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// enumerate (kmers.py:789-861)
+// ---------------------------------------------------------------------------------------------
+extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
+    if (!c) return GK_E_ARG;
+    if (!c->sba) return fail(c, GK_E_STATE, "no sequence loaded");
+    if (min_k < 1) return fail(c, GK_E_ARG, "min_kmer_len must be greater than zero");
+    uint64_t n = 0, shortest = ~0ull;
+    for (uint64_t s = 0; s < c->nseg; ++s) {
+        const uint64_t e = (s + 1 == c->nseg) ? c->sba_len - 1 : (uint64_t)c->hseg[s + 1] - 2;
+        const uint64_t l = e - c->hseg[s] + 1;
+        shortest = std::min(shortest, l);
+        if (l >= min_k) n += l - min_k + 1;
+    }
+    if (min_k > shortest) return fail(c, GK_E_ARG, "min_kmer_len must be <= the shortest sequence length");
+    if (n > 0xFFFFFFFFull) return fail(c, GK_E_LIMIT, "the size of the required kmers array exceeds the limit set by a uint32");
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    c->have_starts = false;
+    int rc = ensure_elems(c, n, 1);
+    if (rc != GK_OK) return rc;
+    c->n = n;
+    c->min_k = min_k;
+    c->cur = 0;
+    // The enumerate output is a pure function of (seg, min_k): it is materialised lazily by the
+    // first reader (materialize_starts); the encoder regenerates positions itself.
+    c->have_starts = true;
+    c->enumerated = true;
+    c->starts_materialized = false;
+    c->sorted = c->keys_valid = c->unique_valid = false;
+    if (n_out) *n_out = n;
+    return GK_OK;
+}
+
+extern "C" int gk_set_start_indices(gk_ctx *c, const uint32_t *src, uint64_t n, uint32_t min_k) {
+    if (!c) return GK_E_ARG;
+    if (!c->sba) return fail(c, GK_E_STATE, "no sequence loaded");
+    if (n > 0 && !src) return fail(c, GK_E_ARG, "null start array");
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    c->have_starts = false;
+    int rc = ensure_elems(c, std::max<uint64_t>(n, 1), 1);
+    if (rc != GK_OK) return rc;
+    c->cur = 0;
+    if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->vals[0], src, 4 * n, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    c->n = n;
+    c->min_k = min_k;
+    c->have_starts = true;
+    c->enumerated = false;
+    c->starts_materialized = true;
+    c->sorted = c->keys_valid = c->unique_valid = false;
+    return GK_OK;
+}
+
+extern "C" int gk_num_kmers(gk_ctx *c, uint64_t *n) {
+    if (!c || !n) return GK_E_ARG;
+    *n = c->have_starts ? c->n : 0;
+    return GK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// sort (kmers.py:1624-1731)
+// ---------------------------------------------------------------------------------------------
+static int bit_width(uint64_t v) {
+    int b = 0;
+    while (v) {
+        ++b;
+        v >>= 1;
+    }
+    return b;
+}
+
+// stable pre-sort of arbitrary start indices by value, so ties end in start order
+static int presort_by_start(gk_ctx *c) {
+    hipLaunchKernelGGL(u32_to_key_kernel, dim3(grid_of(c->n)), dim3(256), 0, c->stream, c->vals[c->cur], c->n,
+                       c->keys[c->cur]);
+    GK_TRY_HIP(c, hipGetLastError());
+    return radix_sort(c, 1, 32, false);
+}
+
+static int sort_direct(gk_ctx *c, const KeySpec &ks) {
+    int rc = ensure_elems(c, c->n, ks.words);
+    if (rc != GK_OK) return rc;
+    bool hist_ready = false;
+    if (c->enumerated) {
+        int slot;
+        timer_begin(c, "encode", &slot);
+        GK_TRY_HIP(c, launch_encode_positions(c, ks, c->keys[c->cur], c->vals[c->cur], c->hist));
+        timer_end(c, slot);
+        hist_ready = true;
+    } else {
+        rc = presort_by_start(c);
+        if (rc != GK_OK) return rc;
+        int slot;
+        timer_begin(c, "encode", &slot);
+        GK_TRY_HIP(c, launch_encode_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur]));
+        timer_end(c, slot);
+    }
+    rc = radix_sort(c, ks.words, ks.total_bits, hist_ready);
+    if (rc != GK_OK) return rc;
+    c->spec = ks;
+    c->keys_valid = true;
+    c->keys_are_ranks = false;
+    return GK_OK;
+}
+
+// Prefix doubling over all non-'$' positions; M = 0 means unbounded (suffix order).
+static int sort_doubling(gk_ctx *c, uint32_t M) {
+    const uint64_t n_kmers = c->n;
+    const bool was_enumerated = c->enumerated;
+    const uint32_t m = c->min_k;
+    const uint64_t L = c->sba_len;
+    uint32_t *user = nullptr;  // user-provided starts survive in a side buffer
+    if (!was_enumerated && n_kmers > 0) {
+        GK_TRY_HIP(c, hipMalloc(&user, 4 * n_kmers));
+        GK_TRY_HIP(c, hipMemcpyAsync(user, c->vals[c->cur], 4 * n_kmers, hipMemcpyDeviceToDevice, c->stream));
+    }
+    // universe: every position inside a segment (min length 1)
+    uint64_t n1 = L - (c->nseg - 1);
+    int rc = ensure_elems(c, std::max(n1, n_kmers), 1);
+    if (rc != GK_OK) return rc;
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->flags), &c->flags_cap, n1 + 64));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_a), &c->idx_cap, 4 * (n1 + 64)));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_b), &c->idx_b_cap, 4 * (n1 + 64)));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ranks), &c->ranks_cap, 4 * (L + 64)));
+
+    KeySpec seed{};
+    seed.bits = c->acgt ? 3 : 4;
+    seed.symbols = c->acgt ? 21 : 16;
+    seed.lenbits = 0;
+    seed.min_len = 1;
+    seed.words = 1;
+    seed.total_bits = seed.bits * seed.symbols;
+    c->n = n1;
+    c->cur = 0;
+    int slot;
+    timer_begin(c, "encode", &slot);
+    GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], c->hist));
+    timer_end(c, slot);
+    rc = radix_sort(c, 1, seed.total_bits, true);
+    if (rc != GK_OK) return rc;
+
+    uint64_t h = (uint64_t)seed.symbols;
+    const bool bounded = M != 0;
+    bool done = bounded && h >= M;  // (direct path covers M <= capacity; keep for safety)
+    while (!done) {
+        // groups of equal keys
+        hipLaunchKernelGGL(full_key_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->keys[c->cur], n1,
+                           c->flags);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t G = 0;
+        GK_TRY_HIP(c, select_flags(c, c->flags, n1, c->idx_b, &G));
+        if (G == n1) break;                          // all distinct
+        if (!bounded && h >= c->max_seg_len) break;  // every suffix ends within h symbols
+        GK_TRY_HIP(c, scan_flags_inclusive(c, c->flags, n1, c->idx_a));
+        GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
+        GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[c->cur], c->idx_a, c->idx_b, n1, c->ranks));
+        const uint64_t o = bounded ? std::min<uint64_t>(h, M - h) : h;
+        hipLaunchKernelGGL(pair_keys_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->vals[c->cur], c->ranks,
+                           c->seg, (uint32_t)c->nseg, L, o, n1, c->keys[c->cur]);
+        GK_TRY_HIP(c, hipGetLastError());
+        rc = radix_sort(c, 1, 64, false);
+        if (rc != GK_OK) return rc;
+        h += o;
+        if (bounded && h >= M) done = true;
+    }
+
+    if (was_enumerated) {
+        // keep starts with >= m bases, in order
+        hipLaunchKernelGGL(len_flags_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->vals[c->cur], c->seg,
+                           (uint32_t)c->nseg, L, (uint64_t)m, n1, c->flags);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t cnt = 0;
+        GK_TRY_HIP(c, select_flags(c, c->flags, n1, c->idx_a, &cnt));
+        if (cnt != n_kmers) return fail(c, GK_E_HIP, "doubling: k-mer count mismatch after filtering");
+        const int o = c->cur ^ 1;
+        hipLaunchKernelGGL(gather_pairs_kernel, dim3(grid_of(cnt)), dim3(256), 0, c->stream, c->idx_a, cnt,
+                           c->vals[c->cur], c->keys[c->cur], c->vals[o], c->keys[o]);
+        GK_TRY_HIP(c, hipGetLastError());
+        c->cur = o;
+        c->n = cnt;
+    } else {
+        // final dense rank of every position, then sort the user's starts by it
+        hipLaunchKernelGGL(full_key_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->keys[c->cur], n1,
+                           c->flags);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t G = 0;
+        GK_TRY_HIP(c, select_flags(c, c->flags, n1, c->idx_b, &G));
+        GK_TRY_HIP(c, scan_flags_inclusive(c, c->flags, n1, c->idx_a));
+        GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
+        GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[c->cur], c->idx_a, c->idx_b, n1, c->ranks));
+        c->n = n_kmers;
+        c->cur = 0;
+        if (n_kmers) GK_TRY_HIP(c, hipMemcpyAsync(c->vals[0], user, 4 * n_kmers, hipMemcpyDeviceToDevice, c->stream));
+        rc = presort_by_start(c);
+        if (rc != GK_OK) return rc;
+        hipLaunchKernelGGL(rank_gather_kernel, dim3(grid_of(n_kmers)), dim3(256), 0, c->stream, c->vals[c->cur],
+                           c->ranks, n_kmers, c->keys[c->cur]);
+        GK_TRY_HIP(c, hipGetLastError());
+        rc = radix_sort(c, 1, 32, false);
+        if (rc != GK_OK) return rc;
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        hipFree(user);
+    }
+    c->spec = KeySpec{0, 0, 0, (int)m, 1, 64};
+    c->keys_valid = true;
+    c->keys_are_ranks = true;
+    return GK_OK;
+}
+
+extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
+    (void)flags;
+    if (!c) return GK_E_ARG;
+    if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (max_kmer_len != 0 && max_kmer_len < c->min_k) return fail(c, GK_E_ARG, "max_kmer_len is less than min_kmer_len");
+    if (c->internal_dollar)
+        return fail(c, GK_E_NO_BASES, "kmers compared were less than min_kmer_len: the sba holds a '$' inside a segment");
+    if (!c->enumerated && c->n > 0) {
+        uint32_t *d_bad = reinterpret_cast<uint32_t *>(c->scalars + 12);
+        GK_TRY_HIP(c, launch_validate_starts(c, c->vals[c->cur], c->n, c->min_k, d_bad));
+        uint32_t bad = 0;
+        GK_TRY_HIP(c, hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        if (bad) return fail(c, GK_E_NO_BASES, "kmers compared were less than min_kmer_len");
+    }
+    c->unique_valid = false;
+    int rc;
+    if (c->n < 2) {
+        rc = materialize_starts(c);
+        if (rc != GK_OK) return rc;
+        // nothing to order; the group pass compares bytes
+        c->sorted = true;
+        c->sort_len = max_kmer_len;
+        c->keys_valid = false;
+        return GK_OK;
+    }
+    // direct key?
+    KeySpec ks{};
+    bool direct = false;
+    if (max_kmer_len != 0) {
+        ks.bits = c->acgt ? 2 : 4;
+        ks.symbols = (int)max_kmer_len;
+        ks.min_len = (int)c->min_k;
+        const bool bounded = max_kmer_len != c->min_k;
+        ks.lenbits = (bounded && ks.bits == 2) ? bit_width(max_kmer_len) : 0;
+        const uint64_t tb = (uint64_t)ks.bits * max_kmer_len + ks.lenbits;
+        if (tb <= 64ull * kMaxWords) {
+            ks.total_bits = (int)tb;
+            ks.words = (int)((tb + 63) / 64);
+            direct = true;
+        }
+    }
+    rc = direct ? sort_direct(c, ks) : sort_doubling(c, max_kmer_len);
+    if (rc != GK_OK) return rc;
+    c->starts_materialized = true;
+    c->sorted = true;
+    c->enumerated = false;
+    c->sort_len = max_kmer_len;
+    return GK_OK;
+}
+
+extern "C" int gk_copy_start_indices(gk_ctx *c, uint32_t *dst, uint64_t n) {
+    if (!c) return GK_E_ARG;
+    if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers");
+    if (int rc = materialize_starts(c)) return rc;
+    if (n != c->n) return fail(c, GK_E_ARG, "n differs from the k-mer count");
+    if (n == 0) return GK_OK;
+    GK_TRY_HIP(c, hipMemcpyAsync(dst, c->vals[c->cur], 4 * n, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
+extern "C" int gk_copy_start_range(gk_ctx *c, uint64_t offset, uint32_t *dst, uint64_t count) {
+    if (!c) return GK_E_ARG;
+    if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers");
+    if (int rc = materialize_starts(c)) return rc;
+    if (offset > c->n || count > c->n - offset) return fail(c, GK_E_ARG, "range outside the k-mer array");
+    if (count == 0) return GK_OK;
+    GK_TRY_HIP(c, hipMemcpyAsync(dst, c->vals[c->cur] + offset, 4 * count, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
+extern "C" int gk_key_layout(gk_ctx *c, uint32_t *words, uint32_t *bits, uint32_t *symbols) {
+    if (!c) return GK_E_ARG;
+    if (!c->keys_valid) return fail(c, GK_E_STATE, "no encoded keys: sort first");
+    if (words) *words = (uint32_t)c->spec.words;
+    if (bits) *bits = c->keys_are_ranks ? 0u : (uint32_t)c->spec.bits;
+    if (symbols) *symbols = c->keys_are_ranks ? 0u : (uint32_t)c->spec.symbols;
+    return GK_OK;
+}
+
+extern "C" int gk_copy_keys(gk_ctx *c, uint64_t *dst, uint64_t n_words) {
+    if (!c) return GK_E_ARG;
+    if (!c->keys_valid) return fail(c, GK_E_STATE, "no encoded keys: sort first");
+    const uint64_t W = (uint64_t)c->spec.words;
+    if (n_words != W * c->n) return fail(c, GK_E_ARG, "n_words differs from words_per_key * n");
+    if (!n_words) return GK_OK;
+    // device SoA (word-major) -> host AoS (key-major)
+    std::vector<uint64_t> tmp(n_words);
+    GK_TRY_HIP(c, hipMemcpyAsync(tmp.data(), c->keys[c->cur], 8 * n_words, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    if (W == 1) {
+        std::memcpy(dst, tmp.data(), 8 * n_words);
+    } else {
+        for (uint64_t i = 0; i < c->n; ++i)
+            for (uint64_t w = 0; w < W; ++w) dst[i * W + w] = tmp[w * c->n + i];
+    }
+    return GK_OK;
+}
+
+extern "C" int gk_set_filter_mask(gk_ctx *c, const uint8_t *mask, uint64_t n) {
+    if (!c) return GK_E_ARG;
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->mask), &c->mask_cap, n + 64));
+    if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->mask, mask, n, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    c->mask_n = n;
+    return GK_OK;
+}
+
+extern "C" int gk_device_views(gk_ctx *c, void **starts, void **keys, uint64_t *n, uint32_t *words) {
+    if (!c) return GK_E_ARG;
+    if (int rc = materialize_starts(c)) return rc;
+    if (starts) *starts = c->vals[c->cur];
+    if (keys) *keys = c->keys[c->cur];
+    if (n) *n = c->n;
+    if (words) *words = (uint32_t)c->spec.words;
+    return GK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// profiling
+// ---------------------------------------------------------------------------------------------
+extern "C" int gk_profile_enable(gk_ctx *c, int on) {
+    if (!c) return GK_E_ARG;
+    hipStreamSynchronize(c->stream);
+    for (auto &t : c->timers) {
+        hipEventDestroy(t.start);
+        hipEventDestroy(t.stop);
+    }
+    c->timers.clear();
+    c->profile = on != 0;
+    return GK_OK;
+}
+
+extern "C" int gk_profile_report(gk_ctx *c, char *buf, uint64_t buflen) {
+    if (!c || !buf || buflen == 0) return GK_E_ARG;
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    std::map<std::string, std::pair<uint64_t, double>> agg;
+    for (auto &t : c->timers) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
+            auto &a = agg[t.name];
+            a.first += 1;
+            a.second += ms;
+        }
+    }
+    std::string s = "{";
+    bool first = true;
+    for (auto &kv : agg) {
+        char tmp[256];
+        std::snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f}", first ? "" : ", ",
+                      kv.first.c_str(), (unsigned long long)kv.second.first, kv.second.second);
+        s += tmp;
+        first = false;
+    }
+    s += "}";
+    std::snprintf(buf, (size_t)buflen, "%s", s.c_str());
+    return s.size() < buflen ? GK_OK : GK_E_ARG;
+}

@@ -1,0 +1,455 @@
+// gkm_encode.hip -- enumerate + encode kernels (gfx950).
+//
+// Reference behaviour restated here (paths relative to the reference's src/genome_kmers/):
+//   enumerate   kmers.py:789-861      starts = concat_s arange(seg_start_s, seg_end_s - min_k + 2)
+//   order       kmers.py:306-397      byte-wise lexicographic, '$'/end-of-array terminates (less)
+//   alphabet    sequence_collection.py:441-458, 694-697  {A,C,G,T,R,Y,S,W,K,M,B,D,H,V,N,$}
+// The encoders turn the k-mer at a start into an integer whose unsigned order equals that byte
+// order: 2-bit codes when the sba is pure ACGT, 4-bit codes ('$' = 0) otherwise.
+#include "gkm_internal.h"
+
+namespace gkm {
+
+// '$' -> 0 ; A B C D G H K M N R S T V W Y -> 1..15 (ASCII order preserved)
+__constant__ uint8_t c_code4[256];
+// 0: A,C,G,T or '$'   1: other IUPAC letter   2: byte not allowed
+__constant__ uint8_t c_class[256];
+
+static bool g_tables_ready = false;
+
+static hipError_t init_tables() {
+    if (g_tables_ready) return hipSuccess;
+    uint8_t code4[256] = {0}, cls[256];
+    const char *order = "ABCDGHKMNRSTVWY";
+    for (int i = 0; i < 256; ++i) cls[i] = 2;
+    for (int i = 0; order[i]; ++i) {
+        code4[(uint8_t)order[i]] = (uint8_t)(i + 1);
+        cls[(uint8_t)order[i]] = 1;
+    }
+    cls['A'] = cls['C'] = cls['G'] = cls['T'] = 0;
+    cls[GK_DOLLAR] = 0;
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_code4), code4, 256);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_class), cls, 256);
+    if (e != hipSuccess) return e;
+    g_tables_ready = true;
+    return hipSuccess;
+}
+
+struct KS {  // POD copy of KeySpec for kernels
+    int bits, symbols, lenbits, min_len, words, total_bits, digits;
+};
+
+static KS pod(const KeySpec &k) { return KS{k.bits, k.symbols, k.lenbits, k.min_len, k.words, k.total_bits, k.digits()}; }
+
+__device__ __forceinline__ uint32_t code2(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
+
+template <int BITS>
+__device__ __forceinline__ uint32_t sym_code(uint32_t c, const uint8_t *lut4) {
+    if (BITS == 2) return code2(c);
+    if (BITS == 3) return c == GK_DOLLAR ? 0u : code2(c) + 1u;
+    return lut4[c];
+}
+
+// segment index of sba position p: last s with seg[s] <= p
+__device__ __forceinline__ uint32_t seg_of(const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t p) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)seg[mid] <= p) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------------------------
+// alphabet / '$' census of the sba (sequence_collection.py:694-697)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void alphabet_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                       uint32_t *__restrict__ out) {
+    uint32_t cls_or = 0, dollars = 0;
+    uint64_t nchunk = L / 16;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nchunk;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = reinterpret_cast<const uint4 *>(sba)[i];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                uint32_t c = (w[k] >> (8 * b)) & 0xFF;
+                cls_or |= 1u << c_class[c];
+                dollars += (c == GK_DOLLAR);
+            }
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (uint64_t i = nchunk * 16 + threadIdx.x; i < L; i += blockDim.x) {
+            uint32_t c = sba[i];
+            cls_or |= 1u << c_class[c];
+            dollars += (c == GK_DOLLAR);
+        }
+    }
+    // wave reduce
+    for (int off = 32; off > 0; off >>= 1) {
+        cls_or |= __shfl_xor(cls_or, off);
+        dollars += __shfl_xor(dollars, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicOr(&out[0], cls_or);
+        atomicAdd(&out[1], dollars);
+    }
+}
+
+hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d_flags, 0, 8, c->stream);
+    if (e != hipSuccess) return e;
+    uint64_t chunks = c->sba_len / 16 + 1;
+    int grid = (int)std::min<uint64_t>((chunks + 255) / 256, 2048);
+    hipLaunchKernelGGL(alphabet_kernel, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len, d_flags);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// enumerate (kmers.py:789-835): out[j] = seg[s] + (j - cumk[s])
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enumerate_kernel(const uint32_t *__restrict__ seg,
+                                                        const uint64_t *__restrict__ cumk, uint32_t nseg,
+                                                        uint64_t n, uint32_t *__restrict__ out) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (cumk[mid] <= j) lo = mid; else hi = mid;
+        }
+        out[j] = (uint32_t)(seg[lo] + (j - cumk[lo]));
+    }
+}
+
+hipError_t launch_enumerate(gk_ctx *c, uint32_t min_k, uint32_t *out) {
+    // cumulative k-mer counts per segment, built on the host from the segment table
+    const std::vector<uint32_t> &hseg = c->hseg;
+    hipError_t e;
+    std::vector<uint64_t> cum(c->nseg + 1, 0);
+    for (uint64_t s = 0; s < c->nseg; ++s) {
+        uint64_t end = (s + 1 == c->nseg) ? c->sba_len - 1 : (uint64_t)hseg[s + 1] - 2;
+        cum[s + 1] = cum[s] + (end - hseg[s] + 1 - min_k + 1);
+    }
+    e = ensure(reinterpret_cast<void **>(&c->cumk), &c->cumk_cap, 8 * (c->nseg + 1));
+    if (e != hipSuccess) return e;
+    uint64_t *dcum = c->cumk;
+    e = hipMemcpyAsync(dcum, cum.data(), 8 * (c->nseg + 1), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    int grid = (int)std::min<uint64_t>((c->n + 255) / 256, 8192);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(enumerate_kernel, dim3(grid), dim3(256), 0, c->stream, c->seg, dcum, (uint32_t)c->nseg, c->n,
+                       out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(c->stream);  // cum is a stack buffer
+}
+
+// ---------------------------------------------------------------------------------------------
+// validate user-provided starts: every start needs min_k bases before '$' (kmers.py:1715-1727)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void validate_starts_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                              const uint32_t *__restrict__ starts, uint64_t n,
+                                                              uint32_t min_k, uint32_t *__restrict__ bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t p = starts[i];
+        bool ok = p < L;
+        for (uint32_t t = 0; ok && t < min_k; ++t) ok = (p + t < L) && sba[p + t] != GK_DOLLAR;
+        if (!ok) atomicAdd(bad, 1u);
+    }
+}
+
+hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n, uint32_t min_k, uint32_t *d_bad) {
+    hipError_t e = hipMemsetAsync(d_bad, 0, 4, c->stream);
+    if (e != hipSuccess) return e;
+    int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(validate_starts_kernel, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len, starts, n,
+                       min_k, d_bad);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// key assembly helpers
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ void bi_shl_or(uint64_t (&w)[W], int s, uint64_t v) {
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) w[k] = (w[k] << s) | (w[k + 1] >> (64 - s));
+    w[W - 1] = (w[W - 1] << s) | v;
+}
+
+// key of the window bytes[0 .. symbols-1] (bytes past the pad are '$')
+template <int W, int BITS, bool BOUNDED, typename ByteFn>
+__device__ __forceinline__ void window_key(const KS &ks, ByteFn byte_at, const uint8_t *lut4, uint64_t (&w)[W]) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) w[k] = 0;
+    int len = ks.symbols;
+    bool term = false;
+    for (int t = 0; t < ks.symbols; ++t) {
+        uint32_t ch = byte_at(t);
+        if (BOUNDED && !term && ch == GK_DOLLAR) {
+            term = true;
+            len = t;
+        }
+        uint32_t sym = (BOUNDED && term) ? 0u : sym_code<BITS>(ch, lut4);
+        bi_shl_or<W>(w, BITS, sym);
+    }
+    if (BOUNDED && ks.lenbits > 0) bi_shl_or<W>(w, ks.lenbits, (uint64_t)len);
+}
+
+// ---------------------------------------------------------------------------------------------
+// encode over positions (enumerated starts): fixed length, one word, rolling 2-/4-bit encode
+//   - the tile's sba bytes (+ halo) are staged in LDS with 16-B loads
+//   - thread t rolls over 16 consecutive positions: key = (key << b | code) & mask
+//   - keys are transposed through LDS so the HBM writes are coalesced
+//   - all digit histograms of the radix sort are accumulated in the same pass
+// ---------------------------------------------------------------------------------------------
+constexpr int kRollR = 16;
+constexpr int kRollPitch = 257;  // 256 threads + 1: conflict-free transposed reads
+
+template <int BITS>
+__global__ __launch_bounds__(256) void encode_roll_w1_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                             const uint32_t *__restrict__ seg, uint32_t nseg, KS ks,
+                                                             uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                             uint32_t *__restrict__ ghist) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kEncodeTile + 256];
+    __shared__ uint64_t s_keys[kRollR * kRollPitch];
+    __shared__ uint32_t s_vmask[256];
+    __shared__ uint32_t s_hist[8 * 256];
+    __shared__ uint8_t s_lut4[256];
+    __shared__ uint32_t s_tile_seg, s_tile_has_dollar;
+
+    const int t = threadIdx.x;
+    const int S = ks.symbols;
+    const int D = ks.digits;
+    const uint64_t mask = ks.total_bits >= 64 ? ~0ull : ((1ull << ks.total_bits) - 1);
+    s_lut4[t] = c_code4[t];
+    for (int i = t; i < 8 * 256; i += 256) s_hist[i] = 0;
+
+    const uint64_t ntiles = (L + kEncodeTile - 1) / kEncodeTile;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t P0 = tile * kEncodeTile;
+        __syncthreads();
+        // stage bytes [P0, P0 + 4096 + 256): 16 B per thread + 16 extra chunks
+        {
+            const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0);
+            uint4 *dst = reinterpret_cast<uint4 *>(s_bytes);
+            dst[t] = src[t];
+            if (t < 16) dst[256 + t] = src[256 + t];
+        }
+        if (t == 0) {
+            s_tile_seg = seg_of(seg, nseg, P0);
+            s_tile_has_dollar = 0;
+        }
+        __syncthreads();
+        // any '$' in the staged window? (decides the cheap segment lookup)
+        {
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_bytes);
+            bool d = false;
+            for (int i = t; i < (kEncodeTile + 256) / 4; i += 256) {
+                uint32_t v = w32[i] ^ 0x24242424u;  // zero byte where '$'
+                d |= ((v - 0x01010101u) & ~v & 0x80808080u) != 0;
+            }
+            if (__any(d) && (t & 63) == 0) s_tile_has_dollar = 1;
+        }
+        // rolling encode of positions 16t .. 16t+15
+        {
+            const int q0 = t * kRollR;
+            uint64_t key = 0;
+            int last_dollar = -1000;
+            uint32_t vm = 0;
+            const int steps = S - 1 + kRollR;
+            for (int i = 0; i < steps; ++i) {
+                uint32_t ch = s_bytes[q0 + i];
+                if (ch == GK_DOLLAR) last_dollar = i;
+                key = ((key << BITS) | sym_code<BITS>(ch, s_lut4)) & mask;
+                int j = i - (S - 1);
+                if (j >= 0) {
+                    s_keys[j * kRollPitch + t] = key;
+                    if (last_dollar < j) vm |= 1u << j;
+                }
+            }
+            s_vmask[t] = vm;
+        }
+        __syncthreads();
+        const bool has_dollar = s_tile_has_dollar != 0;
+        const uint32_t tseg = s_tile_seg;
+#pragma unroll 4
+        for (int i = 0; i < kRollR; ++i) {
+            const int q = t + 256 * i;
+            const int owner = q >> 4, j = q & 15;
+            const uint64_t p = P0 + q;
+            if (((s_vmask[owner] >> j) & 1u) && p < L) {
+                uint64_t key = s_keys[j * kRollPitch + owner];
+                uint32_t s = has_dollar ? seg_of(seg, nseg, p) : tseg;
+                uint64_t o = p - (uint64_t)ks.min_len * s;
+                keys[o] = key;
+                vals[o] = (uint32_t)p;
+                for (int d = 0; d < D; ++d) atomicAdd(&s_hist[d * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < D * 256; i += 256) {
+        uint32_t v = s_hist[i];
+        if (v) atomicAdd(&ghist[i], v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// generic encode over positions: any width W, bounded (padded) keys; one key per thread from LDS
+// ---------------------------------------------------------------------------------------------
+template <int W, int BITS, bool BOUNDED>
+__global__ __launch_bounds__(256) void encode_generic_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                             const uint32_t *__restrict__ seg, uint32_t nseg, KS ks,
+                                                             uint64_t n, uint64_t *__restrict__ keys,
+                                                             uint32_t *__restrict__ vals, uint32_t *__restrict__ ghist) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kEncodeTile + 512];
+    __shared__ uint32_t s_hist[kMaxWords * 8 * 256];
+    __shared__ uint8_t s_lut4[256];
+    const int t = threadIdx.x;
+    const int D = ks.digits;
+    s_lut4[t] = c_code4[t];
+    for (int i = t; i < D * 256; i += 256) s_hist[i] = 0;
+    const uint64_t ntiles = (L + kEncodeTile - 1) / kEncodeTile;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t P0 = tile * kEncodeTile;
+        __syncthreads();
+        {
+            const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0);
+            uint4 *dst = reinterpret_cast<uint4 *>(s_bytes);
+            dst[t] = src[t];
+            if (t < 32) dst[256 + t] = src[256 + t];
+        }
+        __syncthreads();
+        for (int i = 0; i < kEncodeTile / 256; ++i) {
+            const int q = t + 256 * i;
+            const uint64_t p = P0 + q;
+            if (p >= L) break;
+            bool valid = true;
+            for (int k = 0; k < ks.min_len; ++k) valid &= s_bytes[q + k] != GK_DOLLAR;
+            if (!valid) continue;
+            uint64_t w[W];
+            window_key<W, BITS, BOUNDED>(ks, [&](int k) { return (uint32_t)s_bytes[q + k]; }, s_lut4, w);
+            uint32_t s = seg_of(seg, nseg, p);
+            uint64_t o = p - (uint64_t)ks.min_len * s;
+#pragma unroll
+            for (int k = 0; k < W; ++k) keys[(uint64_t)k * n + o] = w[k];
+            vals[o] = (uint32_t)p;
+            for (int d = 0; d < D; ++d) {
+                int word = W - 1 - (d >> 3);
+                atomicAdd(&s_hist[d * 256 + ((w[word] >> (8 * (d & 7))) & 0xFF)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < D * 256; i += 256) {
+        uint32_t v = s_hist[i];
+        if (v) atomicAdd(&ghist[i], v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// gather encode: keys of arbitrary starts (user-provided or re-sorted arrays)
+// ---------------------------------------------------------------------------------------------
+template <int W, int BITS, bool BOUNDED>
+__global__ __launch_bounds__(256) void encode_gather_kernel(const uint8_t *__restrict__ sba, KS ks,
+                                                            const uint32_t *__restrict__ starts, uint64_t n,
+                                                            uint64_t *__restrict__ keys) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t *b = sba + starts[i];
+        uint64_t w[W];
+        window_key<W, BITS, BOUNDED>(ks, [&](int k) { return (uint32_t)b[k]; }, s_lut4, w);
+#pragma unroll
+        for (int k = 0; k < W; ++k) keys[(uint64_t)k * n + i] = w[k];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------------------------
+template <int W, int BITS, bool BOUNDED>
+static hipError_t dispatch_generic(gk_ctx *c, const KS &k, uint64_t *keys, uint32_t *vals, uint32_t *hist, int grid) {
+    hipLaunchKernelGGL((encode_generic_kernel<W, BITS, BOUNDED>), dim3(grid), dim3(256), 0, c->stream, c->sba,
+                       c->sba_len, c->seg, (uint32_t)c->nseg, k, c->n, keys, vals, hist);
+    return hipGetLastError();
+}
+
+template <int BITS, bool BOUNDED>
+static hipError_t dispatch_generic_w(gk_ctx *c, const KS &k, uint64_t *keys, uint32_t *vals, uint32_t *hist, int grid) {
+    switch (k.words) {
+    case 1: return dispatch_generic<1, BITS, BOUNDED>(c, k, keys, vals, hist, grid);
+    case 2: return dispatch_generic<2, BITS, BOUNDED>(c, k, keys, vals, hist, grid);
+    case 3: return dispatch_generic<3, BITS, BOUNDED>(c, k, keys, vals, hist, grid);
+    case 4: return dispatch_generic<4, BITS, BOUNDED>(c, k, keys, vals, hist, grid);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    KS k = pod(ks);
+    e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * k.digits, c->stream);
+    if (e != hipSuccess) return e;
+    const uint64_t ntiles = (c->sba_len + kEncodeTile - 1) / kEncodeTile;
+    int grid = (int)std::min<uint64_t>(ntiles, 256 * 6);
+    if (grid < 1) grid = 1;
+    const bool bounded = ks.symbols != ks.min_len;
+    if (!bounded && ks.words == 1 && (ks.bits == 2 || ks.bits == 4) && ks.symbols <= 64) {
+        if (ks.bits == 2)
+            hipLaunchKernelGGL(encode_roll_w1_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
+                               c->seg, (uint32_t)c->nseg, k, keys, vals, hist);
+        else
+            hipLaunchKernelGGL(encode_roll_w1_kernel<4>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
+                               c->seg, (uint32_t)c->nseg, k, keys, vals, hist);
+        return hipGetLastError();
+    }
+    if (ks.bits == 2) return bounded ? dispatch_generic_w<2, true>(c, k, keys, vals, hist, grid)
+                                     : dispatch_generic_w<2, false>(c, k, keys, vals, hist, grid);
+    if (ks.bits == 3) return dispatch_generic_w<3, true>(c, k, keys, vals, hist, grid);
+    return bounded ? dispatch_generic_w<4, true>(c, k, keys, vals, hist, grid)
+                   : dispatch_generic_w<4, false>(c, k, keys, vals, hist, grid);
+}
+
+template <int W, int BITS, bool BOUNDED>
+static hipError_t gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys) {
+    int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((encode_gather_kernel<W, BITS, BOUNDED>), dim3(grid), dim3(256), 0, c->stream, c->sba, k,
+                       starts, n, keys);
+    return hipGetLastError();
+}
+
+template <int BITS, bool BOUNDED>
+static hipError_t gather_dispatch(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys) {
+    switch (k.words) {
+    case 1: return gather_w<1, BITS, BOUNDED>(c, k, starts, n, keys);
+    case 2: return gather_w<2, BITS, BOUNDED>(c, k, starts, n, keys);
+    case 3: return gather_w<3, BITS, BOUNDED>(c, k, starts, n, keys);
+    case 4: return gather_w<4, BITS, BOUNDED>(c, k, starts, n, keys);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    KS k = pod(ks);
+    const bool bounded = ks.symbols != ks.min_len;
+    if (ks.bits == 2) return bounded ? gather_dispatch<2, true>(c, k, starts, n, keys)
+                                     : gather_dispatch<2, false>(c, k, starts, n, keys);
+    if (ks.bits == 3) return gather_dispatch<3, true>(c, k, starts, n, keys);
+    return bounded ? gather_dispatch<4, true>(c, k, starts, n, keys) : gather_dispatch<4, false>(c, k, starts, n, keys);
+}
+
+}  // namespace gkm

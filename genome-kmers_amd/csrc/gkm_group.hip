@@ -1,0 +1,643 @@
+// gkm_group.hip -- group pass over the sorted k-mers (gfx950): filters, group boundaries,
+// group-size histogram, generator members, unique k-mers + multiplicities.
+//
+// Restates kmer_info_by_group_generator (kmers.py:523-648) as data-parallel steps:
+//   1. valid[i]   = kmer_filter_func(sba, strand, starts[i])          (filters: kmers.py:14-259)
+//   2. cidx       = indices of valid k-mers, in order                  (stream compaction)
+//   3. head[q]    = q == 0 || compare(prev valid, this, kmer_len) != 0  (kmers.py:597-601)
+//   4. gstart     = indices of heads; size[g] = gstart[g+1] - gstart[g]
+//   5. hist[min(size, max_bin)] += 1, total += size for min <= size <= max  (kmers.py:454-520)
+// A generator "yield" is one of the first yield_first_n members of a qualifying group.
+#include <algorithm>
+
+#include "gkm_internal.h"
+
+namespace gkm {
+
+// ---------------------------------------------------------------------------------------------
+// block scan helpers
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp, uint32_t *block_total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const uint32_t x = s_tmp[w];
+        pre += (w < wave) ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    *block_total = tot;
+    return pre + incl - v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// scans over u8 flags and u32 values; tile = 256 threads x 16 consecutive elements
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void load16_flags(const uint8_t *__restrict__ f, uint64_t n, uint64_t at, uint8_t (&v)[16]) {
+    if (at + 16 <= n) {
+        uint4 x = *reinterpret_cast<const uint4 *>(f + at);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = (at + k < n) ? f[at + k] : 0;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void flag_count_kernel(const uint8_t *__restrict__ f, uint64_t n,
+                                                                  uint32_t *__restrict__ tile_sums) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint8_t v[16];
+    load16_flags(f, n, at, v);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
+    uint32_t tot;
+    block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanThreads) void u32_count_kernel(const uint32_t *__restrict__ in, uint64_t n,
+                                                                 uint32_t *__restrict__ tile_sums) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint32_t cnt = 0;
+    for (int k = 0; k < 16; ++k)
+        if (at + k < n) cnt += in[at + k];
+    uint32_t tot;
+    block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+// exclusive scan of the tile sums in place (one 1024-thread block); grand total -> *total
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint32_t *__restrict__ sums, uint64_t ntiles,
+                                                          uint64_t *__restrict__ total) {
+    __shared__ uint32_t s_tmp[16];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += 1024) {
+        const uint64_t i = b + threadIdx.x;
+        const uint32_t v = i < ntiles ? sums[i] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<1024>(v, s_tmp, &tot);
+        if (i < ntiles) sums[i] = (uint32_t)(carry + ex);
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(kScanThreads) void flag_select_kernel(const uint8_t *__restrict__ f, uint64_t n,
+                                                                   const uint32_t *__restrict__ tile_off,
+                                                                   uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint8_t v[16];
+    load16_flags(f, n, at, v);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
+    uint32_t tot;
+    uint32_t o = tile_off[blockIdx.x] + block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (v[k]) out[o++] = (uint32_t)(at + k);
+}
+
+__global__ __launch_bounds__(kScanThreads) void flag_scan_incl_kernel(const uint8_t *__restrict__ f, uint64_t n,
+                                                                      const uint32_t *__restrict__ tile_off,
+                                                                      uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint8_t v[16];
+    load16_flags(f, n, at, v);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
+    uint32_t tot;
+    uint32_t o = tile_off[blockIdx.x] + block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        o += v[k] != 0;
+        if (at + k < n) out[at + k] = o;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void u32_scan_apply_kernel(const uint32_t *__restrict__ in, uint64_t n,
+                                                                      const uint32_t *__restrict__ tile_off,
+                                                                      uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint32_t v[16];
+    uint32_t cnt = 0;
+    for (int k = 0; k < 16; ++k) {
+        v[k] = (at + k < n) ? in[at + k] : 0;
+        cnt += v[k];
+    }
+    uint32_t tot;
+    uint32_t o = tile_off[blockIdx.x] + block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+    for (int k = 0; k < 16; ++k) {
+        if (at + k < n) out[at + k] = o;
+        o += v[k];
+    }
+}
+
+static hipError_t ensure_tile_sums(gk_ctx *c, uint64_t ntiles) {
+    return ensure(reinterpret_cast<void **>(&c->tile_sums), &c->tile_sums_cap, 4 * (ntiles + 16));
+}
+
+static hipError_t read_total(gk_ctx *c, uint64_t *count) {
+    hipError_t e = hipMemcpyAsync(count, c->scalars, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(c->stream);
+}
+
+hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count) {
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    if (n == 0) { *count = 0; return hipSuccess; }
+    hipError_t e = ensure_tile_sums(c, ntiles);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(flag_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    hipLaunchKernelGGL(flag_select_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums, out_idx);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return read_total(c, count);
+}
+
+hipError_t scan_flags_inclusive(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out) {
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    if (n == 0) return hipSuccess;
+    hipError_t e = ensure_tile_sums(c, ntiles);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(flag_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    hipLaunchKernelGGL(flag_scan_incl_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums, out);
+    return hipGetLastError();
+}
+
+static hipError_t scan_u32_exclusive(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    if (n == 0) { *total = 0; return hipSuccess; }
+    hipError_t e = ensure_tile_sums(c, ntiles);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(u32_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
+                       c->tile_sums);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    hipLaunchKernelGGL(u32_scan_apply_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
+                       c->tile_sums, out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return read_total(c, total);
+}
+
+// ---------------------------------------------------------------------------------------------
+// built-in filters on the device (kmers.py:14-259); returns 1 pass, 0 fail, -code raised
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int dev_filter(const uint8_t *__restrict__ sba, uint64_t L, int kind, int64_t p0,
+                                          int64_t p1, int64_t p2, uint64_t idx, const uint8_t *__restrict__ mask,
+                                          uint64_t i) {
+    switch (kind) {
+    case GK_FILTER_KEEP_ALL:
+        return 1;
+    case GK_FILTER_LENGTH:  // kmer_has_required_len (kmers.py:262-282)
+        for (int64_t t = 0; t < p0; ++t)
+            if (idx + t >= L || sba[idx + t] == GK_DOLLAR) return 0;
+        return 1;
+    case GK_FILTER_HOMOPOLYMER: {  // kmers.py:63-98
+        const int64_t maxh = p0, k = p1;
+        if ((int64_t)idx + k - 1 >= (int64_t)L) return -GK_FERR_HOMO_LEN;
+        if (k < maxh) return 1;
+        int64_t h = 1;
+        for (int64_t t = 1; t < k; ++t) {
+            const uint8_t b = sba[idx + t], pb = sba[idx + t - 1];
+            if (b == GK_DOLLAR) return -GK_FERR_HOMO_LEN;
+            if (b == pb) {
+                if (++h > maxh) return 0;
+            } else {
+                h = 1;
+            }
+        }
+        return 1;
+    }
+    case GK_FILTER_GC: {  // kmers.py:150-190
+        const int64_t minc = p0, maxc = p1, k = p2;
+        if (maxc < minc) return 0;
+        int64_t gc = 0;
+        for (int64_t t = 0; t < k; ++t) {
+            if (idx + t >= L) return -GK_FERR_GC_OOB;
+            const uint8_t b = sba[idx + t];
+            if (b == GK_DOLLAR) return -GK_FERR_GC_LEN;
+            if (b == 'G' || b == 'C') {
+                if (++gc > maxc) return 0;
+            }
+        }
+        return (minc <= gc && gc <= maxc) ? 1 : 0;
+    }
+    case GK_FILTER_NO_AMBIGUOUS: {  // kmers.py:209-227
+        const int64_t k = p0;
+        if ((int64_t)idx + k > (int64_t)L) return -GK_FERR_AMBIG_LEN;
+        for (int64_t t = 0; t < k; ++t) {
+            const uint8_t b = sba[idx + t];
+            if (b == GK_DOLLAR) return -GK_FERR_AMBIG_SEG;
+            if (b != 'A' && b != 'T' && b != 'G' && b != 'C') return 0;
+        }
+        return 1;
+    }
+    case GK_FILTER_CRISPR_NGG:  // kmers.py:232-259
+        if (idx + 23 > L) return -GK_FERR_CRISPR_LEN;
+        return (sba[idx + 21] == 'G' && sba[idx + 22] == 'G') ? 1 : 0;
+    case GK_FILTER_MASK:
+        return mask[i] ? 1 : 0;
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(256) void filter_flags_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                           const uint32_t *__restrict__ starts, uint64_t n, int kind,
+                                                           int64_t p0, int64_t p1, int64_t p2,
+                                                           const uint8_t *__restrict__ mask, uint8_t *__restrict__ flags,
+                                                           unsigned long long *__restrict__ err) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int r = dev_filter(sba, L, kind, p0, p1, p2, starts[i], mask, i);
+        flags[i] = r > 0;
+        if (r < 0) atomicMin(err, ((unsigned long long)i << 8) | (unsigned long long)(-r));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// group heads: q == 0 || k-mer(q-1) != k-mer(q) under compare_sba_kmers_lexicographically(kmer_len)
+// ---------------------------------------------------------------------------------------------
+struct KeyMasks {
+    uint64_t m[kMaxWords];
+};
+
+// byte compare (kmers.py:306-397); returns true if equal; kmer_len < 0 = None
+__device__ __forceinline__ bool sba_equal(const uint8_t *__restrict__ sba, uint64_t a, uint64_t b, int64_t kmer_len) {
+    for (int64_t t = 0;; ++t) {
+        const uint8_t x = sba[a + t], y = sba[b + t];  // pad after L reads '$'
+        const bool oa = x == GK_DOLLAR, ob = y == GK_DOLLAR;
+        if (oa || ob) return oa && ob;
+        if (x != y) return false;
+        if (kmer_len >= 0 && t == kmer_len - 1) return true;
+    }
+}
+
+template <int MODE, int W>  // MODE 0: masked key compare, 1: sba byte compare
+__global__ __launch_bounds__(256) void head_flags_kernel(const uint8_t *__restrict__ sba,
+                                                         const uint32_t *__restrict__ starts,
+                                                         const uint64_t *__restrict__ keys, uint64_t nkeys,
+                                                         const uint32_t *__restrict__ cidx, uint64_t count,
+                                                         int64_t kmer_len, KeyMasks km, uint8_t *__restrict__ head) {
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < count;
+         q += (uint64_t)gridDim.x * blockDim.x) {
+        if (q == 0) {
+            head[q] = 1;
+            continue;
+        }
+        const uint64_t i = cidx ? cidx[q] : q;
+        const uint64_t h = cidx ? cidx[q - 1] : q - 1;
+        bool eq;
+        if (MODE == 0) {
+            eq = true;
+#pragma unroll
+            for (int w = 0; w < W; ++w) eq &= ((keys[(uint64_t)w * nkeys + i] ^ keys[(uint64_t)w * nkeys + h]) & km.m[w]) == 0;
+        } else {
+            eq = sba_equal(sba, starts[h], starts[i], kmer_len);
+        }
+        head[q] = !eq;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// group sizes -> histogram / totals / generator members
+// ---------------------------------------------------------------------------------------------
+constexpr int kLdsBins = 2048;
+
+__device__ __forceinline__ uint64_t group_size(const uint32_t *__restrict__ gstart, uint64_t G, uint64_t count,
+                                               uint64_t g) {
+    return (g + 1 < G ? (uint64_t)gstart[g + 1] : count) - gstart[g];
+}
+
+__global__ __launch_bounds__(256) void group_hist_kernel(const uint32_t *__restrict__ gstart, uint64_t G,
+                                                         uint64_t count, int64_t min_g, int64_t max_g, int64_t max_bin,
+                                                         unsigned long long *__restrict__ hist,
+                                                         unsigned long long *__restrict__ total) {
+    __shared__ uint32_t s_hist[kLdsBins];
+    __shared__ unsigned long long s_total;
+    const int64_t lds_bins = max_bin + 1 < kLdsBins ? max_bin + 1 : kLdsBins;
+    for (int i = threadIdx.x; i < lds_bins; i += 256) s_hist[i] = 0;
+    if (threadIdx.x == 0) s_total = 0;
+    __syncthreads();
+    unsigned long long my_total = 0;
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t size = (int64_t)group_size(gstart, G, count, g);
+        if (size < min_g || (max_g >= 0 && size > max_g)) continue;
+        const int64_t bin = size < max_bin ? size : max_bin;
+        if (bin < lds_bins) atomicAdd(&s_hist[bin], 1u);
+        else atomicAdd(&hist[bin], 1ull);
+        my_total += (unsigned long long)size;
+    }
+    for (int off = 32; off > 0; off >>= 1) my_total += __shfl_xor(my_total, off);
+    if ((threadIdx.x & 63) == 0 && my_total) atomicAdd(&s_total, my_total);
+    __syncthreads();
+    for (int i = threadIdx.x; i < lds_bins; i += 256)
+        if (s_hist[i]) atomicAdd(&hist[i], (unsigned long long)s_hist[i]);
+    if (threadIdx.x == 0 && s_total) atomicAdd(total, s_total);
+}
+
+__global__ __launch_bounds__(256) void group_yield_count_kernel(const uint32_t *__restrict__ gstart, uint64_t G,
+                                                                uint64_t count, int64_t min_g, int64_t max_g,
+                                                                int64_t yfn, uint32_t *__restrict__ m) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t size = (int64_t)group_size(gstart, G, count, g);
+        const bool ok = size >= min_g && (max_g < 0 || size <= max_g);
+        m[g] = ok ? (uint32_t)(yfn < 0 ? size : (size < yfn ? size : yfn)) : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void group_yield_write_kernel(const uint32_t *__restrict__ gstart, uint64_t G,
+                                                                uint64_t count, const uint32_t *__restrict__ m,
+                                                                const uint32_t *__restrict__ off,
+                                                                const uint32_t *__restrict__ cidx,
+                                                                uint64_t *__restrict__ out_num,
+                                                                uint32_t *__restrict__ out_y,
+                                                                uint32_t *__restrict__ out_t) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t mg = m[g];
+        if (!mg) continue;
+        const uint32_t size = (uint32_t)group_size(gstart, G, count, g);
+        const uint64_t o = off[g];
+        for (uint32_t r = 0; r < mg; ++r) {
+            const uint64_t q = (uint64_t)gstart[g] + r;
+            out_num[o + r] = cidx ? cidx[q] : q;
+            out_y[o + r] = mg;
+            out_t[o + r] = size;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void unique_counts_kernel(const uint32_t *__restrict__ gstart, uint64_t G,
+                                                            uint64_t count, uint32_t *__restrict__ counts) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x)
+        counts[g] = (uint32_t)group_size(gstart, G, count, g);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host drivers
+// ---------------------------------------------------------------------------------------------
+static int grid_for(uint64_t n, int cap = 8192) {
+    uint64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    return (int)std::min<uint64_t>(g, (uint64_t)cap);
+}
+
+}  // namespace gkm
+
+using namespace gkm;
+
+// Shared front half of gk_group_hist / gk_group_members: filter, compact, heads, group starts.
+// On success: *cidx_out (nullptr = identity), *count (valid k-mers), *G, group starts in c->idx_b.
+static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filter *filter, const uint32_t **cidx_out,
+                       uint64_t *count, uint64_t *G, int32_t *err_code, uint64_t *err_idx) {
+    if (err_code) *err_code = 0;
+    if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
+    if (int rc = materialize_starts(c)) return rc;
+    const uint64_t n = c->n;
+    const uint32_t *starts = c->vals[c->cur];
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->flags), &c->flags_cap, n + 64));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_a), &c->idx_cap, 4 * (n + 64)));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_b), &c->idx_b_cap, 4 * (n + 64)));
+    const int kind = filter ? filter->kind : GK_FILTER_KEEP_ALL;
+    if (kind == GK_FILTER_MASK && c->mask_n != n) return fail(c, GK_E_ARG, "filter mask length differs from the k-mer count");
+    if (kind < 0 || kind > GK_FILTER_MASK) return fail(c, GK_E_ARG, "unknown filter kind");
+
+    // 1-2. filter + compaction
+    const uint32_t *cidx = nullptr;
+    uint64_t cnt = n;
+    if (kind != GK_FILTER_KEEP_ALL) {
+        unsigned long long init = ~0ull;
+        GK_TRY_HIP(c, hipMemcpyAsync(c->scalars + 1, &init, 8, hipMemcpyHostToDevice, c->stream));
+        int slot;
+        timer_begin(c, "filter", &slot);
+        hipLaunchKernelGGL(filter_flags_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, c->sba, c->sba_len, starts,
+                           n, kind, filter->p0, filter->p1, filter->p2, c->mask, c->flags,
+                           reinterpret_cast<unsigned long long *>(c->scalars + 1));
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        unsigned long long err = 0;
+        GK_TRY_HIP(c, hipMemcpyAsync(&err, c->scalars + 1, 8, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        if (err != ~0ull) {
+            const uint64_t i = err >> 8;
+            uint32_t s = 0;
+            GK_TRY_HIP(c, hipMemcpy(&s, starts + i, 4, hipMemcpyDeviceToHost));
+            if (err_code) *err_code = (int32_t)(err & 0xFF);
+            if (err_idx) *err_idx = s;
+            return fail(c, GK_E_FILTER, "k-mer filter raised");
+        }
+        GK_TRY_HIP(c, select_flags(c, c->flags, n, c->idx_a, &cnt));
+        cidx = c->idx_a;
+    }
+    *cidx_out = cidx;
+    *count = cnt;
+    if (cnt == 0) {
+        *G = 0;
+        return GK_OK;
+    }
+
+    // 3. heads
+    if (!is_sorted) {
+        // compare_sba_kmers_always_less_than: every valid k-mer starts a group (kmers.py:295-303, 957-960)
+        GK_TRY_HIP(c, hipMemsetAsync(c->flags, 1, cnt, c->stream));
+    } else {
+        // decide whether the encoded keys decide equality at kmer_len
+        const KeySpec &ks = c->spec;
+        bool use_keys = false;
+        KeyMasks km{};
+        if (c->keys_valid && !c->keys_are_ranks && kmer_len >= 1 && kmer_len <= ks.symbols &&
+            (ks.lenbits == 0 || kmer_len == ks.symbols)) {
+            // compare the top kmer_len symbols (plus the length field when it is the full key)
+            const int top = ks.total_bits;
+            const int lowest = (kmer_len == ks.symbols) ? 0 : (top - (int)kmer_len * ks.bits);
+            for (int w = 0; w < ks.words; ++w) {
+                const int lo = (ks.words - 1 - w) * 64;  // bit index of word w's bit 0
+                uint64_t m = 0;
+                for (int b = 0; b < 64; ++b) {
+                    const int bit = lo + b;
+                    if (bit >= lowest && bit < top) m |= 1ull << b;
+                }
+                km.m[w] = m;
+            }
+            use_keys = true;
+        } else if (c->keys_valid && c->keys_are_ranks && ((kmer_len < 0 && c->sort_len == 0) ||
+                                                          (kmer_len >= 0 && (uint64_t)kmer_len == c->sort_len))) {
+            for (int w = 0; w < ks.words; ++w) km.m[w] = ~0ull;
+            use_keys = true;
+        }
+        int slot;
+        timer_begin(c, "group_heads", &slot);
+        const uint64_t *keys = c->keys[c->cur];
+        if (use_keys) {
+            switch (ks.words) {
+            case 1: hipLaunchKernelGGL((head_flags_kernel<0, 1>), dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->sba, starts, keys, n, cidx, cnt, kmer_len, km, c->flags); break;
+            case 2: hipLaunchKernelGGL((head_flags_kernel<0, 2>), dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->sba, starts, keys, n, cidx, cnt, kmer_len, km, c->flags); break;
+            case 3: hipLaunchKernelGGL((head_flags_kernel<0, 3>), dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->sba, starts, keys, n, cidx, cnt, kmer_len, km, c->flags); break;
+            default: hipLaunchKernelGGL((head_flags_kernel<0, 4>), dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->sba, starts, keys, n, cidx, cnt, kmer_len, km, c->flags); break;
+            }
+        } else {
+            hipLaunchKernelGGL((head_flags_kernel<1, 1>), dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->sba, starts,
+                               keys, n, cidx, cnt, kmer_len, km, c->flags);
+        }
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+    }
+    // 4. group starts
+    uint64_t g = 0;
+    GK_TRY_HIP(c, select_flags(c, c->flags, cnt, c->idx_b, &g));
+    *G = g;
+    return GK_OK;
+}
+
+extern "C" int gk_group_hist(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filter *filter,
+                             int64_t min_group_size, int64_t max_group_size, int64_t max_counts_bin, int64_t *hist,
+                             int64_t *total, int32_t *err_code, uint64_t *err_idx) {
+    if (!c) return GK_E_ARG;
+    if (max_counts_bin <= 0) return fail(c, GK_E_ARG, "max_counts_bin must be >= 1");
+    if (min_group_size < 1) return fail(c, GK_E_ARG, "min_group_size must be >= 1");
+    const uint32_t *cidx;
+    uint64_t count, G;
+    int rc = group_front(c, is_sorted, kmer_len, filter, &cidx, &count, &G, err_code, err_idx);
+    if (rc != GK_OK) return rc;
+    const uint64_t bins = (uint64_t)max_counts_bin + 1;
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->dhist), &c->dhist_cap, 8 * bins));
+    GK_TRY_HIP(c, hipMemsetAsync(c->dhist, 0, 8 * bins, c->stream));
+    GK_TRY_HIP(c, hipMemsetAsync(c->scalars + 2, 0, 8, c->stream));
+    if (G > 0) {
+        int slot;
+        timer_begin(c, "group_hist", &slot);
+        hipLaunchKernelGGL(group_hist_kernel, dim3(grid_for(G, 4096)), dim3(256), 0, c->stream, c->idx_b, G, count,
+                           min_group_size, max_group_size, max_counts_bin,
+                           reinterpret_cast<unsigned long long *>(c->dhist),
+                           reinterpret_cast<unsigned long long *>(c->scalars + 2));
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+    }
+    if (hist) GK_TRY_HIP(c, hipMemcpyAsync(hist, c->dhist, 8 * bins, hipMemcpyDeviceToHost, c->stream));
+    uint64_t tot = 0;
+    GK_TRY_HIP(c, hipMemcpyAsync(&tot, c->scalars + 2, 8, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    if (total) *total = (int64_t)tot;
+    return GK_OK;
+}
+
+extern "C" int gk_group_members(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filter *filter,
+                                int64_t min_group_size, int64_t max_group_size, int64_t yield_first_n,
+                                uint64_t *kmer_num, uint32_t *size_yielded, uint32_t *size_total, uint64_t capacity,
+                                uint64_t *n_out, int32_t *err_code, uint64_t *err_idx) {
+    if (!c) return GK_E_ARG;
+    if (min_group_size < 1) return fail(c, GK_E_ARG, "min_group_size must be >= 1");
+    const uint32_t *cidx;
+    uint64_t count, G;
+    int rc = group_front(c, is_sorted, kmer_len, filter, &cidx, &count, &G, err_code, err_idx);
+    if (rc != GK_OK) return rc;
+    if (G == 0) {
+        if (n_out) *n_out = 0;
+        return GK_OK;
+    }
+    // per-group yield counts (into flags-sized scratch reinterpreted as u32) and their offsets
+    uint32_t *m = nullptr, *off = nullptr;
+    uint64_t *onum = nullptr;
+    uint32_t *oy = nullptr, *ot = nullptr;
+    GK_TRY_HIP(c, hipMallocAsync(reinterpret_cast<void **>(&m), 4 * (G + 16), c->stream));
+    GK_TRY_HIP(c, hipMallocAsync(reinterpret_cast<void **>(&off), 4 * (G + 16), c->stream));
+    hipLaunchKernelGGL(group_yield_count_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, count,
+                       min_group_size, max_group_size, yield_first_n, m);
+    GK_TRY_HIP(c, hipGetLastError());
+    uint64_t M = 0;
+    hipError_t e = scan_u32_exclusive(c, m, G, off, &M);
+    if (e == hipSuccess && kmer_num && M > 0) {
+        if (capacity < M) {
+            hipFreeAsync(m, c->stream);
+            hipFreeAsync(off, c->stream);
+            return fail(c, GK_E_ARG, "capacity smaller than the number of yields");
+        }
+        e = hipMallocAsync(reinterpret_cast<void **>(&onum), 8 * M, c->stream);
+        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&oy), 4 * M, c->stream);
+        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&ot), 4 * M, c->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(group_yield_write_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, count,
+                               m, off, cidx, onum, oy, ot);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(kmer_num, onum, 8 * M, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess && size_yielded) e = hipMemcpyAsync(size_yielded, oy, 4 * M, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess && size_total) e = hipMemcpyAsync(size_total, ot, 4 * M, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    if (onum) hipFreeAsync(onum, c->stream);
+    if (oy) hipFreeAsync(oy, c->stream);
+    if (ot) hipFreeAsync(ot, c->stream);
+    hipFreeAsync(m, c->stream);
+    hipFreeAsync(off, c->stream);
+    GK_TRY_HIP(c, e);
+    if (n_out) *n_out = M;
+    return GK_OK;
+}
+
+extern "C" int gk_unique_counts(gk_ctx *c, uint64_t *n_unique) {
+    if (!c) return GK_E_ARG;
+    if (!c->sorted || !c->keys_valid) return fail(c, GK_E_STATE, "unique counts need a sorted k-mer set");
+    const uint32_t *cidx;
+    uint64_t count, G;
+    const int64_t kl = c->sort_len == 0 ? -1 : (int64_t)c->sort_len;
+    int rc = group_front(c, 1, kl, nullptr, &cidx, &count, &G, nullptr, nullptr);
+    if (rc != GK_OK) return rc;
+    c->n_unique = G;
+    c->unique_valid = true;
+    if (n_unique) *n_unique = G;
+    return GK_OK;
+}
+
+extern "C" int gk_copy_unique(gk_ctx *c, uint64_t *group_start, uint32_t *count, uint64_t n) {
+    if (!c) return GK_E_ARG;
+    if (!c->unique_valid) return fail(c, GK_E_STATE, "call gk_unique_counts first");
+    if (n != c->n_unique) return fail(c, GK_E_ARG, "n differs from the unique k-mer count");
+    if (n == 0) return GK_OK;
+    uint32_t *cnt = c->idx_a;  // idx_a is free after an unfiltered group_front
+    hipLaunchKernelGGL(unique_counts_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, c->idx_b, n, c->n, cnt);
+    GK_TRY_HIP(c, hipGetLastError());
+    if (count) GK_TRY_HIP(c, hipMemcpyAsync(count, cnt, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (group_start) {
+        std::vector<uint32_t> tmp(n);
+        GK_TRY_HIP(c, hipMemcpyAsync(tmp.data(), c->idx_b, 4 * n, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint64_t i = 0; i < n; ++i) group_start[i] = tmp[i];
+    }
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
+namespace gkm {
+// device-side unique counts for the bench step (no host copy): counts into idx_a
+hipError_t unique_counts_device(gk_ctx *c) {
+    if (c->n_unique == 0) return hipSuccess;
+    hipLaunchKernelGGL(unique_counts_kernel, dim3(grid_for(c->n_unique)), dim3(256), 0, c->stream, c->idx_b,
+                       c->n_unique, c->n, c->idx_a);
+    return hipGetLastError();
+}
+}  // namespace gkm

@@ -1,0 +1,165 @@
+// gkm_internal.h -- shared declarations of the libgkm HIP engine (gfx950 / CDNA4 only).
+//
+// Data layout in HBM:
+//   sba      uint8[L + pad]     ASCII bases, '$'-joined contigs; the pad after L is '$' so every
+//                               window read is in bounds and an out-of-array byte reads as '$'.
+//   seg      uint32[nseg]       contig start offsets (SequenceCollection._forward_sba_seg_starts)
+//   vals[2]  uint32[n]          start indices (ping-pong buffers of the radix sort)
+//   keys[2]  uint64[W][n]       encoded k-mers, structure-of-arrays, word 0 most significant
+//   status   uint64[tiles*256]  decoupled look-back state of the radix passes (epoch-tagged)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "gkm.h"
+
+#define GK_DOLLAR 36
+
+namespace gkm {
+
+constexpr int kRadixBits = 8;
+constexpr int kRadixBins = 256;
+constexpr int kMaxWords = 4;          // direct keys up to 256 bits
+constexpr int kEncodeTile = 4096;     // positions per encode tile
+constexpr int kSbaPad = 8192;         // '$' bytes after the sba (>= tile + max symbols)
+constexpr int kSortThreads = 256;     // radix pass workgroup
+constexpr int kSortItems = 16;        // keys per thread per radix tile
+constexpr int kSortTile = kSortThreads * kSortItems;
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+// How a k-mer is turned into an order-preserving integer key:
+//   bits   2: A,C,G,T -> 0..3 (sba holds only ACGT)
+//          3: '$'/end -> 0, A,C,G,T -> 1..4 (doubling seeds on ACGT data)
+//          4: '$'/end -> 0, A B C D G H K M N R S T V W Y -> 1..15 (IUPAC data)
+//   symbols  number of leading symbols encoded (= max_kmer_len for direct keys)
+//   lenbits  2-bit keys of variable length append min(len, symbols) in the low lenbits bits
+struct KeySpec {
+    int bits;
+    int symbols;
+    int lenbits;
+    int min_len;      // validity: a start needs min_len bases before '$'
+    int words;        // W
+    int total_bits;
+    int digits() const { return (total_bits + kRadixBits - 1) / kRadixBits; }
+};
+
+struct Timer {
+    std::string name;
+    hipEvent_t start, stop;
+};
+
+}  // namespace gkm
+
+struct gk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // input
+    uint8_t *sba = nullptr;
+    uint64_t sba_len = 0, sba_cap = 0;
+    uint32_t *seg = nullptr;
+    uint64_t nseg = 0, seg_cap = 0;
+    uint64_t max_seg_len = 0;
+    int acgt = 1;
+
+    // k-mers
+    uint64_t n = 0;
+    uint32_t min_k = 0;
+    bool have_starts = false;
+    bool enumerated = false;   // vals == canonical enumerate output (ascending)
+    bool starts_materialized = true;  // false: enumerated starts not yet written to vals[cur]
+    bool sorted = false;
+    uint32_t sort_len = 0;     // max_kmer_len of the last sort (0 = None)
+    bool keys_valid = false;   // keys[cur] encode the k-mers of vals[cur] (sort order)
+    bool keys_are_ranks = false;
+    gkm::KeySpec spec{};
+
+    uint32_t *vals[2] = {nullptr, nullptr};
+    uint64_t *keys[2] = {nullptr, nullptr};
+    uint64_t elem_cap = 0;     // capacity (elements) of vals/keys buffers
+    int key_words_cap = 0;
+    int cur = 0;
+
+    // radix pass state
+    uint64_t *status = nullptr;
+    uint64_t status_cap = 0;   // words
+    uint32_t epoch = 0;
+    uint32_t *counters = nullptr;   // tile-id counters [64]
+    uint32_t *hist = nullptr;       // [kMaxWords*8][256]
+    uint32_t *offsets = nullptr;    // [kMaxWords*8][256]
+
+    // group / scan scratch
+    uint8_t *flags = nullptr;
+    uint64_t flags_cap = 0;
+    uint32_t *idx_a = nullptr, *idx_b = nullptr;
+    uint64_t idx_cap = 0, idx_b_cap = 0;
+    uint64_t *cumk = nullptr;       // enumerate: cumulative k-mers per segment
+    uint64_t cumk_cap = 0;
+    std::vector<uint32_t> hseg;     // host copy of the segment table
+    bool internal_dollar = false;   // a '$' that is not a segment separator
+    uint32_t *tile_sums = nullptr;
+    uint64_t tile_sums_cap = 0;
+    uint64_t *scalars = nullptr;    // small device scratch [64]
+    int64_t *dhist = nullptr;
+    uint64_t dhist_cap = 0;
+    uint8_t *mask = nullptr;
+    uint64_t mask_cap = 0, mask_n = 0;
+    uint32_t *ranks = nullptr;      // doubling: rank per sba position
+    uint64_t ranks_cap = 0;
+
+    // unique view
+    uint64_t n_unique = 0;
+    bool unique_valid = false;
+
+    // profiling
+    bool profile = false;
+    std::vector<gkm::Timer> timers;
+};
+
+// ---------------------------------------------------------------------------------------------
+// launchers (implemented in gkm_encode.hip / gkm_sort.hip / gkm_group.hip)
+// ---------------------------------------------------------------------------------------------
+namespace gkm {
+
+hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
+void timer_begin(gk_ctx *c, const char *name, int *slot);
+void timer_end(gk_ctx *c, int slot);
+int fail(gk_ctx *c, int code, const std::string &msg);
+int hip_fail(gk_ctx *c, hipError_t e, const char *where);
+
+// encode
+hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags);
+hipError_t launch_enumerate(gk_ctx *c, uint32_t min_k, uint32_t *out);
+hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n, uint32_t min_k, uint32_t *d_bad);
+hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist);
+hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys);
+
+// sort
+hipError_t launch_histogram(gk_ctx *c, const uint64_t *keys, uint64_t n, int words, int digits, uint32_t *hist);
+int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready);
+
+// group / scan
+hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);
+hipError_t scan_flags_inclusive(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out);
+hipError_t unique_counts_device(gk_ctx *c);
+
+// write the lazily enumerated starts into vals[cur] if a reader needs them (gkm_capi.hip)
+int materialize_starts(gk_ctx *c);
+
+// prefix doubling (gkm_capi.hip)
+hipError_t launch_rank_scatter(gk_ctx *c, const uint32_t *vals, const uint32_t *gid, const uint32_t *gstart, uint64_t n, uint32_t *R);
+
+}  // namespace gkm
+
+#define GK_TRY_HIP(c, expr)                                        \
+    do {                                                           \
+        hipError_t _e = (expr);                                    \
+        if (_e != hipSuccess) return gkm::hip_fail((c), _e, #expr); \
+    } while (0)

@@ -1,0 +1,301 @@
+"""ctypes binding of libgkm.so (include/gkm.h) -- the only way this package reaches the GPU.
+
+There is no CPU fallback: if the library is missing or no HIP device is visible, every call that
+needs the engine raises.  ``Engine`` owns one ``gk_ctx`` (one device, one stream, device buffers).
+"""
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+GK_OK = 0
+GK_E_ARG = -1
+GK_E_HIP = -2
+GK_E_OOM = -3
+GK_E_UNSUPPORTED = -4
+GK_E_ALPHABET = -5
+GK_E_STATE = -6
+GK_E_FILTER = -7
+GK_E_LIMIT = -8
+GK_E_NO_BASES = -9
+
+# gk_filter_kind
+FILTER_KEEP_ALL = 0
+FILTER_LENGTH = 1
+FILTER_HOMOPOLYMER = 2
+FILTER_GC = 3
+FILTER_NO_AMBIGUOUS = 4
+FILTER_CRISPR_NGG = 5
+FILTER_MASK = 6
+
+# gk_filter_error
+FERR_HOMO_LEN = 1
+FERR_GC_LEN = 2
+FERR_GC_OOB = 3
+FERR_AMBIG_LEN = 4
+FERR_AMBIG_SEG = 5
+FERR_CRISPR_LEN = 6
+
+LIB_PATH = Path(__file__).with_name("libgkm.so")
+
+# every symbol include/gkm.h declares (checked by tests/test_native_abi.py)
+EXPORTED = (
+    "gk_create", "gk_destroy", "gk_last_error", "gk_sync", "gk_device_count", "gk_set_sequence",
+    "gk_alphabet_is_acgt", "gk_enumerate", "gk_set_start_indices", "gk_sort", "gk_num_kmers",
+    "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
+    "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
+    "gk_profile_enable", "gk_profile_report", "gk_stream",
+)
+
+
+class GkFilter(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("pad", ctypes.c_int32), ("p0", ctypes.c_int64),
+                ("p1", ctypes.c_int64), ("p2", ctypes.c_int64)]
+
+
+class GkError(RuntimeError):
+    """A libgkm call failed; ``code`` is the gk_status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libgkm error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class FilterRaised(GkError):
+    """A built-in filter raised on the device; carries the reference's error site."""
+
+    def __init__(self, ferr: int, sba_idx: int):
+        super().__init__(GK_E_FILTER, f"filter error {ferr} at sba index {sba_idx}")
+        self.ferr = ferr
+        self.sba_idx = sba_idx
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_I32P = ctypes.POINTER(ctypes.c_int32)
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+
+_SIGS = {
+    "gk_create": ([ctypes.POINTER(_P), ctypes.c_int], ctypes.c_int),
+    "gk_destroy": ([_P], None),
+    "gk_last_error": ([_P], ctypes.c_char_p),
+    "gk_sync": ([_P], ctypes.c_int),
+    "gk_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "gk_set_sequence": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_alphabet_is_acgt": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "gk_enumerate": ([_P, ctypes.c_uint32, _U64P], ctypes.c_int),
+    "gk_set_start_indices": ([_P, _U32P, ctypes.c_uint64, ctypes.c_uint32], ctypes.c_int),
+    "gk_sort": ([_P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+    "gk_num_kmers": ([_P, _U64P], ctypes.c_int),
+    "gk_copy_start_indices": ([_P, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_copy_start_range": ([_P, ctypes.c_uint64, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_key_layout": ([_P, _U32P, _U32P, _U32P], ctypes.c_int),
+    "gk_copy_keys": ([_P, _U64P, ctypes.c_uint64], ctypes.c_int),
+    "gk_set_filter_mask": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
+    "gk_group_hist": ([_P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(GkFilter), ctypes.c_int64, ctypes.c_int64,
+                       ctypes.c_int64, _I64P, _I64P, _I32P, _U64P], ctypes.c_int),
+    "gk_group_members": ([_P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(GkFilter), ctypes.c_int64,
+                          ctypes.c_int64, ctypes.c_int64, _U64P, _U32P, _U32P, ctypes.c_uint64, _U64P, _I32P,
+                          _U64P], ctypes.c_int),
+    "gk_unique_counts": ([_P, _U64P], ctypes.c_int),
+    "gk_copy_unique": ([_P, _U64P, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_device_views": ([_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _U64P, _U32P], ctypes.c_int),
+    "gk_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
+    "gk_profile_report": ([_P, ctypes.c_char_p, ctypes.c_uint64], ctypes.c_int),
+    "gk_stream": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
+}
+
+
+def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
+    """Load libgkm.so (raises if it has not been built -- there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not path.exists():
+        raise RuntimeError(
+            f"libgkm.so not found at {path}; build it with `make -C genome-kmers_amd/csrc` "
+            "(genome_kmers has no CPU fallback)"
+        )
+    lib = ctypes.CDLL(str(path))
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _ptr(arr: np.ndarray, ctype):
+    return arr.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int(0)
+    if lib.gk_device_count(ctypes.byref(n)) != GK_OK:
+        return 0
+    return n.value
+
+
+def default_device() -> int:
+    return int(os.environ.get("GENOME_KMERS_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+class Engine:
+    """One libgkm context: a sequence byte array resident in HBM plus its k-mer arrays."""
+
+    def __init__(self, device: int = None):
+        self.lib = load_library()
+        self.device = default_device() if device is None else device
+        self.ctx = _P()
+        rc = self.lib.gk_create(ctypes.byref(self.ctx), self.device)
+        if rc != GK_OK:
+            self.ctx = None
+            raise GkError(rc, f"cannot create a HIP context on device {self.device}: genome_kmers needs an "
+                              "MI355X (gfx950) GPU and has no CPU fallback")
+        self.n = 0
+
+    def __del__(self):
+        ctx = getattr(self, "ctx", None)
+        if ctx:
+            self.lib.gk_destroy(ctx)
+            self.ctx = None
+
+    # -----------------------------------------------------------------------------------------
+    def _check(self, rc: int):
+        if rc != GK_OK:
+            msg = self.lib.gk_last_error(self.ctx)
+            raise GkError(rc, msg.decode() if msg else "")
+
+    def set_sequence(self, sba: np.ndarray, seg_starts: np.ndarray):
+        sba = np.ascontiguousarray(sba, dtype=np.uint8)
+        seg = np.ascontiguousarray(seg_starts, dtype=np.uint32)
+        self._check(self.lib.gk_set_sequence(self.ctx, _ptr(sba, ctypes.c_uint8), sba.size,
+                                             _ptr(seg, ctypes.c_uint32), seg.size))
+
+    def is_acgt(self) -> bool:
+        v = ctypes.c_int(0)
+        self._check(self.lib.gk_alphabet_is_acgt(self.ctx, ctypes.byref(v)))
+        return bool(v.value)
+
+    def enumerate(self, min_kmer_len: int) -> int:
+        n = ctypes.c_uint64(0)
+        self._check(self.lib.gk_enumerate(self.ctx, min_kmer_len, ctypes.byref(n)))
+        self.n = n.value
+        return self.n
+
+    def set_start_indices(self, starts: np.ndarray, min_kmer_len: int):
+        arr = np.ascontiguousarray(starts, dtype=np.uint32)
+        self._check(self.lib.gk_set_start_indices(self.ctx, _ptr(arr, ctypes.c_uint32), arr.size, min_kmer_len))
+        self.n = arr.size
+
+    def sort(self, max_kmer_len: int = None):
+        self._check(self.lib.gk_sort(self.ctx, 0 if max_kmer_len is None else int(max_kmer_len), 0))
+
+    def sync(self):
+        self._check(self.lib.gk_sync(self.ctx))
+
+    def copy_starts(self, out: np.ndarray = None) -> np.ndarray:
+        if out is None:
+            out = np.empty(self.n, dtype=np.uint32)
+        self._check(self.lib.gk_copy_start_indices(self.ctx, _ptr(out, ctypes.c_uint32), self.n))
+        return out
+
+    def start_range(self, offset: int, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=np.uint32)
+        self._check(self.lib.gk_copy_start_range(self.ctx, offset, _ptr(out, ctypes.c_uint32), count))
+        return out
+
+    def key_layout(self):
+        w, b, s = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.gk_key_layout(self.ctx, ctypes.byref(w), ctypes.byref(b), ctypes.byref(s)))
+        return w.value, b.value, s.value
+
+    def copy_keys(self) -> np.ndarray:
+        words, _, _ = self.key_layout()
+        out = np.empty((self.n, words), dtype=np.uint64)
+        self._check(self.lib.gk_copy_keys(self.ctx, _ptr(out, ctypes.c_uint64), out.size))
+        return out
+
+    def set_filter_mask(self, mask: np.ndarray):
+        m = np.ascontiguousarray(mask, dtype=np.uint8)
+        self._check(self.lib.gk_set_filter_mask(self.ctx, _ptr(m, ctypes.c_uint8), m.size))
+
+    def _raise_filter(self, rc, code, idx):
+        if rc == GK_E_FILTER:
+            raise FilterRaised(code.value, idx.value)
+        self._check(rc)
+
+    def group_hist(self, is_sorted, kmer_len, filt: GkFilter, min_group_size, max_group_size, max_counts_bin):
+        hist = np.zeros(max_counts_bin + 1, dtype=np.int64)
+        total = ctypes.c_int64(0)
+        code, idx = ctypes.c_int32(0), ctypes.c_uint64(0)
+        rc = self.lib.gk_group_hist(self.ctx, int(bool(is_sorted)), -1 if kmer_len is None else int(kmer_len),
+                                    ctypes.byref(filt), int(min_group_size),
+                                    -1 if max_group_size is None else int(max_group_size), int(max_counts_bin),
+                                    _ptr(hist, ctypes.c_int64), ctypes.byref(total), ctypes.byref(code),
+                                    ctypes.byref(idx))
+        self._raise_filter(rc, code, idx)
+        return hist, int(total.value)
+
+    def group_members(self, is_sorted, kmer_len, filt: GkFilter, min_group_size, max_group_size, yield_first_n):
+        args = (int(bool(is_sorted)), -1 if kmer_len is None else int(kmer_len), ctypes.byref(filt),
+                int(min_group_size), -1 if max_group_size is None else int(max_group_size),
+                -1 if yield_first_n is None else int(yield_first_n))
+        count = ctypes.c_uint64(0)
+        code, idx = ctypes.c_int32(0), ctypes.c_uint64(0)
+        rc = self.lib.gk_group_members(self.ctx, *args, None, None, None, 0, ctypes.byref(count),
+                                       ctypes.byref(code), ctypes.byref(idx))
+        self._raise_filter(rc, code, idx)
+        m = count.value
+        num = np.empty(m, dtype=np.uint64)
+        yld = np.empty(m, dtype=np.uint32)
+        tot = np.empty(m, dtype=np.uint32)
+        if m:
+            rc = self.lib.gk_group_members(self.ctx, *args, _ptr(num, ctypes.c_uint64), _ptr(yld, ctypes.c_uint32),
+                                           _ptr(tot, ctypes.c_uint32), m, ctypes.byref(count), ctypes.byref(code),
+                                           ctypes.byref(idx))
+            self._raise_filter(rc, code, idx)
+        return num, yld, tot
+
+    def unique_counts(self):
+        g = ctypes.c_uint64(0)
+        self._check(self.lib.gk_unique_counts(self.ctx, ctypes.byref(g)))
+        starts = np.empty(g.value, dtype=np.uint64)
+        counts = np.empty(g.value, dtype=np.uint32)
+        self._check(self.lib.gk_copy_unique(self.ctx, _ptr(starts, ctypes.c_uint64), _ptr(counts, ctypes.c_uint32),
+                                            g.value))
+        return starts, counts
+
+    def unique_count_only(self) -> int:
+        g = ctypes.c_uint64(0)
+        self._check(self.lib.gk_unique_counts(self.ctx, ctypes.byref(g)))
+        return g.value
+
+    def device_views(self):
+        s, k, n, w = _P(), _P(), ctypes.c_uint64(), ctypes.c_uint32()
+        self._check(self.lib.gk_device_views(self.ctx, ctypes.byref(s), ctypes.byref(k), ctypes.byref(n),
+                                             ctypes.byref(w)))
+        return s.value, k.value, n.value, w.value
+
+    def stream_handle(self) -> int:
+        s = _P()
+        self._check(self.lib.gk_stream(self.ctx, ctypes.byref(s)))
+        return s.value or 0
+
+    def profile_enable(self, on: bool = True):
+        self._check(self.lib.gk_profile_enable(self.ctx, int(on)))
+
+    def profile_report(self) -> dict:
+        import json
+
+        buf = ctypes.create_string_buffer(1 << 16)
+        self._check(self.lib.gk_profile_report(self.ctx, buf, len(buf)))
+        return json.loads(buf.value.decode())

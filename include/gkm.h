@@ -1,0 +1,153 @@
+/*
+ * gkm.h -- C ABI of libgkm.so, the MI355X (gfx950) k-mer engine.
+ *
+ * The reference (mrperkett/genome-kmers v1.0.1) is pure Python + numba and has no FFI; its
+ * drop-in boundary is the Kmers / SequenceCollection class surface.  Each entry point below
+ * replaces one reference routine (paths relative to the reference's src/genome_kmers/) and is what
+ * a ctypes binding inside that class surface binds:
+ *
+ *   gk_set_sequence        SequenceCollection.forward_sba / _forward_sba_seg_starts as the input
+ *                          contract (sequence_collection.py:531-576, 663-726, 155-187); H2D copy.
+ *   gk_enumerate           Kmers._initialize_single_pass / _get_unfiltered_kmer_count (kmers.py:789-861)
+ *   gk_sort                Kmers.sort + get_is_less_than_func (kmers.py:1624-1731), numba quicksort
+ *   gk_copy_start_indices  Kmers.kmer_sba_start_indices read-back (kmers.py:811, 1648)
+ *   gk_set_start_indices   assigning Kmers.kmer_sba_start_indices (kmers.py:724, 1462, 1522)
+ *   gk_group_hist          get_kmer_group_size_hist (kmers.py:454-520) behind Kmers.get_kmer_count
+ *                          (kmers.py:994-1083) and Kmers.get_kmer_group_counts (kmers.py:1085-1178)
+ *   gk_group_members       kmer_info_by_group_generator (kmers.py:523-648) behind Kmers.get_kmers
+ *                          (kmers.py:869-992)
+ *   gk_unique_counts       the (unique k-mer, multiplicity) view of the sorted groups (kmers.py:597-625)
+ *   gk_copy_keys           encoded k-mers (no reference counterpart: the reference compares bytes)
+ *
+ * Conventions: every function returns GK_OK (0) or a negative gk_status; gk_last_error(ctx)
+ * describes the last failure.  Host pointers are borrowed for the duration of the call only.
+ * Device memory is owned by the context and freed by gk_destroy.  A context is bound to one HIP
+ * device and one stream; it is not thread-safe.  Work is stream-ordered: functions that return
+ * data to the host synchronise the stream, others may return before the device finishes
+ * (gk_sync waits).
+ */
+#ifndef GKM_H
+#define GKM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gk_ctx gk_ctx;
+
+enum gk_status {
+    GK_OK = 0,
+    GK_E_ARG = -1,          /* invalid argument                                             */
+    GK_E_HIP = -2,          /* HIP runtime error                                             */
+    GK_E_OOM = -3,          /* device allocation failed                                      */
+    GK_E_UNSUPPORTED = -4,  /* configuration not supported by the device path                */
+    GK_E_ALPHABET = -5,     /* byte outside {A,B,C,D,G,H,K,M,N,R,S,T,V,W,Y,$}                */
+    GK_E_STATE = -6,        /* call out of order (e.g. sort before set_sequence)             */
+    GK_E_FILTER = -7,       /* a built-in filter raised (see gk_filter_error)                */
+    GK_E_LIMIT = -8,        /* more than 2^32-1 k-mers (kmers.py:805-808)                     */
+    GK_E_NO_BASES = -9,     /* comparator found no valid base (kmers.py:368-369)             */
+};
+
+/* built-in k-mer filters (kmers.py:14-259); evaluated on the device */
+enum gk_filter_kind {
+    GK_FILTER_KEEP_ALL = 0,      /* kmer_filter_keep_all                       kmers.py:14-16   */
+    GK_FILTER_LENGTH = 1,        /* gen_kmer_length_filter_func(p0=min_len)    kmers.py:19-34   */
+    GK_FILTER_HOMOPOLYMER = 2,   /* gen_kmer_homopolymer_filter_func(p0=max_h, p1=kmer_len)  :37-100 */
+    GK_FILTER_GC = 3,            /* gen_kmer_gc_content_filter_func(p0=min_count, p1=max_count, p2=kmer_len) :103-192 */
+    GK_FILTER_NO_AMBIGUOUS = 4,  /* gen_no_ambiguous_bases_filter(p0=kmer_len) kmers.py:195-229 */
+    GK_FILTER_CRISPR_NGG = 5,    /* crispr_ngg_pam_filter                      kmers.py:232-259 */
+    GK_FILTER_MASK = 6,          /* per-sorted-position byte mask from gk_set_filter_mask      */
+};
+
+/* filter error codes reported through gk_filter_error (match the reference's raise sites) */
+enum gk_filter_error {
+    GK_FERR_NONE = 0,
+    GK_FERR_HOMO_LEN = 1,    /* kmers.py:66-69 / 83-86  "The kmer_len (..) requested is too large for kmer_sba_start_idx (..)" */
+    GK_FERR_GC_LEN = 2,      /* kmers.py:176-179        "... too larger for kmer_sba_start_idx (..)"                        */
+    GK_FERR_GC_OOB = 3,      /* read past the end of the sba (undefined behaviour in numba)                                */
+    GK_FERR_AMBIG_LEN = 4,   /* kmers.py:212-213        "kmer_len (..) is invalid. It extends beyond len(sba)"              */
+    GK_FERR_AMBIG_SEG = 5,   /* kmers.py:220-221        "end of segment was reached. kmer_len (..) invalid."                */
+    GK_FERR_CRISPR_LEN = 6,  /* kmers.py:252-253        "The guide defined at this start index extends beyond the sba"      */
+};
+
+typedef struct gk_filter {
+    int32_t kind;          /* gk_filter_kind */
+    int32_t pad;
+    int64_t p0, p1, p2;
+} gk_filter;
+
+/* gk_sort flags */
+#define GK_SORT_DEFAULT 0u
+
+/* ---- lifetime ------------------------------------------------------------------------------ */
+int gk_create(gk_ctx **out, int device);
+void gk_destroy(gk_ctx *ctx);
+const char *gk_last_error(gk_ctx *ctx);
+int gk_sync(gk_ctx *ctx);
+int gk_device_count(int *count);
+
+/* ---- input contract ------------------------------------------------------------------------- */
+/* sba: ASCII bases, contigs joined by '$' (36), no trailing '$'; seg_starts: ascending uint32. */
+int gk_set_sequence(gk_ctx *ctx, const uint8_t *sba, uint64_t len, const uint32_t *seg_starts, uint64_t nseg);
+/* 1 if the loaded sba holds only {A,C,G,T,$} (2-bit keys), 0 otherwise (4-bit keys) */
+int gk_alphabet_is_acgt(gk_ctx *ctx, int *is_acgt);
+
+/* ---- enumerate / sort ------------------------------------------------------------------------ */
+/* every start with >= min_kmer_len bases before '$' / end, contig by contig, ascending */
+int gk_enumerate(gk_ctx *ctx, uint32_t min_kmer_len, uint64_t *n_out);
+/* replace the start indices with host-provided ones (any order, each must be a valid start) */
+int gk_set_start_indices(gk_ctx *ctx, const uint32_t *src, uint64_t n, uint32_t min_kmer_len);
+/*
+ * Sort the start indices by the k-mer at each start, compared as compare_sba_kmers_lexicographically
+ * with max_kmer_len (0 = None: compare up to the '$' that ends the contig).  Equal k-mers are
+ * ordered by start index (the reference's break_ties=True order, kmers.py:1710-1711).
+ */
+int gk_sort(gk_ctx *ctx, uint32_t max_kmer_len, uint32_t flags);
+int gk_num_kmers(gk_ctx *ctx, uint64_t *n);
+int gk_copy_start_indices(gk_ctx *ctx, uint32_t *dst, uint64_t n);
+/* start indices [offset, offset + count) of the current order (Kmers.get_kmer_str, kmers.py:1604) */
+int gk_copy_start_range(gk_ctx *ctx, uint64_t offset, uint32_t *dst, uint64_t count);
+/* encoded keys of the sorted k-mers: words_per_key uint64 words per k-mer, most significant first */
+int gk_key_layout(gk_ctx *ctx, uint32_t *words_per_key, uint32_t *bits_per_symbol, uint32_t *symbols);
+int gk_copy_keys(gk_ctx *ctx, uint64_t *dst, uint64_t n_words);
+
+/* ---- groups ---------------------------------------------------------------------------------- */
+/* mask for GK_FILTER_MASK: one byte per position of the current start-index order */
+int gk_set_filter_mask(gk_ctx *ctx, const uint8_t *mask, uint64_t n);
+/*
+ * Histogram of group sizes over k-mers passing `filter`; groups are runs of equal k-mers under
+ * compare_sba_kmers_lexicographically(kmer_len) (kmer_len < 0 = None) when is_sorted, else every
+ * k-mer is its own group (compare_sba_kmers_always_less_than).  max_group_size < 0 = None.
+ * hist has max_counts_bin + 1 entries.  On GK_E_FILTER, *err_code / *err_idx name the failing
+ * filter check and the SBA index of the first (in start-index order) k-mer that raised.
+ */
+int gk_group_hist(gk_ctx *ctx, int is_sorted, int64_t kmer_len, const gk_filter *filter, int64_t min_group_size,
+                  int64_t max_group_size, int64_t max_counts_bin, int64_t *hist, int64_t *total,
+                  int32_t *err_code, uint64_t *err_idx);
+/*
+ * The first yield_first_n (< 0 = None) members of every qualifying group, in generator order:
+ * (kmer_num, group_size_yielded, group_size_total).  Two calls: with kmer_num == NULL only
+ * *n_out is set; then call again with arrays of at least *n_out entries.
+ */
+int gk_group_members(gk_ctx *ctx, int is_sorted, int64_t kmer_len, const gk_filter *filter, int64_t min_group_size,
+                     int64_t max_group_size, int64_t yield_first_n, uint64_t *kmer_num, uint32_t *size_yielded,
+                     uint32_t *size_total, uint64_t capacity, uint64_t *n_out, int32_t *err_code, uint64_t *err_idx);
+/* distinct k-mers of the sorted order (kmer_len = sort length): first index and multiplicity */
+int gk_unique_counts(gk_ctx *ctx, uint64_t *n_unique);
+int gk_copy_unique(gk_ctx *ctx, uint64_t *group_start, uint32_t *count, uint64_t n);
+
+/* ---- device views / timing (bench + multi-GPU orchestration) --------------------------------- */
+/* device pointers of the current sorted start indices and keys (valid until the next call) */
+int gk_device_views(gk_ctx *ctx, void **starts, void **keys, uint64_t *n, uint32_t *words_per_key);
+/* enable per-kernel HIP-event timing; gk_profile_report writes a JSON object to buf */
+int gk_profile_enable(gk_ctx *ctx, int on);
+int gk_profile_report(gk_ctx *ctx, char *buf, uint64_t buflen);
+/* stream handle of the context (hipStream_t), for interop */
+int gk_stream(gk_ctx *ctx, void **stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GKM_H */

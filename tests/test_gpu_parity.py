@@ -1,0 +1,318 @@
+"""Device parity: the drop-in Kmers API (libgkm.so through its C ABI) vs the reference's golden
+vectors and the CPU oracle.  Bit-exact for every integer output.
+
+Contract: start indices equal the reference's break_ties=True order (equal
+k-mers by ascending start index); k-mer order, keys, group histograms, counts and generator
+yields equal the reference on that order.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import load_case, load_manifest, seq_list_of
+from genome_kmers import _native
+from genome_kmers import kmers as gk
+from genome_kmers.sequence_collection import SequenceCollection
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = load_manifest()
+CASE_IDS = [c["name"] for c in CASES]
+
+
+def make(case):
+    a = load_case(case["name"])
+    sc = SequenceCollection(sequence_list=seq_list_of(case, a), strands_to_load="forward")
+    np.testing.assert_array_equal(sc.forward_sba, a["sba"])
+    np.testing.assert_array_equal(sc._forward_sba_seg_starts, a["seg_starts"])
+    km = gk.Kmers(sc, min_kmer_len=case["min_kmer_len"], max_kmer_len=case["max_kmer_len"])
+    return km, a
+
+
+def filter_of(spec):
+    k = spec["kind"]
+    if k == "keep_all":
+        return gk.kmer_filter_keep_all
+    if k == "length":
+        return gk.gen_kmer_length_filter_func(spec["min_kmer_len"])
+    if k == "homopolymer":
+        return gk.gen_kmer_homopolymer_filter_func(spec["max_homopolymer_size"], spec["kmer_len"])
+    if k == "gc":
+        return gk.gen_kmer_gc_content_filter_func(spec["min_gc"], spec["max_gc"], spec["kmer_len"])
+    if k == "no_ambiguous":
+        return gk.gen_no_ambiguous_bases_filter(spec["kmer_len"])
+    if k == "crispr_ngg":
+        return gk.crispr_ngg_pam_filter
+    raise ValueError(k)
+
+
+def run_query(km, q):
+    filt = filter_of(q["filter"])
+    try:
+        if q["op"] == "group_counts":
+            h, t = km.get_kmer_group_counts(q["kmer_len"], filt, q["min_group_size"], q["max_group_size"],
+                                            q["max_counts_bin"])
+            return {"hist": h.tolist(), "total": int(t)}
+        if q["op"] == "count":
+            return {"total": int(km.get_kmer_count(q["kmer_len"], filt, q["min_group_size"], q["max_group_size"]))}
+        out = list(km.get_kmers(q["kmer_len"], kmer_filter_func=filt, kmer_info_to_yield=q.get("info", "minimum"),
+                                min_group_size=q["min_group_size"], max_group_size=q["max_group_size"],
+                                yield_first_n=q.get("yield_first_n"), one_based_seq_index=q.get("one_based", False)))
+        return {"kmers": [list(t) for t in out]}
+    except (ValueError, AssertionError) as e:
+        return {"error": type(e).__name__, "message": str(e)}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    assert _native.device_count() > 0, "gpu tests need a visible MI355X"
+
+
+# ---------------------------------------------------------------------------------------------
+# golden vectors (produced by the reference itself)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", CASES, ids=CASE_IDS)
+def test_enumerate_golden(case):
+    km, a = make(case)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, a["starts_unsorted"])
+    assert len(km) == case["num_kmers"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=CASE_IDS)
+def test_sort_golden(case):
+    km, a = make(case)
+    km.sort()
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, a["starts_stable"])
+    # same k-mer sequence as the reference's default order (ties only permute equal k-mers)
+    if case["max_kmer_len"] is not None:
+        sba, mk = a["sba"], case["max_kmer_len"]
+        got = [bytes(sba[s:s + mk]).split(b"$")[0] for s in km.kmer_sba_start_indices.tolist()]
+        ref = [bytes(sba[s:s + mk]).split(b"$")[0] for s in a["starts_default"].tolist()]
+        assert got == ref
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["max_kmer_len"] is not None], ids=lambda c: c["name"])
+def test_encoded_keys_golden(case):
+    km, a = make(case)
+    km.sort()
+    words, bits, symbols = km._engine.key_layout()
+    if bits == 0:
+        pytest.skip("long bound sorted by prefix doubling: keys are ranks")
+    acgt = km._engine.is_acgt()
+    spec = oracle.key_spec(acgt, case["min_kmer_len"], case["max_kmer_len"])
+    assert (words, bits, symbols) == (spec[3], spec[0], spec[1])
+    want = oracle.encode_keys(a["sba"], a["starts_stable"], *spec)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), want)
+
+
+@pytest.mark.parametrize("case", CASES, ids=CASE_IDS)
+def test_group_queries_golden(case):
+    km, _ = make(case)
+    km.sort()
+    for q, want in zip(case["queries"], case["results_stable_order"]):
+        got = run_query(km, q)
+        assert got == want, q
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if not c["ties_differ"]], ids=lambda c: c["name"])
+def test_default_order_equals_when_no_ties(case):
+    km, a = make(case)
+    km.sort()
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, a["starts_default"])
+    for q, want in zip(case["queries"], case["results_default_order"]):
+        assert run_query(km, q) == want, q
+
+
+def test_unsorted_queries_every_kmer_its_own_group():
+    case = next(c for c in CASES if c["name"] == "c1_seed42_10kb_k5")
+    km, a = make(case)
+    assert km.get_kmer_count(5) == len(a["starts_unsorted"])
+    got = list(km.get_kmers(5))
+    assert got == [(i, 1, 1) for i in range(len(a["starts_unsorted"]))]
+    with pytest.raises(AssertionError, match="must be sorted"):
+        km.get_kmer_group_counts(5)
+
+
+def test_get_kmer_str_after_sort():
+    case = next(c for c in CASES if c["name"] == "seq2_min3_maxNone")
+    km, a = make(case)
+    km.sort()
+    sba = a["sba"]
+    for i, s in enumerate(a["starts_stable"].tolist()):
+        end = bytes(sba[s:]).split(b"$")[0]
+        assert km.get_kmer_str(i) == end.decode()
+
+
+# ---------------------------------------------------------------------------------------------
+# oracle parity at larger sizes
+# ---------------------------------------------------------------------------------------------
+def random_genome(rng, lengths, alphabet=b"ACGT", repeat=None, copies=0):
+    seqs = []
+    for i, L in enumerate(lengths):
+        s = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), L).astype(np.uint8)
+        if repeat is not None:
+            for _ in range(copies):
+                at = int(rng.integers(0, max(1, L - len(repeat))))
+                s[at:at + len(repeat)] = repeat[: L - at]
+        seqs.append((f"c{i}", s.tobytes().decode()))
+    return seqs
+
+
+def oracle_check(seqs, min_k, max_k, check_counts=True):
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=min_k, max_kmer_len=max_k)
+    unsorted = oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, min_k)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, unsorted)
+    km.sort()
+    want = oracle.quicksort(sc.forward_sba, unsorted, min_k, max_k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    if check_counts:
+        kl = max_k if max_k is not None else min_k
+        h, t = km.get_kmer_group_counts(kl, max_counts_bin=64)
+        oh, ot = oracle.group_scan(sc.forward_sba, want, kl, max_counts_bin=64)
+        np.testing.assert_array_equal(h, oh)
+        assert t == ot
+    return km, sc, want
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_acgt_k31_vs_oracle(seed):
+    rng = np.random.default_rng(seed)
+    oracle_check(random_genome(rng, [300_000, 150_000, 31, 77_777]), 31, 31)
+
+
+def test_repeats_and_ties_k31_vs_oracle():
+    rng = np.random.default_rng(3)
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 5000).astype(np.uint8)
+    oracle_check(random_genome(rng, [200_000, 120_000], repeat=rep, copies=7), 31, 31)
+
+
+def test_homopolymer_genome_all_ties():
+    seqs = [("a", "A" * 50_000), ("b", "A" * 20_000 + "C" * 20_000)]
+    oracle_check(seqs, 21, 21)
+
+
+def test_iupac_k31_vs_oracle():
+    rng = np.random.default_rng(4)
+    oracle_check(random_genome(rng, [120_000, 60_000], alphabet=b"ACGTACGTACGTNRY"), 31, 31)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 16, 32, 33, 63, 64, 100])
+def test_k_sweep_vs_oracle(k):
+    rng = np.random.default_rng(100 + k)
+    oracle_check(random_genome(rng, [40_000, 9_000, 128]), k, k)
+
+
+@pytest.mark.parametrize("min_k,max_k", [(1, 8), (5, 31), (10, 40), (3, 70)])
+def test_bounded_variable_length_vs_oracle(min_k, max_k):
+    rng = np.random.default_rng(min_k * 7 + max_k)
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 300).astype(np.uint8)
+    oracle_check(random_genome(rng, [30_000, 8_000, 500], repeat=rep, copies=5), min_k, max_k)
+
+
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTN"])
+def test_suffix_mode_vs_oracle(alphabet):
+    rng = np.random.default_rng(len(alphabet))
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 200).astype(np.uint8)
+    oracle_check(random_genome(rng, [12_000, 3_000, 90], alphabet=alphabet, repeat=rep, copies=4), 2, None,
+                 check_counts=False)
+
+
+def test_long_bound_uses_doubling_vs_oracle():
+    rng = np.random.default_rng(9)
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 400).astype(np.uint8)
+    oracle_check(random_genome(rng, [20_000, 5_000], repeat=rep, copies=6), 10, 300)
+
+
+def test_user_assigned_starts_sort_like_break_ties():
+    rng = np.random.default_rng(11)
+    seqs = random_genome(rng, [20_000])
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=12, max_kmer_len=12)
+    user = rng.permutation(km.kmer_sba_start_indices)[:5000].astype(np.uint32)
+    user = np.concatenate([user, user[:100]])  # duplicates tie on key and index
+    km.kmer_sba_start_indices = user
+    km.sort()
+    want = oracle.quicksort(sc.forward_sba, user, 12, 12, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    # in-place semantics: the caller's array object now holds the sorted order
+    np.testing.assert_array_equal(user, want)
+
+
+def test_invalid_user_starts_raise_reference_assertion():
+    sc = SequenceCollection(sequence_list=[("a", "ACGTACGT"), ("b", "GGGCCC")])
+    km = gk.Kmers(sc, min_kmer_len=4, max_kmer_len=4)
+    km.kmer_sba_start_indices = np.array([0, 6, 1], dtype=np.uint32)  # 6: only 2 bases before '$'
+    with pytest.raises(AssertionError, match="kmers compared were less than min_kmer_len"):
+        km.sort()
+
+
+def test_custom_python_filter_is_honoured():
+    rng = np.random.default_rng(12)
+    sc = SequenceCollection(sequence_list=random_genome(rng, [5000]))
+    km = gk.Kmers(sc, min_kmer_len=6, max_kmer_len=6)
+    km.sort()
+
+    def starts_with_a(sba, strand, idx):
+        return sba[idx] == ord("A")
+
+    got = km.get_kmer_count(6, starts_with_a)
+    filt_starts = [s for s in km.kmer_sba_start_indices.tolist() if sc.forward_sba[s] == ord("A")]
+    _, want = oracle.group_scan(sc.forward_sba, np.array(filt_starts, dtype=np.uint32), 6, max_counts_bin=10)
+    assert got == want
+
+
+def test_unique_counts_match_groups():
+    rng = np.random.default_rng(13)
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 700).astype(np.uint8)
+    km, sc, want = oracle_check(random_genome(rng, [50_000, 20_000], repeat=rep, copies=9), 25, 25)
+    first, counts = km.get_unique_kmers()
+    ys = oracle.group_scan(sc.forward_sba, want, 25, yield_first_n=1)
+    assert first.tolist() == [y[0] for y in ys]
+    assert counts.tolist() == [y[2] for y in ys]
+    assert int(counts.sum()) == len(want)
+
+
+def test_single_kmer_and_tiny_inputs():
+    sc = SequenceCollection(sequence_list=[("a", "ACGTA")])
+    km = gk.Kmers(sc, min_kmer_len=5, max_kmer_len=5)
+    km.sort()
+    assert km.kmer_sba_start_indices.tolist() == [0]
+    assert km.get_kmer_group_counts(5, max_counts_bin=3)[0].tolist() == [0, 1, 0, 0]
+    sc = SequenceCollection(sequence_list=[("a", "A")])
+    km = gk.Kmers(sc)
+    km.sort()
+    assert km.kmer_sba_start_indices.tolist() == [0]
+
+
+# ---------------------------------------------------------------------------------------------
+# size-independent properties at a large size
+# ---------------------------------------------------------------------------------------------
+def test_large_single_contig_properties():
+    L = 100_000_000
+    rng = np.random.default_rng(42)
+    sba = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L)]
+    sc = SequenceCollection()
+    sc.forward_sba = sba
+    sc._forward_sba_seg_starts = np.zeros(1, dtype=np.uint32)
+    sc.forward_record_names = ["chr0"]
+    sc._strands_loaded = "forward"
+    km = gk.Kmers(sc, min_kmer_len=31, max_kmer_len=31)
+    km.sort()
+    starts = km.kmer_sba_start_indices
+    n = L - 30
+    assert starts.shape == (n,)
+    # permutation of the enumerate output
+    assert np.array_equal(np.bincount(starts, minlength=n), np.ones(n, dtype=np.int64))
+    keys = km.get_encoded_kmers()[:, 0]
+    assert np.all(keys[1:] >= keys[:-1])
+    ties = keys[1:] == keys[:-1]
+    assert np.all(starts[1:][ties] > starts[:-1][ties])
+    # spot-check keys against the encoding of the sba
+    idx = rng.integers(0, n, 10_000)
+    np.testing.assert_array_equal(oracle.encode_keys(sba, starts[idx], 2, 31, 0, 1)[:, 0], keys[idx])
+    first, counts = km.get_unique_kmers()
+    assert int(counts.sum()) == n
+    h, t = km.get_kmer_group_counts(31, max_counts_bin=8)
+    assert t == n and int((h * np.arange(9))[:8].sum()) <= n

@@ -239,7 +239,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->cumk, c->tile_sums, c->scalars,
-                    c->dhist, c->mask, c->ranks};
+                    c->dhist, c->mask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
         if (b) hipFree(b);
     for (auto &t : c->timers) {

@@ -559,42 +559,27 @@ extern "C" int gk_group_members(gk_ctx *c, int is_sorted, int64_t kmer_len, cons
         if (n_out) *n_out = 0;
         return GK_OK;
     }
-    // per-group yield counts (into flags-sized scratch reinterpreted as u32) and their offsets
-    uint32_t *m = nullptr, *off = nullptr;
-    uint64_t *onum = nullptr;
-    uint32_t *oy = nullptr, *ot = nullptr;
-    GK_TRY_HIP(c, hipMallocAsync(reinterpret_cast<void **>(&m), 4 * (G + 16), c->stream));
-    GK_TRY_HIP(c, hipMallocAsync(reinterpret_cast<void **>(&off), 4 * (G + 16), c->stream));
+    // per-group yield counts and their offsets
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ym), &c->ym_cap, 4 * (G + 16)));
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->yoff), &c->yoff_cap, 4 * (G + 16)));
     hipLaunchKernelGGL(group_yield_count_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, count,
-                       min_group_size, max_group_size, yield_first_n, m);
+                       min_group_size, max_group_size, yield_first_n, c->ym);
     GK_TRY_HIP(c, hipGetLastError());
     uint64_t M = 0;
-    hipError_t e = scan_u32_exclusive(c, m, G, off, &M);
-    if (e == hipSuccess && kmer_num && M > 0) {
-        if (capacity < M) {
-            hipFreeAsync(m, c->stream);
-            hipFreeAsync(off, c->stream);
-            return fail(c, GK_E_ARG, "capacity smaller than the number of yields");
-        }
-        e = hipMallocAsync(reinterpret_cast<void **>(&onum), 8 * M, c->stream);
-        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&oy), 4 * M, c->stream);
-        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&ot), 4 * M, c->stream);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(group_yield_write_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, count,
-                               m, off, cidx, onum, oy, ot);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipMemcpyAsync(kmer_num, onum, 8 * M, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess && size_yielded) e = hipMemcpyAsync(size_yielded, oy, 4 * M, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess && size_total) e = hipMemcpyAsync(size_total, ot, 4 * M, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    GK_TRY_HIP(c, scan_u32_exclusive(c, c->ym, G, c->yoff, &M));
+    if (kmer_num && M > 0) {
+        if (capacity < M) return fail(c, GK_E_ARG, "capacity smaller than the number of yields");
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->onum), &c->onum_cap, 8 * M));
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->oy), &c->oy_cap, 4 * M));
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ot), &c->ot_cap, 4 * M));
+        hipLaunchKernelGGL(group_yield_write_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, count,
+                           c->ym, c->yoff, cidx, c->onum, c->oy, c->ot);
+        GK_TRY_HIP(c, hipGetLastError());
+        GK_TRY_HIP(c, hipMemcpyAsync(kmer_num, c->onum, 8 * M, hipMemcpyDeviceToHost, c->stream));
+        if (size_yielded) GK_TRY_HIP(c, hipMemcpyAsync(size_yielded, c->oy, 4 * M, hipMemcpyDeviceToHost, c->stream));
+        if (size_total) GK_TRY_HIP(c, hipMemcpyAsync(size_total, c->ot, 4 * M, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     }
-    if (onum) hipFreeAsync(onum, c->stream);
-    if (oy) hipFreeAsync(oy, c->stream);
-    if (ot) hipFreeAsync(ot, c->stream);
-    hipFreeAsync(m, c->stream);
-    hipFreeAsync(off, c->stream);
-    GK_TRY_HIP(c, e);
     if (n_out) *n_out = M;
     return GK_OK;
 }

@@ -113,6 +113,9 @@ struct gk_ctx {
     uint64_t mask_cap = 0, mask_n = 0;
     uint32_t *ranks = nullptr;      // doubling: rank per sba position
     uint64_t ranks_cap = 0;
+    uint32_t *ym = nullptr, *yoff = nullptr, *oy = nullptr, *ot = nullptr;  // generator yields
+    uint64_t *onum = nullptr;
+    uint64_t ym_cap = 0, yoff_cap = 0, oy_cap = 0, ot_cap = 0, onum_cap = 0;
 
     // unique view
     uint64_t n_unique = 0;

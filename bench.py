@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--genome-len", type=int, default=3_100_000_000)
     ap.add_argument("--k", type=int, default=31)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-sample", type=int, default=4_000_000, help="k-mers in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=16_000_000, help="k-mers in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=str, default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc (if present)")

@@ -1,0 +1,47 @@
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE CSVs into per-launch HBM bytes per kernel.
+
+Usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json [--label TEXT]
+
+Counter convention (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read, so the read
+side is doubled.  Calibration in this repo: alphabet_kernel streams the 3.1 GB sequence byte array
+with 16-B loads and reports FETCH_SIZE x 1024 x 2 = 3.1 GB (profiles/r1/README.md).
+"""
+
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path):
+    acc = defaultdict(list)
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+            acc[name].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    fetch, write, out = sys.argv[1:4]
+    label = sys.argv[5] if len(sys.argv) > 5 and sys.argv[4] == "--label" else ""
+    f, w = per_kernel(fetch), per_kernel(write)
+    res = {"_label": label, "_convention": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024, averaged per launch"}
+    for k in sorted(set(f) | set(w)):
+        fk = sum(f.get(k, [0])) / max(len(f.get(k, [])), 1)
+        wk = sum(w.get(k, [0])) / max(len(w.get(k, [])), 1)
+        short = k.split("::")[-1].split("<")[0]
+        res[short] = {"kernel": k, "launches": max(len(f.get(k, [])), len(w.get(k, []))),
+                      "fetch_bytes_per_launch": fk * 1024 * 2, "write_bytes_per_launch": wk * 1024,
+                      "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for k, v in res.items():
+        if not k.startswith("_"):
+            print(f"{k:28s} x{v['launches']:3d}  read {v['fetch_bytes_per_launch'] / 1e9:8.2f} GB  "
+                  f"write {v['write_bytes_per_launch'] / 1e9:8.2f} GB")
+
+
+if __name__ == "__main__":
+    main()

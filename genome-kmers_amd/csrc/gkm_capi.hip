@@ -8,6 +8,7 @@
 //            and finally the starts with >= min_kmer_len bases are kept, in order.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 
@@ -396,6 +397,16 @@ static int presort_by_start(gk_ctx *c) {
 static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     int rc = ensure_elems(c, c->n, ks.words);
     if (rc != GK_OK) return rc;
+    // fixed-length one-word keys from the enumerated starts: stable MSD (gkm_msd.hip)
+    static const bool force_lsd = std::getenv("GKM_SORT_LSD") != nullptr;
+    if (c->enumerated && ks.words == 1 && ks.symbols == ks.min_len && (ks.bits == 2 || ks.bits == 4) && !force_lsd) {
+        rc = msd_sort(c, ks);
+        if (rc != GK_OK) return rc;
+        c->spec = ks;
+        c->keys_valid = true;
+        c->keys_are_ranks = false;
+        return GK_OK;
+    }
     bool hist_ready = false;
     if (c->enumerated) {
         int slot;

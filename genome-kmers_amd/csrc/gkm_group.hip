@@ -626,3 +626,9 @@ hipError_t unique_counts_device(gk_ctx *c) {
     return hipGetLastError();
 }
 }  // namespace gkm
+
+namespace gkm {
+hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {
+    return scan_u32_exclusive(c, in, n, out, total);
+}
+}  // namespace gkm

@@ -12,7 +12,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "gkm.h"
@@ -25,7 +27,7 @@ constexpr int kRadixBits = 8;
 constexpr int kRadixBins = 256;
 constexpr int kMaxWords = 4;          // direct keys up to 256 bits
 constexpr int kEncodeTile = 4096;     // positions per encode tile
-constexpr int kSbaPad = 8192;         // '$' bytes after the sba (>= tile + max symbols)
+constexpr int kSbaPad = 32768;        // '$' bytes after the sba (>= largest tile + max symbols)
 constexpr int kSortThreads = 256;     // radix pass workgroup
 constexpr int kSortItems = 16;        // keys per thread per radix tile
 constexpr int kSortTile = kSortThreads * kSortItems;
@@ -121,6 +123,9 @@ struct gk_ctx {
     uint64_t n_unique = 0;
     bool unique_valid = false;
 
+    // named, grow-only scratch buffers (MSD sort tables etc.)
+    std::map<std::string, std::pair<void *, uint64_t>> scratch;
+
     // profiling
     bool profile = false;
     std::vector<gkm::Timer> timers;
@@ -132,6 +137,16 @@ struct gk_ctx {
 namespace gkm {
 
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
+// grow-only named device scratch buffer of at least `bytes` (contents not preserved on growth)
+template <typename T>
+inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) {
+    auto &e = c->scratch[name];
+    hipError_t r = ensure(&e.first, &e.second, sizeof(T) * (count + 16));
+    *out = static_cast<T *>(e.first);
+    return r;
+}
+// MSD sort of one-word keys from the enumerated positions (gkm_msd.hip)
+int msd_sort(gk_ctx *c, const KeySpec &ks);
 void timer_begin(gk_ctx *c, const char *name, int *slot);
 void timer_end(gk_ctx *c, int slot);
 int fail(gk_ctx *c, int code, const std::string &msg);

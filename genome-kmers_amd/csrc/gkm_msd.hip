@@ -18,13 +18,12 @@
 #include <cstdlib>
 
 #include "gkm_internal.h"
+#include "gkm_partition.h"
 
 namespace gkm {
 
-// partition tile shape: T threads x I items (wave-striped), LDS staging of T*I keys
-constexpr int kPartThreads = 1024;
-constexpr int kPartItems = 12;
-constexpr int kPartTile = kPartThreads * kPartItems;  // 12288
+// partition tile shapes (T threads x I items, wave-striped; LDS staging of T*I keys) are template
+// parameters of the host driver; msd_sort picks one (default 1024 x 12)
 constexpr int kChunkTiles = 256;                       // tiles per scan chunk
 constexpr int kLocalMax = 512;                         // buckets <= this are finished by one wave
 constexpr int kLocalChunks = kLocalMax / 64;
@@ -41,148 +40,6 @@ static hipError_t msd_tables() {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_code4_msd), code4, 256);
     if (e == hipSuccess) g_msd_tables = true;
     return e;
-}
-
-struct Dig {
-    int shift;
-    uint32_t mask;
-};
-
-__host__ __device__ inline Dig digit_at(int B, int l) {
-    int hi = B - 8 * l;
-    int lo = hi - 8;
-    if (lo < 0) lo = 0;
-    return Dig{lo, (1u << (hi - lo)) - 1u};
-}
-
-__host__ __device__ inline int num_digits(int B) { return (B + 7) / 8; }
-
-__device__ __forceinline__ uint32_t dg_of(uint64_t k, Dig d) { return (uint32_t)(k >> d.shift) & d.mask; }
-
-// local-list entry: x = bucket start, y = len << 8 | level << 1 | parity
-__host__ __device__ inline uint2 local_entry(uint32_t start, uint32_t len, int level, int parity) {
-    return make_uint2(start, (len << 8) | ((uint32_t)level << 1) | (uint32_t)parity);
-}
-
-// ---------------------------------------------------------------------------------------------
-// shared building blocks
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool valid) {
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        peers &= bit ? bb : ~bb;
-    }
-    return peers;
-}
-
-// stable 64-lane ranking of I wave-striped items by an 8-bit digit (per-wave LDS counters)
-template <int I>
-__device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool (&valid)[I], uint32_t *s_wc_wave,
-                                           int lane, uint32_t (&rank)[I]) {
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const uint64_t peers = match_peers(dig[i], valid[i]);
-        const int leader = valid[i] ? (__ffsll((unsigned long long)peers) - 1) : lane;
-        const uint32_t rank_in = __popcll(peers & lt_mask);
-        uint32_t old = 0;
-        if (valid[i] && lane == leader) {
-            old = s_wc_wave[dig[i]];
-            s_wc_wave[dig[i]] = old + (uint32_t)__popcll(peers);
-        }
-        old = __shfl(old, leader);
-        rank[i] = old + rank_in;
-    }
-}
-
-template <int T, int I>
-struct PartSmem {
-    static constexpr int kTile = T * I;
-    static constexpr int kWaves = T / 64;
-    static constexpr int kStage = kTile * 8;          // keys, then starts, in digit order
-    static constexpr int kCounters = kWaves * 256 * 4;  // per-wave digit counters (aliased)
-    static constexpr int kUnion = kStage > kCounters ? kStage : kCounters;
-};
-
-// Stable partition of one tile (item i of lane l in wave w = tile element w*I*64 + i*64 + l) by
-// digit d: rank in registers, tile digit starts, then keys and starts are staged in LDS in digit
-// order and written as coalesced runs at tile_off[digit] (global digit offsets of this tile).
-// s_wc (= s_raw) must be zero on entry.  Barriers inside: all T threads must call.
-template <int T, int I>
-__device__ __forceinline__ void partition_tile(const uint64_t (&key)[I], const uint32_t (&val)[I],
-                                               const bool (&valid)[I], Dig d, unsigned char *s_raw,
-                                               uint32_t *s_start, const uint32_t *s_toff, uint32_t *s_wsum,
-                                               uint32_t *s_count, uint64_t *__restrict__ kout,
-                                               uint32_t *__restrict__ vout) {
-    constexpr int NW = T / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
-    uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_raw);
-    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_raw);
-
-    uint32_t dig[I], rank[I];
-#pragma unroll
-    for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
-    rank_items<I>(dig, valid, s_wc + wave * 256, lane, rank);
-    __syncthreads();
-    // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
-    uint32_t total = 0, incl = 0;
-    if (tid < 256) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t v = s_wc[w * 256 + tid];
-            s_wc[w * 256 + tid] = total;
-            total += v;
-        }
-        incl = total;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        if (lane == 63) s_wsum[wave] = incl;
-    }
-    __syncthreads();
-    if (tid < 256) {
-        uint32_t pre = 0;
-        for (int w = 0; w < wave; ++w) pre += s_wsum[w];
-        s_start[tid] = pre + incl - total;
-        if (tid == 255) *s_count = pre + incl;
-    }
-    __syncthreads();
-    uint32_t slot[I];
-#pragma unroll
-    for (int i = 0; i < I; ++i) slot[i] = s_start[dig[i]] + s_wc[wave * 256 + dig[i]] + rank[i];
-    __syncthreads();  // counters consumed: the staging area is reused
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-        if (valid[i]) s_keys[slot[i]] = key[i];
-    __syncthreads();
-    const uint32_t cnt = *s_count;
-    uint32_t o[I];
-#pragma unroll
-    for (int j = 0; j < I; ++j) {
-        const uint32_t s = tid + j * T;
-        if (s < cnt) {
-            const uint64_t k = s_keys[s];
-            const uint32_t dd = dg_of(k, d);
-            o[j] = s_toff[dd] + (s - s_start[dd]);
-            kout[o[j]] = k;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-        if (valid[i]) s_vals[slot[i]] = val[i];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < I; ++j) {
-        const uint32_t s = tid + j * T;
-        if (s < cnt) vout[o[j]] = s_vals[s];
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -203,14 +60,23 @@ struct L0Pack {
     static constexpr int kCodeWords = kGroups * BITS / 2 + 1;  // u64 words (+1 for the funnel)
 };
 
+// thread g < kGroups holds the 32 bytes of group g (two 16-B loads)
 template <int BITS, int TILE>
-__device__ __forceinline__ void l0_pack(const uint8_t *__restrict__ src, uint64_t *s_code, uint32_t *s_dol,
-                                        const uint8_t *lut4, int T) {
+__device__ __forceinline__ void l0_load(const uint8_t *__restrict__ src, uint4 &ra, uint4 &rb) {
+    // threads past kGroups re-load the last group: no branch, so load counts stay static
+    const uint32_t g = min((uint32_t)threadIdx.x, (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src + 32 * g);
+    ra = s4[0];
+    rb = s4[1];
+}
+
+template <int BITS, int TILE>
+__device__ __forceinline__ void l0_pack(const uint4 &ra, const uint4 &rb, uint64_t *s_code, uint32_t *s_dol,
+                                        const uint8_t *lut4) {
     using P = L0Pack<BITS, TILE>;
-    for (int g = threadIdx.x; g < P::kGroups; g += T) {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(src + 32 * g);
-        const uint4 a = s4[0], b = s4[1];
-        const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int g = threadIdx.x;
+    if (g < P::kGroups) {
+        const uint32_t wv[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
         uint64_t c0 = 0, c1 = 0;
         uint32_t dm = 0;
 #pragma unroll
@@ -232,7 +98,7 @@ __device__ __forceinline__ void l0_pack(const uint8_t *__restrict__ src, uint64_
         }
         s_dol[g] = dm;
     }
-    if (threadIdx.x == 0) s_code[P::kCodeWords - 1] = 0;
+    if (g == 0) s_code[P::kCodeWords - 1] = 0;
 }
 
 template <int BITS>
@@ -262,108 +128,72 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
         s_lut4[t] = c_code4_msd[t];
         s_hist[t] = 0;
     }
-    __syncthreads();
+    lds_barrier();
     const uint64_t P0 = (uint64_t)blockIdx.x * TILE;
-    l0_pack<BITS, TILE>(a.sba + P0, s_code, s_dol, s_lut4, T);
-    __syncthreads();
+    uint4 ra, rb;
+    l0_load<BITS, TILE>(a.sba + P0, ra, rb);
+    l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         const uint32_t p = i * T + t;
         if (l0_valid(s_dol, p, a.symbols)) atomicAdd(&s_hist[dg_of(l0_key<BITS>(s_code, p, a.total_bits), d0)], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     if (t < 256) tile_hist[(uint64_t)blockIdx.x * 256 + t] = s_hist[t];
 }
 
+// persistent (see msd_scatter_kernel): the next tile's bytes are loaded while runs are stored
 template <int BITS, int T, int I>
 __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
-                                                         uint64_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+                                                         uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                         uint32_t ntiles, uint64_t sink) {
     constexpr int TILE = T * I;
     using P = L0Pack<BITS, TILE>;
     using SM = PartSmem<T, I>;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
     __shared__ uint64_t s_code[P::kCodeWords];
     __shared__ uint32_t s_dol[P::kGroups];
-    __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_toff[256];
     __shared__ uint32_t s_wsum[4];
     __shared__ uint32_t s_count;
     __shared__ uint8_t s_lut4[256];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t P0 = tile * TILE;
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
-    for (int i = tid; i < SM::kWaves * 256; i += T) s_wc[i] = 0;
-    if (tid < 256) {
-        s_lut4[tid] = c_code4_msd[tid];
-        s_toff[tid] = tile_off[tile * 256 + tid];
-    }
-    __syncthreads();
-    l0_pack<BITS, TILE>(a.sba + P0, s_code, s_dol, s_lut4, T);
-    __syncthreads();
-    uint64_t key[I];
-    uint32_t val[I];
-    bool valid[I];
+    if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    const TileWalk walk(ntiles);
+    uint4 ra, rb;
+    uint32_t toff = 0;
+    auto load = [&](uint32_t t) {
+        l0_load<BITS, TILE>(a.sba + (uint64_t)t * TILE, ra, rb);
+        toff = tile_off[(uint64_t)t * 256 + (tid & 255)];  // every lane loads: no branch
+    };
+    if (walk.first < walk.end) load(walk.first);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see msd_scatter_kernel
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        lds_barrier();  // the previous tile's runs have been read out of LDS
+        for (int i = tid; i < SM::kWaves * 256; i += T) s_wc[i] = 0;
+        if (tid < 256) s_toff[tid] = toff;
+        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+        lds_barrier();
+        const uint64_t P0 = (uint64_t)t * TILE;
+        uint64_t key[I];
+        uint32_t val[I];
+        bool valid[I];
+        uint32_t p0 = wave * (I * 64) + lane;
+        asm volatile("" : "+v"(p0));  // keep the per-item offsets inside the loop (no hoisting)
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const uint32_t p = wave * (I * 64) + i * 64 + lane;
-        valid[i] = l0_valid(s_dol, p, a.symbols);
-        key[i] = l0_key<BITS>(s_code, p, a.total_bits);
-        val[i] = (uint32_t)(P0 + p);
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = p0 + i * 64;
+            valid[i] = l0_valid(s_dol, p, a.symbols);
+            key[i] = l0_key<BITS>(s_code, p, a.total_bits);
+            val[i] = (uint32_t)(P0 + p);
+        }
+        partition_stage<T, I>(key, val, valid, d0, s_raw, s_toff, s_wsum, &s_count);
+        const uint32_t cnt = s_count;
+        if (t + walk.step < walk.end) load(t + walk.step);
+        partition_store<T, I, 0>(d0, s_raw, s_toff, cnt, sink, kout, vout);
     }
-    partition_tile<T, I>(key, val, valid, d0, s_raw, s_start, s_toff, s_wsum, &s_count, kout, vout);
-}
-
-// ---------------------------------------------------------------------------------------------
-// L>=1: partition big buckets; tiles never cross bucket boundaries
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void msd_count_kernel(const uint32_t *__restrict__ t_start,
-                                                        const uint32_t *__restrict__ t_count, Dig dl,
-                                                        const uint64_t *__restrict__ kin,
-                                                        uint32_t *__restrict__ tile_hist) {
-    __shared__ uint32_t s_hist[256];
-    const int t = threadIdx.x;
-    s_hist[t] = 0;
-    __syncthreads();
-    const uint64_t b = t_start[blockIdx.x];
-    const uint32_t m = t_count[blockIdx.x];
-    for (uint32_t i = t; i < m; i += 256) atomicAdd(&s_hist[dg_of(kin[b + i], dl)], 1u);
-    __syncthreads();
-    tile_hist[(uint64_t)blockIdx.x * 256 + t] = s_hist[t];
-}
-
-template <int T, int I>
-__global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restrict__ t_start,
-                                                        const uint32_t *__restrict__ t_count, Dig dl,
-                                                        const uint32_t *__restrict__ tile_off,
-                                                        const uint64_t *__restrict__ kin,
-                                                        const uint32_t *__restrict__ vin, uint64_t *__restrict__ kout,
-                                                        uint32_t *__restrict__ vout) {
-    using SM = PartSmem<T, I>;
-    __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
-    __shared__ uint32_t s_start[256];
-    __shared__ uint32_t s_toff[256];
-    __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_count;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t b = t_start[tile];
-    const uint32_t m = t_count[tile];
-    uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
-    for (int i = tid; i < SM::kWaves * 256; i += T) s_wc[i] = 0;
-    if (tid < 256) s_toff[tid] = tile_off[tile * 256 + tid];
-    uint64_t key[I];
-    uint32_t val[I];
-    bool valid[I];
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const uint32_t q = wave * (I * 64) + i * 64 + lane;
-        valid[i] = q < m;
-        key[i] = valid[i] ? kin[b + q] : 0;
-        val[i] = valid[i] ? vin[b + q] : 0;
-    }
-    __syncthreads();
-    partition_tile<T, I>(key, val, valid, dl, s_raw, s_start, s_toff, s_wsum, &s_count, kout, vout);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -502,16 +332,16 @@ __global__ __launch_bounds__(256) void classify_kernel(const uint32_t *__restric
 __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restrict__ s_start,
                                                          const uint32_t *__restrict__ s_len,
                                                          const uint32_t *__restrict__ s_tfirst,
-                                                         const uint32_t *__restrict__ s_cfirst, uint32_t nseg,
+                                                         const uint32_t *__restrict__ s_cfirst, uint32_t nseg, uint32_t tile,
                                                          uint32_t *__restrict__ t_start, uint32_t *__restrict__ t_count,
                                                          uint32_t *__restrict__ c_first, uint32_t *__restrict__ c_ntiles) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
     const uint32_t st = s_start[s], len = s_len[s], tf = s_tfirst[s], cf = s_cfirst[s];
-    const uint32_t nt = (len + kPartTile - 1) / kPartTile;
+    const uint32_t nt = (len + tile - 1) / tile;
     for (uint32_t j = 0; j < nt; ++j) {
-        t_start[tf + j] = st + j * kPartTile;
-        t_count[tf + j] = std::min<uint32_t>(kPartTile, len - j * kPartTile);
+        t_start[tf + j] = st + j * tile;
+        t_count[tf + j] = std::min<uint32_t>(tile, len - j * tile);
     }
     const uint32_t nc = (nt + kChunkTiles - 1) / kChunkTiles;
     for (uint32_t j = 0; j < nc; ++j) {
@@ -520,11 +350,11 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restr
     }
 }
 
-__global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg,
+__global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg, uint32_t tile,
                                                          uint32_t *__restrict__ ntiles, uint32_t *__restrict__ nchunks) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
-    const uint32_t nt = (s_len[s] + kPartTile - 1) / kPartTile;
+    const uint32_t nt = (s_len[s] + tile - 1) / tile;
     ntiles[s] = nt;
     nchunks[s] = (nt + kChunkTiles - 1) / kChunkTiles;
 }
@@ -544,7 +374,6 @@ __global__ __launch_bounds__(64) void msd_local_kernel(const uint2 *__restrict__
     __shared__ uint32_t s_cnt[256];
     __shared__ uint32_t s_strt[256];
     const int lane = threadIdx.x;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint2 e = list[blockIdx.x];
     const uint64_t st = e.x;
     const uint32_t len = e.y >> 8;
@@ -601,14 +430,10 @@ __global__ __launch_bounds__(64) void msd_local_kernel(const uint2 *__restrict__
         const bool valid = c * 64 + lane < len;
         const uint32_t d = dg_of(key[c], dd);
         const uint64_t peers = match_peers(d, valid);
-        const int leader = valid ? (__ffsll((unsigned long long)peers) - 1) : lane;
-        uint32_t old = 0;
-        if (valid && lane == leader) {
-            old = s_cnt[d];
-            s_cnt[d] = old + (uint32_t)__popcll(peers);
-        }
-        old = __shfl(old, leader);
-        rk[c] = old + __popcll(peers & lt_mask);
+        const uint32_t rank_in = lanes_below(peers);
+        const uint32_t old = s_cnt[d];
+        if (valid && rank_in == 0) s_cnt[d] = old + (uint32_t)__popcll(peers);
+        rk[c] = old + rank_in;
     }
     {
         uint32_t c4[4], s4 = 0;
@@ -737,13 +562,23 @@ static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t
     return hipSuccess;
 }
 
+// partition grid: 4 workgroups per CU (one resident at a time: LDS-bound), a multiple of 8 (equal
+// shares per XCD); measured 4% faster than exactly one per CU (profiles/r1/README.md)
+static unsigned persistent_grid(gk_ctx *c) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus < 8) cus = 256;
+    return (unsigned)(cus / 8 * 8 * 4);
+}
+
 static int read_ctr(gk_ctx *c, const uint32_t *d, uint32_t *h, int count) {
     GK_TRY_HIP(c, hipMemcpyAsync(h, d, 4 * count, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     return GK_OK;
 }
 
-int msd_sort(gk_ctx *c, const KeySpec &ks) {
+template <int PT, int PI>
+static int msd_sort_shape(gk_ctx *c, const KeySpec &ks) {
+    constexpr uint32_t kPartTile = PT * PI;
     GK_TRY_HIP(c, msd_tables());
     int total_slot;
     timer_begin(c, "msd_total", &total_slot);
@@ -778,12 +613,13 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     }
     L0Args a{c->sba, ks.symbols, B};
     const Dig d0 = digit_at(B, 0);
+    const unsigned pgrid = persistent_grid(c);
     int slot;
     timer_begin(c, "msd_l0_count", &slot);
     if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_count_kernel<2, kPartThreads, kPartItems>), dim3((unsigned)nt0), dim3(kPartThreads), 0, c->stream, a, d0, tile_hist);
+        hipLaunchKernelGGL((msd0_count_kernel<2, PT, PI>), dim3((unsigned)nt0), dim3(PT), 0, c->stream, a, d0, tile_hist);
     else
-        hipLaunchKernelGGL((msd0_count_kernel<4, kPartThreads, kPartItems>), dim3((unsigned)nt0), dim3(kPartThreads), 0, c->stream, a, d0, tile_hist);
+        hipLaunchKernelGGL((msd0_count_kernel<4, PT, PI>), dim3((unsigned)nt0), dim3(PT), 0, c->stream, a, d0, tile_hist);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     timer_begin(c, "msd_scan", &slot);
@@ -793,11 +629,11 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     timer_end(c, slot);
     timer_begin(c, "msd_pass_l0", &slot);
     if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_scatter_kernel<2, kPartThreads, kPartItems>), dim3((unsigned)nt0), dim3(kPartThreads), 0, c->stream, a, d0, tile_hist,
-                           c->keys[0], c->vals[0]);
+        hipLaunchKernelGGL((msd0_scatter_kernel<2, PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, a, d0, tile_hist,
+                           c->keys[0], c->vals[0], (uint32_t)nt0, n);
     else
-        hipLaunchKernelGGL((msd0_scatter_kernel<4, kPartThreads, kPartItems>), dim3((unsigned)nt0), dim3(kPartThreads), 0, c->stream, a, d0, tile_hist,
-                           c->keys[0], c->vals[0]);
+        hipLaunchKernelGGL((msd0_scatter_kernel<4, PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, a, d0, tile_hist,
+                           c->keys[0], c->vals[0], (uint32_t)nt0, n);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
 
@@ -833,7 +669,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
         GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
         hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig, 1 << 30)), dim3(256), 0, c->stream, lst_len[li], nbig,
-                           ntl, nch);
+                           kPartTile, ntl, nch);
         GK_TRY_HIP(c, hipGetLastError());
         uint64_t T = 0, C = 0;
         GK_TRY_HIP(c, scan_u32_exclusive_pub(c, ntl, nbig, tfirst, &T));
@@ -849,7 +685,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         GK_TRY_HIP(c, scratch(c, "seg_cnt", (uint64_t)nbig * 256, &seg_cnt));
         GK_TRY_HIP(c, grow_keep(c, "local", (uint64_t)nlocal + 256ull * nbig, nlocal, &local));
         hipLaunchKernelGGL(tile_table_kernel, dim3(grid_n(nbig, 1 << 30)), dim3(256), 0, c->stream, lst_start[li],
-                           lst_len[li], tfirst, cfirst, nbig, t_start, t_count, c_first, c_ntiles);
+                           lst_len[li], tfirst, cfirst, nbig, kPartTile, t_start, t_count, c_first, c_ntiles);
         const Dig dl = digit_at(B, level);
         timer_begin(c, "msd_count", &slot);
         hipLaunchKernelGGL(msd_count_kernel, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
@@ -864,8 +700,8 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                            "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
         timer_begin(c, kPassNames[level & 7], &slot);
-        hipLaunchKernelGGL((msd_scatter_kernel<kPartThreads, kPartItems>), dim3((unsigned)T), dim3(kPartThreads), 0, c->stream, t_start, t_count, dl,
-                           tile_hist, c->keys[in], c->vals[in], c->keys[out], c->vals[out]);
+        hipLaunchKernelGGL((msd_scatter_kernel<PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, t_start, t_count, dl,
+                           tile_hist, c->keys[in], c->vals[in], c->keys[out], c->vals[out], (uint32_t)T, n);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         const bool has_next = level + 1 < D;
@@ -915,6 +751,17 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     timer_end(c, total_slot);
     c->cur = 0;
     return GK_OK;
+}
+
+int msd_sort(gk_ctx *c, const KeySpec &ks) {
+    const char *e = getenv("GKM_MSD_SHAPE");  // tuning experiments only
+    const int shape = e ? atoi(e) : 0;
+    switch (shape) {
+    case 1: return msd_sort_shape<512, 12>(c, ks);
+    case 2: return msd_sort_shape<512, 16>(c, ks);
+    case 3: return msd_sort_shape<256, 16>(c, ks);
+    default: return msd_sort_shape<1024, 12>(c, ks);
+    }
 }
 
 }  // namespace gkm

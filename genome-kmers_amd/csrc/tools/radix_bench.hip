@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../gkm_onesweep.h"
+#include "../gkm_partition.h"
 
 #define CK(x)                                                                                   \
     do {                                                                                        \
@@ -73,6 +74,133 @@ struct Bufs {
     uint64_t n;
     uint32_t epoch = 0;
 };
+
+// ideal uniform partition: tile t sends R = TILE/256 consecutive elements to each digit region,
+// landing next to tile t-1's run -- the memory-side ceiling of a partition pass with runs of R
+// one MSD partition pass (production msd_scatter_kernel) over the whole array as one bucket
+struct MsdTables {
+    uint32_t *t_start = nullptr, *t_count = nullptr, *tile_off = nullptr;
+    uint64_t tiles = 0;
+    int tile = 0;
+};
+
+static void msd_tables_for(Bufs &b, hipStream_t st, int tile, MsdTables &m) {
+    if (m.tile == tile) return;
+    if (m.t_start) {
+        CK(hipFree(m.t_start));
+        CK(hipFree(m.t_count));
+        CK(hipFree(m.tile_off));
+    }
+    m.tile = tile;
+    m.tiles = (b.n + tile - 1) / tile;
+    std::vector<uint32_t> ts(m.tiles), tc(m.tiles);
+    for (uint64_t j = 0; j < m.tiles; ++j) {
+        ts[j] = (uint32_t)(j * tile);
+        tc[j] = (uint32_t)std::min<uint64_t>(tile, b.n - j * tile);
+    }
+    CK(hipMalloc(&m.t_start, 4 * m.tiles));
+    CK(hipMalloc(&m.t_count, 4 * m.tiles));
+    CK(hipMalloc(&m.tile_off, 4 * 256 * m.tiles));
+    CK(hipMemcpy(m.t_start, ts.data(), 4 * m.tiles, hipMemcpyHostToDevice));
+    CK(hipMemcpy(m.t_count, tc.data(), 4 * m.tiles, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(msd_count_kernel, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count, Dig{54, 255u},
+                       b.k[0], m.tile_off);
+    CK(hipStreamSynchronize(st));
+    std::vector<uint32_t> h(256 * m.tiles);
+    CK(hipMemcpy(h.data(), m.tile_off, 4 * 256 * m.tiles, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> tot(256, 0);
+    for (uint64_t j = 0; j < m.tiles; ++j)
+        for (int d = 0; d < 256; ++d) tot[d] += h[j * 256 + d];
+    std::vector<uint64_t> run(256);
+    uint64_t r = 0;
+    for (int d = 0; d < 256; ++d) {
+        run[d] = r;
+        r += tot[d];
+    }
+    for (uint64_t j = 0; j < m.tiles; ++j)
+        for (int d = 0; d < 256; ++d) {
+            const uint32_t c = h[j * 256 + d];
+            h[j * 256 + d] = (uint32_t)run[d];
+            run[d] += c;
+        }
+    CK(hipMemcpy(m.tile_off, h.data(), 4 * 256 * m.tiles, hipMemcpyHostToDevice));
+}
+
+template <int T, int I, int MODE>
+static void run_msd(Bufs &b, MsdTables &m, const char *name, hipStream_t st, unsigned long long ref_sum,
+                    unsigned grid = 256) {
+    msd_tables_for(b, st, T * I, m);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float tot = 0, best = 1e30f;
+    const int R = 4;
+    for (int r = 0; r <= R; ++r) {
+        CK(hipEventRecord(e0, st));
+        hipLaunchKernelGGL((msd_scatter_kernel<T, I, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+                           Dig{54, 255u}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r) {
+            tot += ms;
+            best = std::min(best, ms);
+        }
+    }
+    const char *verdict = "-";
+    if (MODE == 0) {
+        unsigned long long *d;
+        CK(hipMalloc(&d, 16));
+        CK(hipMemset(d, 0, 16));
+        hipLaunchKernelGGL(check_kernel, dim3(2048), dim3(256), 0, st, b.k[1], b.v[1], b.n, 54, d, d + 1);
+        unsigned long long hh[2];
+        CK(hipMemcpy(hh, d, 16, hipMemcpyDeviceToHost));
+        CK(hipFree(d));
+        verdict = (hh[0] == 0 && hh[1] == ref_sum) ? "sorted" : "WRONG";
+    }
+    std::printf("%-34s tile %6d  avg %8.3f ms  best %8.3f ms  %7.1f GB/s (24 B/key)  %s\n", name, T * I, tot / R, best,
+                b.n * 24.0 / (best * 1e-3) / 1e9, verdict);
+}
+
+template <int TILE>
+__global__ __launch_bounds__(256) void runscatter_kernel(const uint64_t *__restrict__ k, const uint32_t *__restrict__ v,
+                                                         uint64_t *__restrict__ ko, uint32_t *__restrict__ vo,
+                                                         uint64_t n, uint64_t stride) {
+    constexpr int R = TILE / 256;
+    const uint64_t t = blockIdx.x;
+    for (int s = threadIdx.x; s < TILE; s += 256) {
+        const uint64_t e = t * TILE + s;
+        const uint64_t o = (uint64_t)(s / R) * stride + t * R + (s % R);
+        if (e < n && o < n) {
+            ko[o] = k[e];
+            vo[o] = v[e];
+        }
+    }
+}
+
+template <int TILE>
+static void run_scatter(Bufs &b, hipStream_t st) {
+    const uint64_t nt = (b.n + TILE - 1) / TILE;
+    const uint64_t stride = nt * (TILE / 256);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float tot = 0;
+    for (int r = 0; r < 4; ++r) {
+        CK(hipEventRecord(e0, st));
+        hipLaunchKernelGGL(runscatter_kernel<TILE>, dim3((unsigned)nt), dim3(256), 0, st, b.k[0], b.v[0], b.k[1], b.v[1],
+                           b.n, stride);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r) tot += ms;
+    }
+    std::printf("ideal run scatter, run %4d keys   tile %6d  avg %8.3f ms                  %7.1f GB/s\n", TILE / 256,
+                TILE, tot / 3, b.n * 24.0 / (tot / 3 * 1e-3) / 1e9);
+}
+
 
 template <int T, int I, bool LB>
 float run_variant(Bufs &b, const char *name, hipStream_t st, int reps, unsigned long long ref_sum) {
@@ -176,6 +304,18 @@ int main(int argc, char **argv) {
         std::printf("%-34s                avg %8.3f ms                  %7.1f GB/s\n", "copy keys+vals (uint4)", tot / 3,
                     n * 24.0 / (tot / 3 * 1e-3) / 1e9);
     }
+    run_scatter<4096>(b, st);
+    run_scatter<12288>(b, st);
+    run_scatter<24576>(b, st);
+    run_scatter<49152>(b, st);
+    run_scatter<98304>(b, st);
+    MsdTables m;
+    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12", st, ref_sum);
+    run_msd<1024, 12, 1>(b, m, "msd pass T1024 I12 no-store", st, ref_sum);
+    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12 grid 512", st, ref_sum, 512);
+    run_msd<1024, 12, 3>(b, m, "msd pass T1024 I12 seq-store", st, ref_sum);
+    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12 grid 1024", st, ref_sum, 1024);
+    if (argc > 2) return 0;
     const int R = 4;
     run_variant<256, 16, true>(b, "onesweep T256 I16 (current)", st, R, ref_sum);
     run_variant<256, 16, false>(b, "onesweep T256 I16 no-lookback", st, R, ref_sum);

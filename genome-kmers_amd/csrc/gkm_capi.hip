@@ -301,7 +301,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     uint32_t h[2] = {0, 0};
     GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = false;
+    c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = false;
     c->n = 0;
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;
@@ -343,7 +343,7 @@ extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
     c->have_starts = true;
     c->enumerated = true;
     c->starts_materialized = false;
-    c->sorted = c->keys_valid = c->unique_valid = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
     if (n_out) *n_out = n;
     return GK_OK;
 }
@@ -364,7 +364,7 @@ extern "C" int gk_set_start_indices(gk_ctx *c, const uint32_t *src, uint64_t n, 
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
     return GK_OK;
 }
 
@@ -550,7 +550,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         if (bad) return fail(c, GK_E_NO_BASES, "kmers compared were less than min_kmer_len");
     }
-    c->unique_valid = false;
+    c->unique_valid = c->heads_valid = false;
     int rc;
     if (c->n < 2) {
         rc = materialize_starts(c);

@@ -97,21 +97,39 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
+// Striped: thread t of the tile owns positions base + 256 k + t (k < 16), so the selected
+// positions of a row are ranked with one ballot per wave and written as contiguous runs.
 __global__ __launch_bounds__(kScanThreads) void flag_select_kernel(const uint8_t *__restrict__ f, uint64_t n,
                                                                    const uint32_t *__restrict__ tile_off,
                                                                    uint32_t *__restrict__ out) {
-    __shared__ uint32_t s_tmp[kScanThreads / 64];
-    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
-    uint8_t v[16];
-    load16_flags(f, n, at, v);
-    uint32_t cnt = 0;
+    constexpr int NW = kScanThreads / 64;
+    __shared__ uint32_t s_cnt[kScanItems][NW];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
+    bool sel[kScanItems];
+    uint32_t below[kScanItems];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
-    uint32_t tot;
-    uint32_t o = tile_off[blockIdx.x] + block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t p = base + (uint64_t)k * kScanThreads;
+        sel[k] = p < n && f[p] != 0;
+        const uint64_t m = __ballot(sel[k]);
+        below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_cnt[k][wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint32_t run = tile_off[blockIdx.x];
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (v[k]) out[o++] = (uint32_t)(at + k);
+    for (int k = 0; k < kScanItems; ++k) {
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t x = s_cnt[k][w];
+            pre += w < wave ? x : 0u;
+            tot += x;
+        }
+        if (sel[k]) out[run + pre + below[k]] = (uint32_t)(base + (uint64_t)k * kScanThreads);
+        run += tot;
+    }
 }
 
 __global__ __launch_bounds__(kScanThreads) void flag_scan_incl_kernel(const uint8_t *__restrict__ f, uint64_t n,
@@ -461,7 +479,11 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
     }
 
     // 3. heads
-    if (!is_sorted) {
+    const uint8_t *heads = c->flags;
+    if (is_sorted && kind == GK_FILTER_KEEP_ALL && c->heads_valid && c->keys_valid && !c->keys_are_ranks &&
+        c->spec.lenbits == 0 && kmer_len == c->spec.symbols) {
+        heads = c->heads;  // full-key heads written by the MSD sort (gkm_msd.hip)
+    } else if (!is_sorted) {
         // compare_sba_kmers_always_less_than: every valid k-mer starts a group (kmers.py:295-303, 957-960)
         GK_TRY_HIP(c, hipMemsetAsync(c->flags, 1, cnt, c->stream));
     } else {
@@ -508,7 +530,7 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
     }
     // 4. group starts
     uint64_t g = 0;
-    GK_TRY_HIP(c, select_flags(c, c->flags, cnt, c->idx_b, &g));
+    GK_TRY_HIP(c, select_flags(c, heads, cnt, c->idx_b, &g));
     *G = g;
     return GK_OK;
 }

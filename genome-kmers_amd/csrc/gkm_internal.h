@@ -119,6 +119,11 @@ struct gk_ctx {
     uint64_t *onum = nullptr;
     uint64_t ym_cap = 0, yoff_cap = 0, oy_cap = 0, ot_cap = 0, onum_cap = 0;
 
+    // full-key group heads of the sorted order (1 = key differs from its predecessor), written
+    // by the MSD sort as it finishes buckets; valid until the k-mer set or its order changes
+    uint8_t *heads = nullptr;
+    bool heads_valid = false;
+
     // unique view
     uint64_t n_unique = 0;
     bool unique_valid = false;

@@ -1,19 +1,21 @@
-// gkm_msd.hip -- stable MSD radix sort of one-word k-mer keys (the C3 hot path), gfx950.
+// gkm_msd.hip -- MSD radix sort of one-word k-mer keys (the C3 hot path), gfx950.
 //
-// Why MSD: an LSD sort of 62-bit keys moves every (key, start) pair 8 times.  Here each pass
-// partitions only what is still unsorted, and the tail is finished one bucket per wave:
+// An LSD sort of 62-bit keys moves every (key, start) pair 8 times.  Here each pass partitions
+// only what is still unsorted, and buckets small enough for LDS are finished there:
 //   L0     encode + partition by the top 8 bits, straight from the sequence byte array
-//   L1..   partition every bucket larger than kLocalMax by the next 8 bits (big buckets only)
-//   local  every bucket <= kLocalMax: one wave loads it, counting-sorts it by the next digit in
-//          LDS, finishes sub-buckets <= kSmall by rank-by-count, writes it once; larger
-//          sub-buckets spill to another round (one more digit each round).
-// For 3.1e9 random 31-mers: L0, L1, L2 and one local round -- 4 movements instead of 8.
+//   L1..   partition every bucket larger than kBlockMax by the next 8 bits
+//   local  buckets of kWaveMax+1..kBlockMax elements: one 256-thread workgroup each; buckets of
+//          1..kWaveMax: one wave each.  The bucket is partitioned by its next digit in LDS,
+//          sub-buckets of <= kSmall are finished by rank-by-count, and the bucket is written
+//          back once, with its group-head flags; larger sub-buckets go to another round.
+// For 3.1e9 random 31-mers: L0, L1, L2 and one wave-local round -- 4 movements of the data.
 //
-// Every partition is STABLE (64-lane ballot-match ranking, tiles in input order) and every
-// partition offset is known before the scatter starts (count pass + column scan of per-tile
-// digit histograms): no decoupled look-back chain.  Stability + ascending-start input make equal
-// k-mers come out ordered by start index, the reference's break_ties=True order
-// (kmers.py:1710-1711); a bucket whose key bits are exhausted is already in final order.
+// Order contract: equal keys come out by ascending start index, the reference's break_ties=True
+// order (kmers.py:1710-1711).  Every partition here is STABLE (64-lane ballot-match ranking,
+// tiles and workgroups in input order) and the L0 input is in ascending start order, so equal
+// keys stay in start order without ever comparing starts; a sub-bucket whose key bits are
+// exhausted is final as it stands.  Every global partition offset is known before its scatter
+// starts (count pass + column scan of per-tile digit histograms): no look-back chain.
 #include <algorithm>
 #include <cstdlib>
 
@@ -22,12 +24,16 @@
 
 namespace gkm {
 
-// partition tile shapes (T threads x I items, wave-striped; LDS staging of T*I keys) are template
-// parameters of the host driver; msd_sort picks one (default 1024 x 12)
-constexpr int kChunkTiles = 256;                       // tiles per scan chunk
-constexpr int kLocalMax = 512;                         // buckets <= this are finished by one wave
-constexpr int kLocalChunks = kLocalMax / 64;
-constexpr int kSmall = 24;                             // sub-buckets <= this: rank-by-count
+constexpr int kGR = 8;                  // global digit bits
+constexpr int kGRadix = 1 << kGR;
+constexpr int kPT = 1024, kPI = 12;     // global partition tile: 1024 threads x 12 keys
+constexpr int kPTile = kPT * kPI;
+constexpr int kChunkTiles = 256;        // tiles per scan chunk
+constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
+constexpr int kBlockMax = kBT * kBI;    // 4096
+constexpr int kWT = 64, kWI = 4, kWR = 6;    // wave-local: 64 threads x 4 keys, 6-bit digit
+constexpr int kWaveMax = kWT * kWI;     // 256
+constexpr int kSmall = 24;              // sub-buckets <= this: rank-by-count
 
 __constant__ uint8_t c_code4_msd[256];
 static bool g_msd_tables = false;
@@ -115,19 +121,18 @@ __device__ __forceinline__ bool l0_valid(const uint32_t *s_dol, uint32_t p, int 
     return (x >> (64 - S)) == 0;
 }
 
-template <int BITS, int T, int I>
+template <int BITS, int T, int I, int R>
 __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_t *__restrict__ tile_hist) {
     constexpr int TILE = T * I;
+    constexpr int RADIX = 1 << R;
     using P = L0Pack<BITS, TILE>;
     __shared__ uint64_t s_code[P::kCodeWords];
     __shared__ uint32_t s_dol[P::kGroups];
-    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_hist[RADIX];
     __shared__ uint8_t s_lut4[256];
     const int t = threadIdx.x;
-    if (t < 256) {
-        s_lut4[t] = c_code4_msd[t];
-        s_hist[t] = 0;
-    }
+    if (t < 256) s_lut4[t] = c_code4_msd[t];
+    for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
     lds_barrier();
     const uint64_t P0 = (uint64_t)blockIdx.x * TILE;
     uint4 ra, rb;
@@ -140,23 +145,24 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
         if (l0_valid(s_dol, p, a.symbols)) atomicAdd(&s_hist[dg_of(l0_key<BITS>(s_code, p, a.total_bits), d0)], 1u);
     }
     lds_barrier();
-    if (t < 256) tile_hist[(uint64_t)blockIdx.x * 256 + t] = s_hist[t];
+    for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
 }
 
 // persistent (see msd_scatter_kernel): the next tile's bytes are loaded while runs are stored
-template <int BITS, int T, int I>
+template <int BITS, int T, int I, int R>
 __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                          uint32_t ntiles, uint64_t sink) {
     constexpr int TILE = T * I;
     using P = L0Pack<BITS, TILE>;
-    using SM = PartSmem<T, I>;
+    using SM = PartSmem<T, I, R>;
+    constexpr int RADIX = SM::kRadix;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
     __shared__ uint64_t s_code[P::kCodeWords];
     __shared__ uint32_t s_dol[P::kGroups];
-    __shared__ uint32_t s_toff[256];
-    __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_count;
+    __shared__ uint32_t s_toff[RADIX];
+    __shared__ uint32_t s_wsum[SM::kWaves];
+    __shared__ uint32_t s_start[RADIX + 1];
     __shared__ uint8_t s_lut4[256];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
@@ -166,19 +172,19 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
         l0_load<BITS, TILE>(a.sba + (uint64_t)t * TILE, ra, rb);
-        toff = tile_off[(uint64_t)t * 256 + (tid & 255)];  // every lane loads: no branch
+        toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
     };
     if (walk.first < walk.end) load(walk.first);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see msd_scatter_kernel
     for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
         lds_barrier();  // the previous tile's runs have been read out of LDS
-        for (int i = tid; i < SM::kWaves * 256; i += T) s_wc[i] = 0;
-        if (tid < 256) s_toff[tid] = toff;
+        for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
+        if (tid < RADIX) s_toff[tid] = toff;
         l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
         lds_barrier();
         const uint64_t P0 = (uint64_t)t * TILE;
         uint64_t key[I];
-        uint32_t val[I];
+        uint32_t val[I], slot[I];
         bool valid[I];
         uint32_t p0 = wave * (I * 64) + lane;
         asm volatile("" : "+v"(p0));  // keep the per-item offsets inside the loop (no hoisting)
@@ -189,20 +195,22 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
             key[i] = l0_key<BITS>(s_code, p, a.total_bits);
             val[i] = (uint32_t)(P0 + p);
         }
-        partition_stage<T, I>(key, val, valid, d0, s_raw, s_toff, s_wsum, &s_count);
-        const uint32_t cnt = s_count;
+        partition_stage<T, I, R>(key, val, valid, d0, s_raw, s_toff, s_wsum, s_start, slot);
+        const uint32_t cnt = s_start[RADIX];
         if (t + walk.step < walk.end) load(t + walk.step);
-        partition_store<T, I, 0>(d0, s_raw, s_toff, cnt, sink, kout, vout);
+        partition_store<T, I, R, 0>(d0, s_raw, s_toff, cnt, sink, kout, vout);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // column-wise segmented exclusive scan of per-tile digit histograms -> per-tile digit offsets
+// (one thread per digit: blockDim = RADIX)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void chunk_sum_kernel(const uint32_t *__restrict__ tile_hist,
-                                                        const uint32_t *__restrict__ c_first,
-                                                        const uint32_t *__restrict__ c_ntiles,
-                                                        uint32_t *__restrict__ chunk_hist) {
+template <int RADIX>
+__global__ __launch_bounds__(RADIX) void chunk_sum_kernel(const uint32_t *__restrict__ tile_hist,
+                                                          const uint32_t *__restrict__ c_first,
+                                                          const uint32_t *__restrict__ c_ntiles,
+                                                          uint32_t *__restrict__ chunk_hist) {
     const int d = threadIdx.x;
     const uint64_t f = c_first[blockIdx.x];
     const uint32_t nt = c_ntiles[blockIdx.x];
@@ -211,39 +219,29 @@ __global__ __launch_bounds__(256) void chunk_sum_kernel(const uint32_t *__restri
     for (; i + 8 <= nt; i += 8) {
         uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = tile_hist[(f + i + u) * 256 + d];
+        for (int u = 0; u < 8; ++u) v[u] = tile_hist[(f + i + u) * RADIX + d];
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; i < nt; ++i) acc += tile_hist[(f + i) * 256 + d];
-    chunk_hist[(uint64_t)blockIdx.x * 256 + d] = acc;
+    for (; i < nt; ++i) acc += tile_hist[(f + i) * RADIX + d];
+    chunk_hist[(uint64_t)blockIdx.x * RADIX + d] = acc;
 }
 
 // one block per bucket: chunk bases within the bucket, digit bases, digit counts
-__global__ __launch_bounds__(256) void seg_scan_kernel(uint32_t *__restrict__ chunk_hist,
-                                                       const uint32_t *__restrict__ s_cfirst,
-                                                       const uint32_t *__restrict__ s_nchunks,
-                                                       const uint32_t *__restrict__ s_start,
-                                                       uint32_t *__restrict__ seg_base, uint32_t *__restrict__ seg_cnt) {
-    __shared__ uint32_t s_wsum[4];
+template <int RADIX>
+__global__ __launch_bounds__(RADIX) void seg_scan_kernel(uint32_t *__restrict__ chunk_hist,
+                                                         const uint32_t *__restrict__ s_cfirst,
+                                                         const uint32_t *__restrict__ s_nchunks,
+                                                         const uint32_t *__restrict__ s_start,
+                                                         uint32_t *__restrict__ seg_base, uint32_t *__restrict__ seg_cnt) {
+    __shared__ uint32_t s_wsum[RADIX / 64];
     const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
     const uint64_t cf = s_cfirst[blockIdx.x];
     const uint32_t nc = s_nchunks[blockIdx.x];
     uint32_t run = 0;
-    uint32_t i = 0;
-    for (; i + 8 <= nc; i += 8) {
-        uint32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = chunk_hist[(cf + i + u) * 256 + d];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            chunk_hist[(cf + i + u) * 256 + d] = run;
-            run += v[u];
-        }
-    }
-    for (; i < nc; ++i) {
-        const uint32_t v = chunk_hist[(cf + i) * 256 + d];
-        chunk_hist[(cf + i) * 256 + d] = run;
+    for (uint32_t i = 0; i < nc; ++i) {
+        const uint32_t v = chunk_hist[(cf + i) * RADIX + d];
+        chunk_hist[(cf + i) * RADIX + d] = run;
         run += v;
     }
     uint32_t incl = run;
@@ -257,33 +255,34 @@ __global__ __launch_bounds__(256) void seg_scan_kernel(uint32_t *__restrict__ ch
     uint32_t pre = 0;
     for (int w = 0; w < wave; ++w) pre += s_wsum[w];
     const uint32_t base = s_start[blockIdx.x] + pre + incl - run;
-    seg_base[(uint64_t)blockIdx.x * 256 + d] = base;
-    seg_cnt[(uint64_t)blockIdx.x * 256 + d] = run;
-    for (uint32_t c = 0; c < nc; ++c) chunk_hist[(cf + c) * 256 + d] += base;
+    seg_base[(uint64_t)blockIdx.x * RADIX + d] = base;
+    seg_cnt[(uint64_t)blockIdx.x * RADIX + d] = run;
+    for (uint32_t c = 0; c < nc; ++c) chunk_hist[(cf + c) * RADIX + d] += base;
 }
 
-__global__ __launch_bounds__(256) void tile_apply_kernel(uint32_t *__restrict__ tile_hist,
-                                                         const uint32_t *__restrict__ c_first,
-                                                         const uint32_t *__restrict__ c_ntiles,
-                                                         const uint32_t *__restrict__ chunk_base) {
+template <int RADIX>
+__global__ __launch_bounds__(RADIX) void tile_apply_kernel(uint32_t *__restrict__ tile_hist,
+                                                           const uint32_t *__restrict__ c_first,
+                                                           const uint32_t *__restrict__ c_ntiles,
+                                                           const uint32_t *__restrict__ chunk_base) {
     const int d = threadIdx.x;
     const uint64_t f = c_first[blockIdx.x];
     const uint32_t nt = c_ntiles[blockIdx.x];
-    uint32_t run = chunk_base[(uint64_t)blockIdx.x * 256 + d];
+    uint32_t run = chunk_base[(uint64_t)blockIdx.x * RADIX + d];
     uint32_t i = 0;
     for (; i + 8 <= nt; i += 8) {
         uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = tile_hist[(f + i + u) * 256 + d];
+        for (int u = 0; u < 8; ++u) v[u] = tile_hist[(f + i + u) * RADIX + d];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            tile_hist[(f + i + u) * 256 + d] = run;
+            tile_hist[(f + i + u) * RADIX + d] = run;
             run += v[u];
         }
     }
     for (; i < nt; ++i) {
-        const uint32_t v = tile_hist[(f + i) * 256 + d];
-        tile_hist[(f + i) * 256 + d] = run;
+        const uint32_t v = tile_hist[(f + i) * RADIX + d];
+        tile_hist[(f + i) * RADIX + d] = run;
         run += v;
     }
 }
@@ -300,41 +299,58 @@ __device__ __forceinline__ uint32_t wave_append(bool flag, uint32_t *counter, in
     return base + (uint32_t)__popcll(m & lt_mask);
 }
 
-// sub-buckets of this level: > kLocalMax -> next level (or done when no digit is left),
-// 1..kLocalMax -> local list (sorted from digit `level + 1` on by the local rounds)
+// list counters (device, one array): next global level, done, block-local, wave-local lists
+enum { kCtrBig = 0, kCtrDone = 1, kCtrBlock = 2, kCtrWave = 3, kCtrN = 8 };
+
+struct Lists {
+    uint32_t *nb_start, *nb_len;                 // buckets for the next global level
+    uint32_t *dn_start, *dn_len;                 // key bits exhausted: final as they stand
+    uint8_t *dn_par;
+    uint2 *blk, *wav;                            // block-local / wave-local entries
+};
+
+// route one sub-bucket (size >= 1) by size; hi = key bits sorted once it is cut out
+__device__ __forceinline__ void route(uint32_t st, uint32_t size, int hi, int B, int parity, bool allow_big,
+                                      const Lists &L, uint32_t *ctr, int lane) {
+    const bool live = size >= 1;
+    const bool done = live && hi >= B;
+    const bool big = live && !done && size > (uint32_t)kBlockMax && allow_big;
+    const bool blk = live && !done && !big && size > (uint32_t)kWaveMax;
+    const bool wav = live && !done && !big && !blk;
+    const uint32_t a = wave_append(big, &ctr[kCtrBig], lane);
+    if (big) {
+        L.nb_start[a] = st;
+        L.nb_len[a] = size;
+    }
+    const uint32_t b = wave_append(done, &ctr[kCtrDone], lane);
+    if (done) {
+        L.dn_start[b] = st;
+        L.dn_len[b] = size;
+        L.dn_par[b] = (uint8_t)parity;
+    }
+    const uint32_t c = wave_append(blk, &ctr[kCtrBlock], lane);
+    if (blk) L.blk[c] = local_entry(st, size, hi, parity);
+    const uint32_t d = wave_append(wav, &ctr[kCtrWave], lane);
+    if (wav) L.wav[d] = local_entry(st, size, hi, parity);
+}
+
+// the sub-buckets of one global level
 __global__ __launch_bounds__(256) void classify_kernel(const uint32_t *__restrict__ seg_base,
-                                                       const uint32_t *__restrict__ seg_cnt, int level, int has_next,
-                                                       int parity, uint32_t *__restrict__ nb_start,
-                                                       uint32_t *__restrict__ nb_len, uint32_t *__restrict__ ctr,
-                                                       uint32_t *__restrict__ dn_start, uint32_t *__restrict__ dn_len,
-                                                       uint8_t *__restrict__ dn_par, uint2 *__restrict__ local) {
-    const int lane = threadIdx.x & 63;
+                                                       const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
+                                                       int B, int parity, Lists L, uint32_t *__restrict__ ctr) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t size = seg_cnt[i], st = seg_base[i];
-    const bool big = size > (uint32_t)kLocalMax;
-    const uint32_t a = wave_append(big && has_next, &ctr[0], lane);
-    if (big && has_next) {
-        nb_start[a] = st;
-        nb_len[a] = size;
-    }
-    const uint32_t b = wave_append(big && !has_next, &ctr[1], lane);
-    if (big && !has_next) {
-        dn_start[b] = st;
-        dn_len[b] = size;
-        dn_par[b] = (uint8_t)parity;
-    }
-    const bool small = size >= 1 && !big;
-    const uint32_t c = wave_append(small, &ctr[2], lane);
-    if (small) local[c] = local_entry(st, size, level + 1, parity);
+    const bool in = i < nsub;
+    route(in ? seg_base[i] : 0, in ? seg_cnt[i] : 0, hi, B, parity, true, L, ctr, threadIdx.x & 63);
 }
 
 // tile + chunk tables of a bucket list (one thread per bucket)
 __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restrict__ s_start,
                                                          const uint32_t *__restrict__ s_len,
                                                          const uint32_t *__restrict__ s_tfirst,
-                                                         const uint32_t *__restrict__ s_cfirst, uint32_t nseg, uint32_t tile,
-                                                         uint32_t *__restrict__ t_start, uint32_t *__restrict__ t_count,
-                                                         uint32_t *__restrict__ c_first, uint32_t *__restrict__ c_ntiles) {
+                                                         const uint32_t *__restrict__ s_cfirst, uint32_t nseg,
+                                                         uint32_t tile, uint32_t *__restrict__ t_start,
+                                                         uint32_t *__restrict__ t_count, uint32_t *__restrict__ c_first,
+                                                         uint32_t *__restrict__ c_ntiles) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
     const uint32_t st = s_start[s], len = s_len[s], tf = s_tfirst[s], cf = s_cfirst[s];
@@ -350,8 +366,9 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restr
     }
 }
 
-__global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg, uint32_t tile,
-                                                         uint32_t *__restrict__ ntiles, uint32_t *__restrict__ nchunks) {
+__global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg,
+                                                         uint32_t tile, uint32_t *__restrict__ ntiles,
+                                                         uint32_t *__restrict__ nchunks) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
     const uint32_t nt = (s_len[s] + tile - 1) / tile;
@@ -360,166 +377,167 @@ __global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restr
 }
 
 // ---------------------------------------------------------------------------------------------
-// local rounds: one wave per bucket of <= kLocalMax elements
+// local rounds: a bucket of <= T*I elements per workgroup, persistent over a list
 // ---------------------------------------------------------------------------------------------
-// Stable counting sort of the bucket by digit `level` (registers -> LDS), then per sub-bucket:
-// singleton or key exhausted -> final; <= kSmall -> rank-by-count (full key, ties by position);
-// larger -> written in stable order and re-listed for the next round with level + 1.
+// Per bucket (entry = start, len, hi, parity):
+//   1. stable partition by the R-bit digit below the top `hi` bits into LDS (partition_stage);
+//   2. each sub-bucket: singleton, or no key bits left after this digit (equal keys, already in
+//      start order) -> final; <= kSmall -> rank-by-count on the key (ties: staging order =
+//      start order); larger -> left in stable order and re-listed for the next round (its head
+//      flags are provisional: that round rewrites them);
+//   3. keys, starts and head flags (key differs from its predecessor) are written back in order.
 // Output always goes to buffer 0; the bucket is read fully before any write, so in place is safe.
-__global__ __launch_bounds__(64) void msd_local_kernel(const uint2 *__restrict__ list, int B, uint64_t *k0, uint32_t *v0,
-                                                       const uint64_t *__restrict__ k1, const uint32_t *__restrict__ v1,
-                                                       uint2 *__restrict__ spill, uint32_t *__restrict__ spill_count) {
-    __shared__ uint64_t s_k[kLocalMax];
-    __shared__ uint32_t s_v[kLocalMax];
-    __shared__ uint32_t s_cnt[256];
-    __shared__ uint32_t s_strt[256];
-    const int lane = threadIdx.x;
-    const uint2 e = list[blockIdx.x];
+// Loads and stores are branch-free with static counts (clamped to the bucket), so the next
+// bucket's loads -- issued once the current one is final in LDS -- overlap its stores.
+template <int T, int I>
+__device__ __forceinline__ void local_load(const uint2 e, const uint64_t *k0, const uint32_t *v0, const uint64_t *k1,
+                                           const uint32_t *v1, uint64_t (&key)[I], uint32_t (&val)[I]) {
     const uint64_t st = e.x;
     const uint32_t len = e.y >> 8;
-    const int level = (e.y >> 1) & 127;
-    const int par = e.y & 1;
-    const uint64_t *sk = par ? k1 : k0;
-    const uint32_t *sv = par ? v1 : v0;
-    const int D = num_digits(B);
-
-    if (len <= (uint32_t)kSmall || level >= D) {
-        // tiny bucket (or key exhausted: stable order is final)
-        if (level >= D) {
-            if (par)
-                for (uint32_t i = lane; i < len; i += 64) {
-                    k0[st + i] = sk[st + i];
-                    v0[st + i] = sv[st + i];
-                }
-            return;
-        }
-        uint64_t mk = 0;
-        uint32_t mv = 0;
-        if ((uint32_t)lane < len) {
-            mk = sk[st + lane];
-            mv = sv[st + lane];
-        }
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < len; ++j) {
-            const uint64_t kj = __shfl(mk, (int)j);
-            r += (kj < mk) || (kj == mk && j < (uint32_t)lane);
-        }
-        if ((uint32_t)lane < len) {
-            k0[st + r] = mk;
-            v0[st + r] = mv;
-        }
-        return;
-    }
-
-    // counting sort by digit `level`
-    const Dig dd = digit_at(B, level);
-    for (int i = lane; i < 256; i += 64) s_cnt[i] = 0;
-    uint64_t key[kLocalChunks];
-    uint32_t val[kLocalChunks], rk[kLocalChunks];
+    const uint64_t *sk = (e.y & 1) ? k1 : k0;
+    const uint32_t *sv = (e.y & 1) ? v1 : v0;
+    uint32_t q0 = (threadIdx.x >> 6) * (I * 64) + (threadIdx.x & 63);
+    asm volatile("" : "+v"(q0));
 #pragma unroll
-    for (int c = 0; c < kLocalChunks; ++c) {
-        const uint32_t i = c * 64 + lane;
-        const bool valid = i < len;
-        key[c] = valid ? sk[st + i] : 0;
-        val[c] = valid ? sv[st + i] : 0;
-    }
-#pragma unroll
-    for (int c = 0; c < kLocalChunks; ++c) {
-        rk[c] = 0;
-        if ((uint32_t)c * 64 >= len) continue;  // wave-uniform
-        const bool valid = c * 64 + lane < len;
-        const uint32_t d = dg_of(key[c], dd);
-        const uint64_t peers = match_peers(d, valid);
-        const uint32_t rank_in = lanes_below(peers);
-        const uint32_t old = s_cnt[d];
-        if (valid && rank_in == 0) s_cnt[d] = old + (uint32_t)__popcll(peers);
-        rk[c] = old + rank_in;
-    }
-    {
-        uint32_t c4[4], s4 = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            c4[u] = s_cnt[lane * 4 + u];
-            s4 += c4[u];
-        }
-        uint32_t incl = s4;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        uint32_t run = incl - s4;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            s_strt[lane * 4 + u] = run;
-            run += c4[u];
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < kLocalChunks; ++c) {
-        if (c * 64 + lane < len) {
-            const uint32_t p = s_strt[dg_of(key[c], dd)] + rk[c];
-            s_k[p] = key[c];
-            s_v[p] = val[c];
-        }
-    }
-    const bool last = level + 1 >= D;
-    for (uint32_t c0 = 0; c0 < len; c0 += 64) {
-        const uint32_t p = c0 + lane;
-        bool respill = false;
-        uint32_t sub_start = 0, sub_len = 0;
-        if (p < len) {
-            const uint64_t kk = s_k[p];
-            const uint32_t vv = s_v[p];
-            const uint32_t d = dg_of(kk, dd);
-            const uint32_t size = s_cnt[d], sb = s_strt[d];
-            uint32_t out = p;
-            if (size > 1 && !last) {
-                if (size <= (uint32_t)kSmall) {
-                    const uint32_t me = p - sb;
-                    uint32_t r = 0;
-                    for (uint32_t j = 0; j < size; ++j) {
-                        const uint64_t kj = s_k[sb + j];
-                        r += (kj < kk) || (kj == kk && j < me);
-                    }
-                    out = sb + r;
-                } else if (p == sb) {
-                    respill = true;
-                    sub_start = (uint32_t)st + sb;
-                    sub_len = size;
-                }
-            }
-            k0[st + out] = kk;
-            v0[st + out] = vv;
-        }
-        const uint32_t slot = wave_append(respill, spill_count, lane);
-        if (respill) spill[slot] = local_entry(sub_start, sub_len, level + 1, 0);
+    for (int i = 0; i < I; ++i) {
+        const uint64_t e_ = st + min(q0 + i * 64, len - 1);
+        key[i] = sk[e_];
+        val[i] = sv[e_];
     }
 }
 
+template <int T, int I, int R>
+__global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
+                                                      uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                      const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
+                                                      uint32_t *__restrict__ ctr) {
+    using SM = PartSmem<T, I, R>;
+    constexpr int TILE = SM::kTile;
+    constexpr int RADIX = SM::kRadix;
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
+    __shared__ uint32_t s_wsum[SM::kWaves];
+    __shared__ uint32_t s_start[RADIX + 1];
+    __shared__ uint8_t s_hd[TILE + 1];
+    __shared__ uint32_t s_any;
+    uint64_t *s_k = reinterpret_cast<uint64_t *>(s_raw);
+    uint32_t *s_v = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
+    uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t idx = blockIdx.x;
+    if (idx >= count) return;
+    uint2 e = list[idx];
+    uint64_t key[I];
+    uint32_t val[I];
+    local_load<T, I>(e, k0, v0, k1, v1, key, val);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (; idx < count; idx += gridDim.x) {
+        const uint2 ce = e;
+        const uint64_t st = ce.x;
+        const uint32_t len = ce.y >> 8;
+        const int hi = (ce.y >> 1) & 127;
+        const Dig dd = dig_at(B, hi, R);
+        const int nhi = hi + R;      // key bits sorted within a sub-bucket
+        const bool last = nhi >= B;  // sub-bucket keys are equal
+        if (idx + gridDim.x < count) e = list[idx + gridDim.x];  // else: re-load the current one
+
+        // 1. stable partition into LDS
+        for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
+        if (tid == 0) s_any = 0;
+        lds_barrier();
+        bool valid[I];
+        uint32_t slot[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < len;
+        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot);
+
+        // 2. final position and head flag of every element
+        uint32_t out[I];
+        uint8_t hd[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t dg = dg_of(key[i], dd);
+            const uint32_t sb = s_start[dg], size = s_start[dg + 1] - sb;
+            out[i] = slot[i];
+            hd[i] = slot[i] == sb;  // singleton or equal keys: the first is the head
+            if (valid[i] && size > 1 && !last) {
+                if (size <= (uint32_t)kSmall) {
+                    const uint32_t me = slot[i] - sb;
+                    uint32_t lt = 0, eq = 0;
+                    for (uint32_t j = 0; j < size; ++j) {
+                        const uint64_t kj = s_k[sb + j];
+                        lt += kj < key[i];
+                        eq += kj == key[i] && j < me;
+                    }
+                    out[i] = sb + lt + eq;
+                    hd[i] = eq == 0;
+                } else {
+                    hd[i] = 2;  // not final: re-listed, head written by the next round
+                }
+            }
+        }
+        // re-list the large sub-buckets (rare): one entry each, from its first element
+        bool first[I], any = false;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            first[i] = valid[i] && hd[i] == 2 && slot[i] == s_start[dg_of(key[i], dd)];
+            any |= first[i];
+        }
+        if (any) s_any = 1;
+        lds_barrier();  // also: every rank-by-count read is done before the staging is overwritten
+        if (s_any) {
+#pragma unroll
+            for (int i = 0; i < I; ++i) {
+                const uint32_t dg = dg_of(key[i], dd);
+                const uint32_t size = first[i] ? s_start[dg + 1] - s_start[dg] : 0;
+                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < I; ++i) {  // invalid items: out = sink slot
+            s_k[out[i]] = key[i];
+            s_v[out[i]] = val[i];
+            s_hd[out[i]] = hd[i] == 1;
+        }
+        // the next bucket's loads fly while this one is written back
+        local_load<T, I>(e, k0, v0, k1, v1, key, val);  // unconditional: static load count
+        lds_barrier();
+
+        // 3. in-order write-back with head flags
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = min((uint32_t)(i * T + tid), len - 1);
+            k0[st + p] = s_k[p];
+            v0[st + p] = s_v[p];
+            heads[st + p] = s_hd[p];
+        }
+        lds_barrier();  // the write-back has read LDS before the next bucket's staging
+    }
+}
+
+// sub-buckets whose key bits are exhausted: in order already (copied to buffer 0 if needed);
+// all keys equal, so the only head is the first element
 __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restrict__ dn_start,
                                                         const uint32_t *__restrict__ dn_len,
                                                         const uint8_t *__restrict__ dn_par, const uint64_t *__restrict__ k1,
                                                         const uint32_t *__restrict__ v1, uint64_t *__restrict__ k0,
-                                                        uint32_t *__restrict__ v0) {
+                                                        uint32_t *__restrict__ v0, uint8_t *__restrict__ heads) {
     const uint32_t s = blockIdx.x;
-    if (!dn_par[s]) return;
     const uint64_t st = dn_start[s];
     const uint32_t len = dn_len[s];
+    const bool copy = dn_par[s];
     for (uint32_t i = threadIdx.x; i < len; i += 256) {
-        k0[st + i] = k1[st + i];
-        v0[st + i] = v1[st + i];
+        if (copy) {
+            k0[st + i] = k1[st + i];
+            v0[st + i] = v1[st + i];
+        }
+        heads[st + i] = i == 0;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
-static int grid_n(uint64_t n, int cap = 8192) {
-    uint64_t g = (n + 255) / 256;
-    if (g < 1) g = 1;
-    return (int)std::min<uint64_t>(g, (uint64_t)cap);
-}
+static int grid_n(uint64_t n) { return (int)std::max<uint64_t>((n + 255) / 256, 1); }
 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
 
@@ -527,12 +545,12 @@ hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uin
 static int scan_offsets(gk_ctx *c, uint32_t *tile_hist, uint32_t *chunk_hist, const uint32_t *c_first,
                         const uint32_t *c_ntiles, uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks,
                         const uint32_t *s_start, uint64_t nseg, uint32_t *seg_base, uint32_t *seg_cnt) {
-    hipLaunchKernelGGL(chunk_sum_kernel, dim3((unsigned)C), dim3(256), 0, c->stream, tile_hist, c_first, c_ntiles,
-                       chunk_hist);
-    hipLaunchKernelGGL(seg_scan_kernel, dim3((unsigned)nseg), dim3(256), 0, c->stream, chunk_hist, s_cfirst, s_nchunks,
-                       s_start, seg_base, seg_cnt);
-    hipLaunchKernelGGL(tile_apply_kernel, dim3((unsigned)C), dim3(256), 0, c->stream, tile_hist, c_first, c_ntiles,
-                       chunk_hist);
+    hipLaunchKernelGGL(chunk_sum_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist, c_first,
+                       c_ntiles, chunk_hist);
+    hipLaunchKernelGGL(seg_scan_kernel<kGRadix>, dim3((unsigned)nseg), dim3(kGRadix), 0, c->stream, chunk_hist,
+                       s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
+    hipLaunchKernelGGL(tile_apply_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist, c_first,
+                       c_ntiles, chunk_hist);
     GK_TRY_HIP(c, hipGetLastError());
     return GK_OK;
 }
@@ -564,10 +582,10 @@ static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t
 
 // partition grid: 4 workgroups per CU (one resident at a time: LDS-bound), a multiple of 8 (equal
 // shares per XCD); measured 4% faster than exactly one per CU (profiles/r1/README.md)
-static unsigned persistent_grid(gk_ctx *c) {
+static unsigned cu_count(gk_ctx *c) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus < 8) cus = 256;
-    return (unsigned)(cus / 8 * 8 * 4);
+    return (unsigned)(cus / 8 * 8);
 }
 
 static int read_ctr(gk_ctx *c, const uint32_t *d, uint32_t *h, int count) {
@@ -576,29 +594,53 @@ static int read_ctr(gk_ctx *c, const uint32_t *d, uint32_t *h, int count) {
     return GK_OK;
 }
 
-template <int PT, int PI>
-static int msd_sort_shape(gk_ctx *c, const KeySpec &ks) {
-    constexpr uint32_t kPartTile = PT * PI;
+static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
+                                   "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
+
+int msd_sort(gk_ctx *c, const KeySpec &ks) {
     GK_TRY_HIP(c, msd_tables());
-    int total_slot;
+    int total_slot, slot;
     timer_begin(c, "msd_total", &total_slot);
-    const int B = ks.total_bits, D = num_digits(B);
+    const int B = ks.total_bits;
     const uint64_t n = c->n, L = c->sba_len;
-    uint32_t *ctr;  // [0] next-level buckets, [1] done buckets, [2] local entries, [3] spill entries
-    GK_TRY_HIP(c, scratch(c, "msd_ctr", 4, &ctr));
-    GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 16, c->stream));
+    const unsigned cus = cu_count(c);
+    uint32_t *ctr, h[kCtrN];
+    GK_TRY_HIP(c, scratch(c, "msd_ctr", kCtrN, &ctr));
+    GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
+
+    // lists: big (ping-pong), done, and two generations of block/wave lists; a local round
+    // re-lists at most n / (kSmall + 1) sub-buckets
+    const uint64_t max_big = n / kBlockMax + 2, max_spill = n / (kSmall + 1) + 1024;
+    uint32_t *big_start[2], *big_len[2];
+    GK_TRY_HIP(c, scratch(c, "big_start0", max_big, &big_start[0]));
+    GK_TRY_HIP(c, scratch(c, "big_len0", max_big, &big_len[0]));
+    GK_TRY_HIP(c, scratch(c, "big_start1", max_big, &big_start[1]));
+    GK_TRY_HIP(c, scratch(c, "big_len1", max_big, &big_len[1]));
+    uint32_t *dn_start, *dn_len;
+    uint8_t *dn_par;
+    GK_TRY_HIP(c, grow_keep(c, "dn_start", 1024, 0, &dn_start));
+    GK_TRY_HIP(c, grow_keep(c, "dn_len", 1024, 0, &dn_len));
+    GK_TRY_HIP(c, grow_keep(c, "dn_par", 1024, 0, &dn_par));
+    uint2 *blk[2], *wav[2];
+    GK_TRY_HIP(c, grow_keep(c, "blk0", 1024, 0, &blk[0]));
+    GK_TRY_HIP(c, grow_keep(c, "wav0", 1024, 0, &wav[0]));
+    uint8_t *heads;
+    GK_TRY_HIP(c, scratch(c, "msd_heads", n + 64, &heads));
+    auto lists = [&](int g, int bigsel) {
+        return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par, blk[g], wav[g]};
+    };
 
     // ---- L0: one bucket (all k-mers), tiles over sba positions ----
-    const uint64_t nt0 = (L + kPartTile - 1) / kPartTile;
+    const uint64_t nt0 = (L + kPTile - 1) / kPTile;
     const uint64_t nc0 = (nt0 + kChunkTiles - 1) / kChunkTiles;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *s_misc, *seg_base, *seg_cnt;
-    GK_TRY_HIP(c, scratch(c, "tile_hist", nt0 * 256, &tile_hist));
-    GK_TRY_HIP(c, scratch(c, "chunk_hist", nc0 * 256, &chunk_hist));
+    GK_TRY_HIP(c, scratch(c, "tile_hist", nt0 * kGRadix, &tile_hist));
+    GK_TRY_HIP(c, scratch(c, "chunk_hist", nc0 * kGRadix, &chunk_hist));
     GK_TRY_HIP(c, scratch(c, "c_first", nc0, &c_first));
     GK_TRY_HIP(c, scratch(c, "c_ntiles", nc0, &c_ntiles));
     GK_TRY_HIP(c, scratch(c, "s_misc", 4, &s_misc));
-    GK_TRY_HIP(c, scratch(c, "seg_base", 256, &seg_base));
-    GK_TRY_HIP(c, scratch(c, "seg_cnt", 256, &seg_cnt));
+    GK_TRY_HIP(c, scratch(c, "seg_base", kGRadix, &seg_base));
+    GK_TRY_HIP(c, scratch(c, "seg_cnt", kGRadix, &seg_cnt));
     {
         std::vector<uint32_t> cf(nc0), cn(nc0);
         for (uint64_t j = 0; j < nc0; ++j) {
@@ -611,15 +653,15 @@ static int msd_sort_shape(gk_ctx *c, const KeySpec &ks) {
         GK_TRY_HIP(c, hipMemcpyAsync(s_misc, misc, 12, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     }
-    L0Args a{c->sba, ks.symbols, B};
-    const Dig d0 = digit_at(B, 0);
-    const unsigned pgrid = persistent_grid(c);
-    int slot;
+    const L0Args a{c->sba, ks.symbols, B};
+    const Dig d0 = dig_at(B, 0, kGR);
     timer_begin(c, "msd_l0_count", &slot);
     if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_count_kernel<2, PT, PI>), dim3((unsigned)nt0), dim3(PT), 0, c->stream, a, d0, tile_hist);
+        hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a, d0,
+                           tile_hist);
     else
-        hipLaunchKernelGGL((msd0_count_kernel<4, PT, PI>), dim3((unsigned)nt0), dim3(PT), 0, c->stream, a, d0, tile_hist);
+        hipLaunchKernelGGL((msd0_count_kernel<4, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a, d0,
+                           tile_hist);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     timer_begin(c, "msd_scan", &slot);
@@ -628,48 +670,53 @@ static int msd_sort_shape(gk_ctx *c, const KeySpec &ks) {
     if (rc != GK_OK) return rc;
     timer_end(c, slot);
     timer_begin(c, "msd_pass_l0", &slot);
+    const unsigned pgrid = cus * 4;
     if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_scatter_kernel<2, PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, a, d0, tile_hist,
-                           c->keys[0], c->vals[0], (uint32_t)nt0, n);
+        hipLaunchKernelGGL((msd0_scatter_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+                           tile_hist, c->keys[0], c->vals[0], (uint32_t)nt0, n);
     else
-        hipLaunchKernelGGL((msd0_scatter_kernel<4, PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, a, d0, tile_hist,
-                           c->keys[0], c->vals[0], (uint32_t)nt0, n);
+        hipLaunchKernelGGL((msd0_scatter_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+                           tile_hist, c->keys[0], c->vals[0], (uint32_t)nt0, n);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
 
-    // bucket lists (ping-pong), done list, local list
-    const uint64_t max_big = n / kLocalMax + 2;
-    uint32_t *lst_start[2], *lst_len[2], *dn_start, *dn_len;
-    uint8_t *dn_par;
-    uint2 *local;
-    GK_TRY_HIP(c, scratch(c, "lstA_start", max_big, &lst_start[0]));
-    GK_TRY_HIP(c, scratch(c, "lstA_len", max_big, &lst_len[0]));
-    GK_TRY_HIP(c, scratch(c, "lstB_start", max_big, &lst_start[1]));
-    GK_TRY_HIP(c, scratch(c, "lstB_len", max_big, &lst_len[1]));
-    GK_TRY_HIP(c, scratch(c, "dn_start", max_big, &dn_start));
-    GK_TRY_HIP(c, scratch(c, "dn_len", max_big, &dn_len));
-    GK_TRY_HIP(c, scratch(c, "dn_par", max_big, &dn_par));
-    GK_TRY_HIP(c, grow_keep(c, "local", 256, 0, &local));
-    int li = 0;
-    hipLaunchKernelGGL(classify_kernel, dim3(1), dim3(256), 0, c->stream, seg_base, seg_cnt, 0, D > 1 ? 1 : 0, 0,
-                       lst_start[li], lst_len[li], ctr, dn_start, dn_len, dn_par, local);
-    GK_TRY_HIP(c, hipGetLastError());
-    uint32_t h[4];
-    rc = read_ctr(c, ctr, h, 4);
+    // ---- classify L0's sub-buckets; then global levels while buckets exceed kBlockMax ----
+    uint64_t nblk = 0, nwav = 0, ndone = 0;
+    auto classify = [&](uint64_t nsub, int hi, int parity, int bigsel) -> int {
+        // capacity: every sub-bucket could land in any one list
+        GK_TRY_HIP(c, grow_keep(c, "blk0", nblk + nsub, nblk, &blk[0]));
+        GK_TRY_HIP(c, grow_keep(c, "wav0", nwav + nsub, nwav, &wav[0]));
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nsub, ndone, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nsub, ndone, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nsub, ndone, &dn_par));
+        GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
+        timer_begin(c, "msd_classify", &slot);
+        hipLaunchKernelGGL(classify_kernel, dim3(grid_n(nsub)), dim3(256), 0, c->stream, seg_base, seg_cnt, nsub, hi, B,
+                           parity, lists(0, bigsel), ctr);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        int r = read_ctr(c, ctr, h, 4);
+        if (r != GK_OK) return r;
+        nblk = h[kCtrBlock];
+        nwav = h[kCtrWave];
+        ndone = h[kCtrDone];
+        return GK_OK;
+    };
+    int cur_big = 0;
+    rc = classify(kGRadix, kGR, 0, cur_big);
     if (rc != GK_OK) return rc;
-    uint32_t nbig = h[0], nlocal = h[2];
-
-    // ---- L1..: partition big buckets by the next digit ----
+    uint32_t nbig = h[kCtrBig];
     int level = 1, in = 0;
-    while (nbig > 0 && level < D) {
+    while (nbig > 0) {
         const int out = in ^ 1;
+        const int hi = level * kGR;
         uint32_t *ntl, *nch, *tfirst, *cfirst;
         GK_TRY_HIP(c, scratch(c, "s_ntiles", nbig, &ntl));
         GK_TRY_HIP(c, scratch(c, "s_nchunks", nbig, &nch));
         GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
         GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
-        hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig, 1 << 30)), dim3(256), 0, c->stream, lst_len[li], nbig,
-                           kPartTile, ntl, nch);
+        hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big], nbig,
+                           (uint32_t)kPTile, ntl, nch);
         GK_TRY_HIP(c, hipGetLastError());
         uint64_t T = 0, C = 0;
         GK_TRY_HIP(c, scan_u32_exclusive_pub(c, ntl, nbig, tfirst, &T));
@@ -677,91 +724,88 @@ static int msd_sort_shape(gk_ctx *c, const KeySpec &ks) {
         uint32_t *t_start, *t_count;
         GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
         GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));
-        GK_TRY_HIP(c, scratch(c, "tile_hist", T * 256, &tile_hist));
-        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * 256, &chunk_hist));
+        GK_TRY_HIP(c, scratch(c, "tile_hist", T * kGRadix, &tile_hist));
+        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * kGRadix, &chunk_hist));
         GK_TRY_HIP(c, scratch(c, "c_first", C, &c_first));
         GK_TRY_HIP(c, scratch(c, "c_ntiles", C, &c_ntiles));
-        GK_TRY_HIP(c, scratch(c, "seg_base", (uint64_t)nbig * 256, &seg_base));
-        GK_TRY_HIP(c, scratch(c, "seg_cnt", (uint64_t)nbig * 256, &seg_cnt));
-        GK_TRY_HIP(c, grow_keep(c, "local", (uint64_t)nlocal + 256ull * nbig, nlocal, &local));
-        hipLaunchKernelGGL(tile_table_kernel, dim3(grid_n(nbig, 1 << 30)), dim3(256), 0, c->stream, lst_start[li],
-                           lst_len[li], tfirst, cfirst, nbig, kPartTile, t_start, t_count, c_first, c_ntiles);
-        const Dig dl = digit_at(B, level);
+        GK_TRY_HIP(c, scratch(c, "seg_base", (uint64_t)nbig * kGRadix, &seg_base));
+        GK_TRY_HIP(c, scratch(c, "seg_cnt", (uint64_t)nbig * kGRadix, &seg_cnt));
+        hipLaunchKernelGGL(tile_table_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
+                           big_len[cur_big], tfirst, cfirst, nbig, (uint32_t)kPTile, t_start, t_count, c_first,
+                           c_ntiles);
+        const Dig dl = dig_at(B, hi, kGR);
         timer_begin(c, "msd_count", &slot);
-        hipLaunchKernelGGL(msd_count_kernel, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
+        hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
                            c->keys[in], tile_hist);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         timer_begin(c, "msd_scan", &slot);
-        rc = scan_offsets(c, tile_hist, chunk_hist, c_first, c_ntiles, C, cfirst, nch, lst_start[li], nbig, seg_base,
-                          seg_cnt);
+        rc = scan_offsets(c, tile_hist, chunk_hist, c_first, c_ntiles, C, cfirst, nch, big_start[cur_big], nbig,
+                          seg_base, seg_cnt);
         if (rc != GK_OK) return rc;
         timer_end(c, slot);
-        static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
-                                           "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
         timer_begin(c, kPassNames[level & 7], &slot);
-        hipLaunchKernelGGL((msd_scatter_kernel<PT, PI>), dim3(pgrid), dim3(PT), 0, c->stream, t_start, t_count, dl,
-                           tile_hist, c->keys[in], c->vals[in], c->keys[out], c->vals[out], (uint32_t)T, n);
+        hipLaunchKernelGGL((msd_scatter_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
+                           dl, tile_hist, c->keys[in], c->vals[in], c->keys[out], c->vals[out], (uint32_t)T, n);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        const bool has_next = level + 1 < D;
-        const int lo = li ^ 1;
-        GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4, c->stream));
-        timer_begin(c, "msd_classify", &slot);
-        hipLaunchKernelGGL(classify_kernel, dim3(nbig), dim3(256), 0, c->stream, seg_base, seg_cnt, level,
-                           has_next ? 1 : 0, out, lst_start[lo], lst_len[lo], ctr, dn_start, dn_len, dn_par, local);
-        GK_TRY_HIP(c, hipGetLastError());
-        timer_end(c, slot);
-        rc = read_ctr(c, ctr, h, 4);
+        cur_big ^= 1;
+        rc = classify((uint64_t)nbig * kGRadix, hi + kGR, out, cur_big);
         if (rc != GK_OK) return rc;
-        nbig = h[0];
-        nlocal = h[2];
-        li = lo;
+        nbig = h[kCtrBig];
         ++level;
         in = out;
     }
 
-    // ---- local rounds: every bucket <= kLocalMax, written to buffer 0 ----
-    uint2 *spill;
-    GK_TRY_HIP(c, scratch(c, "spill", n / (kSmall + 1) + 256, &spill));
-    GK_TRY_HIP(c, grow_keep(c, "local", std::max<uint64_t>(nlocal, n / (kSmall + 1) + 256), nlocal, &local));
-    const uint2 *cur_list = local;
-    uint32_t ncur = nlocal;
-    int round = 0;
-    while (ncur > 0) {
-        GK_TRY_HIP(c, hipMemsetAsync(ctr + 3, 0, 4, c->stream));
-        uint2 *out_list = (round % 2 == 0) ? spill : local;  // spills of round r live in the other list
-        timer_begin(c, round == 0 ? "msd_local" : "msd_local_spill", &slot);
-        hipLaunchKernelGGL(msd_local_kernel, dim3(ncur), dim3(64), 0, c->stream, cur_list, B, c->keys[0], c->vals[0],
-                           c->keys[1], c->vals[1], out_list, ctr + 3);
-        GK_TRY_HIP(c, hipGetLastError());
-        timer_end(c, slot);
-        rc = read_ctr(c, ctr + 3, &ncur, 1);
+    // ---- local rounds: generation g lists -> re-listed sub-buckets in generation g ^ 1 ----
+    GK_TRY_HIP(c, grow_keep(c, "blk0", std::max<uint64_t>(nblk, max_spill), nblk, &blk[0]));
+    GK_TRY_HIP(c, grow_keep(c, "wav0", std::max<uint64_t>(nwav, max_spill), nwav, &wav[0]));
+    GK_TRY_HIP(c, grow_keep(c, "blk1", max_spill, 0, &blk[1]));
+    GK_TRY_HIP(c, grow_keep(c, "wav1", max_spill, 0, &wav[1]));
+    GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
+    GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
+    GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
+    int g = 0, round = 0;
+    while (nblk + nwav > 0) {
+        const int ng = g ^ 1;
+        // the re-list counters of this round start from 0 (the done count carries on)
+        const uint32_t zero2[2] = {0, 0};
+        GK_TRY_HIP(c, hipMemcpyAsync(ctr + kCtrBlock, zero2, 8, hipMemcpyHostToDevice, c->stream));
+        const Lists nl = lists(ng, 0);
+        if (nblk) {
+            timer_begin(c, round == 0 ? "msd_local_block" : "msd_local_block_r", &slot);
+            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>), dim3((unsigned)std::min<uint64_t>(nblk, cus * 8)),
+                               dim3(kBT), 0, c->stream, blk[g], (uint32_t)nblk, B, c->keys[0], c->vals[0], c->keys[1],
+                               c->vals[1], heads, nl, ctr);
+            GK_TRY_HIP(c, hipGetLastError());
+            timer_end(c, slot);
+        }
+        if (nwav) {
+            timer_begin(c, round == 0 ? "msd_local_wave" : "msd_local_wave_r", &slot);
+            hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, kWR>), dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)),
+                               dim3(kWT), 0, c->stream, wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1],
+                               c->vals[1], heads, nl, ctr);
+            GK_TRY_HIP(c, hipGetLastError());
+            timer_end(c, slot);
+        }
+        rc = read_ctr(c, ctr, h, 4);
         if (rc != GK_OK) return rc;
-        cur_list = out_list;
-        ++round;
-        if (round > 16) return fail(c, GK_E_HIP, "msd local rounds did not converge");
+        nblk = h[kCtrBlock];
+        nwav = h[kCtrWave];
+        ndone = h[kCtrDone];
+        g = ng;
+        if (++round > 64) return fail(c, GK_E_HIP, "msd local rounds did not converge");
     }
-    const uint32_t ndone = h[1];
     if (ndone > 0) {
-        hipLaunchKernelGGL(done_copy_kernel, dim3(ndone), dim3(256), 0, c->stream, dn_start, dn_len, dn_par,
-                           c->keys[1], c->vals[1], c->keys[0], c->vals[0]);
+        hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len, dn_par,
+                           c->keys[1], c->vals[1], c->keys[0], c->vals[0], heads);
         GK_TRY_HIP(c, hipGetLastError());
     }
     timer_end(c, total_slot);
+    c->heads = heads;
+    c->heads_valid = true;
     c->cur = 0;
     return GK_OK;
-}
-
-int msd_sort(gk_ctx *c, const KeySpec &ks) {
-    const char *e = getenv("GKM_MSD_SHAPE");  // tuning experiments only
-    const int shape = e ? atoi(e) : 0;
-    switch (shape) {
-    case 1: return msd_sort_shape<512, 12>(c, ks);
-    case 2: return msd_sort_shape<512, 16>(c, ks);
-    case 3: return msd_sort_shape<256, 16>(c, ks);
-    default: return msd_sort_shape<1024, 12>(c, ks);
-    }
 }
 
 }  // namespace gkm

@@ -21,37 +21,37 @@ __device__ __forceinline__ void lds_barrier() {
 // s_waitcnt immediate (gfx9 encoding) for vmcnt(0) with expcnt/lgkmcnt left at their maximum
 constexpr int kVmcnt0 = 0x0F70;
 
+// A digit is `w` bits of a B-bit key below its top `hi` bits (the bits already sorted).
 struct Dig {
     int shift;
     uint32_t mask;
 };
 
-__host__ __device__ inline Dig digit_at(int B, int l) {
-    int hi = B - 8 * l;
-    int lo = hi - 8;
+__host__ __device__ inline Dig dig_at(int B, int hi, int w) {
+    int lo = B - hi - w;
     if (lo < 0) lo = 0;
-    return Dig{lo, (1u << (hi - lo)) - 1u};
+    return Dig{lo, (uint32_t)((1ull << (B - hi - lo)) - 1)};
 }
-
-__host__ __device__ inline int num_digits(int B) { return (B + 7) / 8; }
 
 __device__ __forceinline__ uint32_t dg_of(uint64_t k, Dig d) { return (uint32_t)(k >> d.shift) & d.mask; }
 
-// local-list entry: x = bucket start, y = len << 8 | level << 1 | parity
-__host__ __device__ inline uint2 local_entry(uint32_t start, uint32_t len, int level, int parity) {
-    return make_uint2(start, (len << 8) | ((uint32_t)level << 1) | (uint32_t)parity);
+// bucket-list entry: x = bucket start, y = len << 8 | hi << 1 | parity (hi = key bits already
+// sorted, parity = the key/start buffer holding the bucket)
+__host__ __device__ inline uint2 local_entry(uint32_t start, uint32_t len, int hi, int parity) {
+    return make_uint2(start, (len << 8) | ((uint32_t)hi << 1) | (uint32_t)parity);
 }
 
 // ---------------------------------------------------------------------------------------------
 // shared building blocks
 // ---------------------------------------------------------------------------------------------
-// lanes of the wave holding the same 8-bit digit (and valid): 8 ballots; per bit the lane keeps
+// lanes of the wave holding the same R-bit digit (and valid): R ballots; per bit the lane keeps
 // the ballot or its complement via a sign-extended bit (one 3-input bitop per half)
+template <int R>
 __device__ __forceinline__ uint64_t match_peers(uint32_t d, bool valid) {
     const uint64_t v = __ballot(valid);
     uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < R; ++b) {
         const uint32_t m = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);  // 0 or ~0
         const uint64_t bb = __ballot(m != 0);
         lo &= ~((uint32_t)bb ^ m);
@@ -64,15 +64,15 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// stable 64-lane ranking of I wave-striped items by an 8-bit digit (per-wave LDS counters):
+// stable 64-lane ranking of I wave-striped items by an R-bit digit (per-wave LDS counters):
 // every lane reads its digit's counter, the first lane of each peer group bumps it.  LDS ops of
 // one wave complete in order, so item i+1 reads item i's update.
-template <int I>
+template <int I, int R>
 __device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool (&valid)[I], uint32_t *s_wc_wave,
                                            uint32_t (&rank)[I]) {
 #pragma unroll
     for (int i = 0; i < I; ++i) {
-        const uint64_t peers = match_peers(dig[i], valid[i]);
+        const uint64_t peers = match_peers<R>(dig[i], valid[i]);
         const uint32_t rank_in = lanes_below(peers);
         const uint32_t old = s_wc_wave[dig[i]];
         if (valid[i] && rank_in == 0) s_wc_wave[dig[i]] = old + (uint32_t)__popcll(peers);
@@ -80,45 +80,52 @@ __device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool 
     }
 }
 
-template <int T, int I>
+template <int T, int I, int R>
 struct PartSmem {
     static constexpr int kTile = T * I;
     static constexpr int kWaves = T / 64;
-    static constexpr int kValOff = (kTile + 2) * 8;     // keys [kTile + 1], then starts [kTile + 1]
+    static constexpr int kRadix = 1 << R;
+    static constexpr int kValOff = (kTile + 2) * 8;           // keys [kTile + 1], then starts [kTile + 1]
     static constexpr int kStage = kValOff + (kTile + 1) * 4;  // (slot kTile: sink for invalid items)
-    static constexpr int kCounters = kWaves * 256 * 4;  // per-wave digit counters (aliased)
+    static constexpr int kCounters = kWaves * kRadix * 4;     // per-wave digit counters (aliased)
     static constexpr int kUnion = kStage > kCounters ? kStage : kCounters;
+    static_assert(kRadix <= T, "one thread per digit");
 };
 
 // Stable partition of one tile (item i of lane l in wave w = tile element w*I*64 + i*64 + l) by
-// digit d, in two halves so the caller can issue the next tile's loads in between:
+// an R-bit digit d, in two halves so the caller can issue the next tile's loads in between:
 //   partition_stage  rank in registers, tile digit starts, keys and starts into LDS in digit order
 //   partition_store  coalesced runs from LDS to tile_off[digit] (global digit offsets of the tile)
-// s_wc (= s_raw) must be zero on entry.  Barriers inside: all T threads must call.
-template <int T, int I>
+// s_wc (= s_raw) must be zero on entry; s_toff holds the tile's global digit offsets.
+// Barriers inside: all T threads must call.
+// s_start[RADIX + 1] receives the tile-local digit starts (s_start[RADIX] = item count) and
+// slot[] each item's staging slot (invalid items: the sink slot kTile); s_toff may be null.
+template <int T, int I, int R>
 __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const uint32_t (&val)[I],
                                                 const bool (&valid)[I], Dig d, unsigned char *s_raw,
-                                                uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_count) {
-    constexpr int NW = T / 64;
-    constexpr int TILE = T * I;
+                                                uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_start,
+                                                uint32_t (&slot)[I]) {
+    using SM = PartSmem<T, I, R>;
+    constexpr int NW = SM::kWaves;
+    constexpr int TILE = SM::kTile;
+    constexpr int RADIX = SM::kRadix;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
     uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_raw);
-    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_raw + PartSmem<T, I>::kValOff);
-    __shared__ uint32_t s_start[256];
+    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
 
     uint32_t dig[I], rank[I];
 #pragma unroll
     for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
-    rank_items<I>(dig, valid, s_wc + wave * 256, rank);
+    rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank);
     lds_barrier();
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
     uint32_t total = 0, incl = 0;
-    if (tid < 256) {
+    if (tid < RADIX) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
-            const uint32_t v = s_wc[w * 256 + tid];
-            s_wc[w * 256 + tid] = total;
+            const uint32_t v = s_wc[w * RADIX + tid];
+            s_wc[w * RADIX + tid] = total;
             total += v;
         }
         incl = total;
@@ -130,23 +137,22 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
         if (lane == 63) s_wsum[wave] = incl;
     }
     lds_barrier();
-    if (tid < 256) {
+    if (tid < RADIX) {
         uint32_t pre = 0;
         for (int w = 0; w < wave; ++w) pre += s_wsum[w];
         s_start[tid] = pre + incl - total;
-        s_toff[tid] -= pre + incl - total;  // global offset of tile slot s = s_toff[digit] + s
-        if (tid == 255) *s_count = pre + incl;
+        if (s_toff) s_toff[tid] -= pre + incl - total;  // global offset of tile slot s = s_toff[digit] + s
+        if (tid == RADIX - 1) s_start[RADIX] = pre + incl;
     }
     lds_barrier();
-    uint32_t slot[I];
 #pragma unroll
-    for (int i = 0; i < I; ++i) slot[i] = s_start[dig[i]] + s_wc[wave * 256 + dig[i]] + rank[i];
+    for (int i = 0; i < I; ++i)
+        slot[i] = valid[i] ? s_start[dig[i]] + s_wc[wave * RADIX + dig[i]] + rank[i] : (uint32_t)TILE;
     lds_barrier();  // counters consumed: the staging area is reused
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const uint32_t sl = valid[i] ? slot[i] : (uint32_t)TILE;  // branch-free: invalid -> sink slot
-        s_keys[sl] = key[i];
-        s_vals[sl] = val[i];
+    for (int i = 0; i < I; ++i) {  // branch-free: invalid items go to the sink slot
+        s_keys[slot[i]] = key[i];
+        s_vals[slot[i]] = val[i];
     }
     lds_barrier();
 }
@@ -154,12 +160,12 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
 // Branch-free and fully unrolled, so the compiler's count of stores in flight is static (it can
 // then wait for the next tile's loads without draining these stores): slots past cnt repeat the
 // last valid element (an identical rewrite); an empty tile writes only to the sink element.
-template <int T, int I, int MODE>
+template <int T, int I, int R, int MODE>
 __device__ __forceinline__ void partition_store(Dig d, const unsigned char *s_raw, const uint32_t *s_toff,
                                                 uint32_t cnt, uint64_t sink, uint64_t *__restrict__ kout,
                                                 uint32_t *__restrict__ vout, uint64_t seq_base = 0) {
     const uint64_t *s_keys = reinterpret_cast<const uint64_t *>(s_raw);
-    const uint32_t *s_vals = reinterpret_cast<const uint32_t *>(s_raw + PartSmem<T, I>::kValOff);
+    const uint32_t *s_vals = reinterpret_cast<const uint32_t *>(s_raw + PartSmem<T, I, R>::kValOff);
 #pragma unroll
     for (int j = 0; j < I; ++j) {
         const uint32_t s = min(threadIdx.x + j * T, cnt - 1);  // cnt == 0: s stays in the tile
@@ -189,24 +195,26 @@ struct TileWalk {
 // ---------------------------------------------------------------------------------------------
 // L>=1: partition big buckets; tiles never cross bucket boundaries
 // ---------------------------------------------------------------------------------------------
+template <int R>
 __global__ __launch_bounds__(256) void msd_count_kernel(const uint32_t *__restrict__ t_start,
                                                         const uint32_t *__restrict__ t_count, Dig dl,
                                                         const uint64_t *__restrict__ kin,
                                                         uint32_t *__restrict__ tile_hist) {
-    __shared__ uint32_t s_hist[256];
+    constexpr int RADIX = 1 << R;
+    __shared__ uint32_t s_hist[RADIX];
     const int t = threadIdx.x;
-    s_hist[t] = 0;
+    for (int i = t; i < RADIX; i += 256) s_hist[i] = 0;
     lds_barrier();
     const uint64_t b = t_start[blockIdx.x];
     const uint32_t m = t_count[blockIdx.x];
     for (uint32_t i = t; i < m; i += 256) atomicAdd(&s_hist[dg_of(kin[b + i], dl)], 1u);
     lds_barrier();
-    tile_hist[(uint64_t)blockIdx.x * 256 + t] = s_hist[t];
+    for (int i = t; i < RADIX; i += 256) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
 }
 
 // persistent: grid = a multiple of 8 blocks, each walks its XCD's tiles; the next tile's keys
 // and starts are loaded while the current tile's runs are stored
-template <int T, int I, int MODE = 0>
+template <int T, int I, int R, int MODE = 0>
 __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restrict__ t_start,
                                                         const uint32_t *__restrict__ t_count, Dig dl,
                                                         const uint32_t *__restrict__ tile_off,
@@ -214,11 +222,12 @@ __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restri
                                                         const uint32_t *__restrict__ vin, uint64_t *__restrict__ kout,
                                                         uint32_t *__restrict__ vout, uint32_t ntiles,
                                                         uint64_t sink) {
-    using SM = PartSmem<T, I>;
+    using SM = PartSmem<T, I, R>;
+    constexpr int RADIX = SM::kRadix;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
-    __shared__ uint32_t s_toff[256];
-    __shared__ uint32_t s_wsum[4];
-    __shared__ uint32_t s_count;
+    __shared__ uint32_t s_toff[RADIX];
+    __shared__ uint32_t s_wsum[SM::kWaves];
+    __shared__ uint32_t s_start[RADIX + 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
     const TileWalk walk(ntiles);
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restri
     auto load = [&](uint32_t t) {
         const uint64_t b = t_start[t];
         m = t_count[t];  // >= 1
-        toff = tile_off[(uint64_t)t * 256 + (tid & 255)];  // every lane loads: no branch
+        toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
         uint32_t q0 = wave * (I * 64) + lane;
         asm volatile("" : "+v"(q0));  // keep the per-item offsets inside the loop (no hoisting)
 #pragma unroll
@@ -243,17 +252,18 @@ __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restri
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
         lds_barrier();  // the previous tile's runs have been read out of LDS
-        for (int i = tid; i < SM::kWaves * 256; i += T) s_wc[i] = 0;
-        if (tid < 256) s_toff[tid] = toff;
+        for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
+        if (tid < RADIX) s_toff[tid] = toff;
         lds_barrier();
         bool valid[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
-        partition_stage<T, I>(key, val, valid, dl, s_raw, s_toff, s_wsum, &s_count);
-        const uint32_t cnt = s_count;
+        uint32_t slot[I];
+        partition_stage<T, I, R>(key, val, valid, dl, s_raw, s_toff, s_wsum, s_start, slot);
+        const uint32_t cnt = s_start[RADIX];
         const uint64_t seq = (uint64_t)t * (T * I);
         if (t + walk.step < walk.end) load(t + walk.step);
-        partition_store<T, I, MODE>(dl, s_raw, s_toff, cnt, sink, kout, vout, seq);
+        partition_store<T, I, R, MODE>(dl, s_raw, s_toff, cnt, sink, kout, vout, seq);
     }
 }
 

@@ -103,7 +103,7 @@ static void msd_tables_for(Bufs &b, hipStream_t st, int tile, MsdTables &m) {
     CK(hipMalloc(&m.tile_off, 4 * 256 * m.tiles));
     CK(hipMemcpy(m.t_start, ts.data(), 4 * m.tiles, hipMemcpyHostToDevice));
     CK(hipMemcpy(m.t_count, tc.data(), 4 * m.tiles, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(msd_count_kernel, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count, Dig{54, 255u},
+    hipLaunchKernelGGL(msd_count_kernel<8>, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count, Dig{54, 255u},
                        b.k[0], m.tile_off);
     CK(hipStreamSynchronize(st));
     std::vector<uint32_t> h(256 * m.tiles);
@@ -137,7 +137,7 @@ static void run_msd(Bufs &b, MsdTables &m, const char *name, hipStream_t st, uns
     const int R = 4;
     for (int r = 0; r <= R; ++r) {
         CK(hipEventRecord(e0, st));
-        hipLaunchKernelGGL((msd_scatter_kernel<T, I, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+        hipLaunchKernelGGL((msd_scatter_kernel<T, I, 8, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
                            Dig{54, 255u}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n);
         CK(hipEventRecord(e1, st));
         CK(hipEventSynchronize(e1));
@@ -310,11 +310,12 @@ int main(int argc, char **argv) {
     run_scatter<49152>(b, st);
     run_scatter<98304>(b, st);
     MsdTables m;
-    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12", st, ref_sum);
-    run_msd<1024, 12, 1>(b, m, "msd pass T1024 I12 no-store", st, ref_sum);
-    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12 grid 512", st, ref_sum, 512);
-    run_msd<1024, 12, 3>(b, m, "msd pass T1024 I12 seq-store", st, ref_sum);
-    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12 grid 1024", st, ref_sum, 1024);
+    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12", st, ref_sum, 1024);
+    run_msd<1024, 12, 1>(b, m, "msd pass T1024 I12 no-store", st, ref_sum, 1024);
+    run_msd<512, 12, 0>(b, m, "msd pass T512 I12 grid 512", st, ref_sum, 512);
+    run_msd<512, 12, 0>(b, m, "msd pass T512 I12 grid 2048", st, ref_sum, 2048);
+    run_msd<512, 8, 0>(b, m, "msd pass T512 I8 grid 2048", st, ref_sum, 2048);
+    run_msd<256, 16, 0>(b, m, "msd pass T256 I16 grid 2048", st, ref_sum, 2048);
     if (argc > 2) return 0;
     const int R = 4;
     run_variant<256, 16, true>(b, "onesweep T256 I16 (current)", st, R, ref_sum);

@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-sample", type=int, default=16_000_000, help="k-mers in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the multi-GPU (all-to-all) path even at N = 1 (exercises it on one GPU)")
     ap.add_argument("--traffic", type=str, default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc (if present)")
     return ap.parse_args()
@@ -76,7 +78,7 @@ def load_traffic(path: str, kernel: str):
     try:
         with open(path) as fh:
             t = json.load(fh)
-        return t.get(kernel, {}).get("hbm_bytes_per_launch")
+        return t.get(kernel, {}).get("hbm_bytes_max_launch")
     except (OSError, ValueError):
         return None
 
@@ -92,10 +94,13 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
 
     from genome_kmers import _native
 
@@ -108,7 +113,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if world == 1:
+    if world == 1 and not args.sharded:
         eng = _native.Engine(local)
         t0 = time.perf_counter()
         eng.set_sequence(sba, np.zeros(1, dtype=np.uint32))
@@ -156,20 +161,44 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = n_units * args.steps / dt
 
-    # dominant kernel: one radix scatter pass; algorithmic bytes = read (key 8 B + start 4 B) +
-    # write (8 B + 4 B) per k-mer of the launch
-    rp = report.get("radix_pass", {"count": 0, "total_ms": 0.0})
-    local_n = eng.n if world == 1 else job.local_kmers
-    bytes_per_launch = local_n * 24
+    # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4
+    seq_bytes = L if dist is None else job.hi - job.lo
+
+    def stage_bytes(name, v):
+        u = v.get("units", 0)
+        if name == "msd_pass_l0":
+            return seq_bytes * v["count"] + 12 * u  # sequence bytes in, (key, start) out
+        if name.startswith("msd_pass_l"):
+            return 24 * u  # (key 8 B, start 4 B) in and out
+        if name.startswith("msd_local"):
+            return 25 * u  # (key, start) in and out + 1 head flag
+        if name == "msd_count":
+            return 8 * u
+        return 0
+
+    kernels = {}
+    for name, v in report.items():
+        b = stage_bytes(name, v)
+        if b and v["total_ms"] > 0:
+            kernels[name] = {"ms_per_launch": round(v["total_ms"] / v["count"], 4),
+                             "gbs": round(b / (v["total_ms"] * 1e-3) / 1e9, 1)}
+    # dominant kernel: the largest partition pass (msd_scatter_kernel, level >= 1) or, when a
+    # genome needs none, the L0 pass
+    cands = [n for n in report if n.startswith("msd_pass_l") and n != "msd_pass_l0" and report[n]["units"]]
+    dom = max(cands, key=lambda n: report[n]["total_ms"]) if cands else "msd_pass_l0"
+    rp = report.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
     avg_ms = rp["total_ms"] / max(rp["count"], 1)
+    bytes_per_launch = stage_bytes(dom, rp) / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
-    traffic = load_traffic(args.traffic, "onesweep_kernel")
+    kname = "msd_scatter_kernel" if dom != "msd_pass_l0" else "msd0_scatter_kernel"
+    traffic = load_traffic(args.traffic, kname)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "onesweep_kernel<1> (one 8-bit LSD radix pass)", "avg_launch_ms": round(avg_ms, 4),
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "pipeline_read_frac": round(n_units * 105 / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)}
+                "kernel": f"{kname}<1024,12,8> ({dom}: one stable 8-bit MSD partition pass)",
+                "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "units_per_launch": int(rp["units"] / max(rp["count"], 1)), "bytes_per_unit": 24,
+                "stages": kernels}
 
     if rank == 0:
         cpu = None
@@ -183,7 +212,8 @@ def main():
             "data": f"synthetic: uniform random ACGT, numpy PCG64 seed {args.seed}",
             "config": {"workload": f"C3: {L:,}-base synthetic single-contig genome, k={k} (min=max={k})",
                        "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
-                       "parallelism": f"position-range shards x{world} + 1 RCCL all-to-all" if world > 1 else "1 GPU",
+                       "parallelism": (f"position-range shards x{world} + 1 RCCL all-to-all" if dist is not None
+                                       else "1 GPU"),
                        "h2d_sba_ms": round(h2d_ms, 2), "stages_ms_per_step": stages},
             "roofline": roofline,
             "cpu_baseline": cpu,

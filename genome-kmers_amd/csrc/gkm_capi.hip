@@ -60,6 +60,10 @@ void timer_end(gk_ctx *c, int slot) {
     hipEventRecord(c->timers[slot].stop, c->stream);
 }
 
+void timer_units(gk_ctx *c, int slot, uint64_t units) {
+    if (slot >= 0 && c->profile) c->timers[slot].units = units;
+}
+
 // ---------------------------------------------------------------------------------------------
 // prefix-doubling kernels
 // ---------------------------------------------------------------------------------------------
@@ -673,25 +677,95 @@ extern "C" int gk_profile_enable(gk_ctx *c, int on) {
 extern "C" int gk_profile_report(gk_ctx *c, char *buf, uint64_t buflen) {
     if (!c || !buf || buflen == 0) return GK_E_ARG;
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    std::map<std::string, std::pair<uint64_t, double>> agg;
+    struct Agg {
+        uint64_t count = 0, units = 0;
+        double ms = 0;
+    };
+    std::map<std::string, Agg> agg;
     for (auto &t : c->timers) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
             auto &a = agg[t.name];
-            a.first += 1;
-            a.second += ms;
+            a.count += 1;
+            a.ms += ms;
+            a.units += t.units;
         }
     }
     std::string s = "{";
     bool first = true;
     for (auto &kv : agg) {
-        char tmp[256];
-        std::snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f}", first ? "" : ", ",
-                      kv.first.c_str(), (unsigned long long)kv.second.first, kv.second.second);
+        char tmp[320];
+        std::snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f, \"units\": %llu}",
+                      first ? "" : ", ", kv.first.c_str(), (unsigned long long)kv.second.count, kv.second.ms,
+                      (unsigned long long)kv.second.units);
         s += tmp;
         first = false;
     }
     s += "}";
     std::snprintf(buf, (size_t)buflen, "%s", s.c_str());
     return s.size() < buflen ? GK_OK : GK_E_ARG;
+}
+
+// ---------------------------------------------------------------------------------------------
+// multi-GPU shards
+// ---------------------------------------------------------------------------------------------
+static int shard_spec(gk_ctx *c, uint32_t k, KeySpec *ks) {
+    const int bits = c->acgt ? 2 : 4;
+    if (k == 0 || (uint64_t)bits * k > 64) return fail(c, GK_E_ARG, "shard k-mers must fit one 64-bit key");
+    *ks = KeySpec{};
+    ks->bits = bits;
+    ks->symbols = (int)k;
+    ks->min_len = (int)k;
+    ks->lenbits = 0;
+    ks->words = 1;
+    ks->total_bits = bits * (int)k;
+    return GK_OK;
+}
+
+extern "C" int gk_shard_bucket_bits(void) { return gkm::msd_radix_bits(); }
+
+extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint64_t *d_keys,
+                                  uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out) {
+    if (!c || !d_keys || !d_starts || !h_hist || !n_out) return GK_E_ARG;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
+    if (hi > c->sba_len) hi = c->sba_len;
+    if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
+    KeySpec ks;
+    int rc = shard_spec(c, k, &ks);
+    if (rc != GK_OK) return rc;
+    return msd_shard_partition(c, ks, lo, std::max(hi, lo), d_keys, d_starts, cap, h_hist, n_out);
+}
+
+extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
+                             const uint64_t *h_piece_off, const uint64_t *h_piece_len,
+                             const uint32_t *h_piece_bucket, uint32_t npieces) {
+    if (!c || (n && (!d_keys || !d_starts || !h_piece_off || !h_piece_len || !h_piece_bucket))) return GK_E_ARG;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (n > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
+    KeySpec ks;
+    int rc = shard_spec(c, k, &ks);
+    if (rc != GK_OK) return rc;
+    for (uint32_t i = 1; i < npieces; ++i)
+        if (h_piece_bucket[i] < h_piece_bucket[i - 1]) return fail(c, GK_E_ARG, "pieces must be in bucket order");
+    rc = ensure_elems(c, std::max<uint64_t>(n, 1), 1);
+    if (rc != GK_OK) return rc;
+    c->n = n;
+    c->min_k = k;
+    c->have_starts = true;
+    c->enumerated = false;
+    c->starts_materialized = true;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
+    if (n > 0) {
+        rc = msd_shard_sort(c, ks, d_keys, d_starts, h_piece_off, h_piece_len, h_piece_bucket, npieces);
+        if (rc != GK_OK) return rc;
+    } else {
+        c->cur = 0;
+    }
+    c->spec = ks;
+    c->keys_valid = true;
+    c->keys_are_ranks = false;
+    c->sorted = true;
+    c->sort_len = k;
+    return GK_OK;
 }

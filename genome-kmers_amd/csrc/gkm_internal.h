@@ -54,6 +54,7 @@ struct KeySpec {
 struct Timer {
     std::string name;
     hipEvent_t start, stop;
+    uint64_t units = 0;  // work items the timed launch processed (k-mers), 0 = not recorded
 };
 
 }  // namespace gkm
@@ -152,8 +153,16 @@ inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) 
 }
 // MSD sort of one-word keys from the enumerated positions (gkm_msd.hip)
 int msd_sort(gk_ctx *c, const KeySpec &ks);
+// multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the
+// top msd_radix_bits() key bits; receive-side sort of buckets given as pieces
+int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,
+                        uint64_t cap, uint64_t *hist, uint64_t *count);
+int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint32_t *vin, const uint64_t *poff,
+                   const uint64_t *plen, const uint32_t *pbucket, uint32_t np);
+int msd_radix_bits();
 void timer_begin(gk_ctx *c, const char *name, int *slot);
 void timer_end(gk_ctx *c, int slot);
+void timer_units(gk_ctx *c, int slot, uint64_t units);
 int fail(gk_ctx *c, int code, const std::string &msg);
 int hip_fail(gk_ctx *c, hipError_t e, const char *where);
 

@@ -31,7 +31,7 @@ constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk
 constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
 constexpr int kBlockMax = kBT * kBI;    // 4096
-constexpr int kWT = 64, kWI = 4, kWR = 6;    // wave-local: 64 threads x 4 keys, 6-bit digit
+constexpr int kWT = 64, kWI = 4, kWR = 8;    // wave-local: 64 threads x 4 keys, 8-bit digit
 constexpr int kWaveMax = kWT * kWI;     // 256
 constexpr int kSmall = 24;              // sub-buckets <= this: rank-by-count
 
@@ -57,6 +57,7 @@ static hipError_t msd_tables() {
 // pad after the array is '$').
 struct L0Args {
     const uint8_t *sba;
+    uint64_t lo, hi;  // k-mer starts in [lo, hi) (lo a multiple of 32: 16-B aligned tiles)
     int symbols, total_bits;
 };
 
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     if (t < 256) s_lut4[t] = c_code4_msd[t];
     for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
     lds_barrier();
-    const uint64_t P0 = (uint64_t)blockIdx.x * TILE;
+    const uint64_t P0 = a.lo + (uint64_t)blockIdx.x * TILE;
     uint4 ra, rb;
     l0_load<BITS, TILE>(a.sba + P0, ra, rb);
     l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         const uint32_t p = i * T + t;
-        if (l0_valid(s_dol, p, a.symbols)) atomicAdd(&s_hist[dg_of(l0_key<BITS>(s_code, p, a.total_bits), d0)], 1u);
+        if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi)
+            atomicAdd(&s_hist[dg_of(l0_key<BITS>(s_code, p, a.total_bits), d0)], 1u);
     }
     lds_barrier();
     for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
     uint4 ra, rb;
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
-        l0_load<BITS, TILE>(a.sba + (uint64_t)t * TILE, ra, rb);
+        l0_load<BITS, TILE>(a.sba + a.lo + (uint64_t)t * TILE, ra, rb);
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
     };
     if (walk.first < walk.end) load(walk.first);
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
         if (tid < RADIX) s_toff[tid] = toff;
         l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
         lds_barrier();
-        const uint64_t P0 = (uint64_t)t * TILE;
+        const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         uint64_t key[I];
         uint32_t val[I], slot[I];
         bool valid[I];
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = p0 + i * 64;
-            valid[i] = l0_valid(s_dol, p, a.symbols);
+            valid[i] = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi;
             key[i] = l0_key<BITS>(s_code, p, a.total_bits);
             val[i] = (uint32_t)(P0 + p);
         }
@@ -334,13 +336,71 @@ __device__ __forceinline__ void route(uint32_t st, uint32_t size, int hi, int B,
     if (wav) L.wav[d] = local_entry(st, size, hi, parity);
 }
 
-// the sub-buckets of one global level
-__global__ __launch_bounds__(256) void classify_kernel(const uint32_t *__restrict__ seg_base,
-                                                       const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
-                                                       int B, int parity, Lists L, uint32_t *__restrict__ ctr) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool in = i < nsub;
-    route(in ? seg_base[i] : 0, in ? seg_cnt[i] : 0, hi, B, parity, true, L, ctr, threadIdx.x & 63);
+// The sub-buckets of one global level, one per thread: a workgroup-aggregated append (one
+// atomic per list per workgroup) into the next-level / done / block-local / wave-local lists;
+// sums[l] += elements routed to list l (for the profile's work counts).
+constexpr int kClassT = 1024;
+
+__global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__restrict__ seg_base,
+                                                           const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
+                                                           int B, int parity, Lists L, uint32_t *__restrict__ ctr,
+                                                           unsigned long long *__restrict__ sums) {
+    constexpr int NW = kClassT / 64;
+    __shared__ uint32_t s_cnt[4][NW];
+    __shared__ uint32_t s_elems[4][NW];
+    __shared__ uint32_t s_base[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * kClassT + tid;
+    const uint32_t size = i < nsub ? seg_cnt[i] : 0, st = i < nsub ? seg_base[i] : 0;
+    const bool live = size >= 1;
+    const bool done = live && hi >= B;
+    const bool big = live && !done && size > (uint32_t)kBlockMax;
+    const bool blk = live && !done && !big && size > (uint32_t)kWaveMax;
+    const bool wav = live && !done && !big && !blk;
+    const bool f[4] = {big, done, blk, wav};  // list order = kCtrBig, kCtrDone, kCtrBlock, kCtrWave
+    uint32_t below[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const uint64_t m = __ballot(f[l]);
+        below[l] = lanes_below(m);
+        uint32_t e = f[l] ? size : 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) e += __shfl_xor(e, off);
+        if (lane == 0) {
+            s_cnt[l][wave] = (uint32_t)__popcll(m);
+            s_elems[l][wave] = e;
+        }
+    }
+    __syncthreads();
+    if (tid < 4) {
+        uint32_t tot = 0;
+        unsigned long long el = 0;
+        for (int w = 0; w < NW; ++w) {
+            tot += s_cnt[tid][w];
+            el += s_elems[tid][w];
+        }
+        s_base[tid] = tot ? atomicAdd(&ctr[tid], tot) : 0;
+        if (el) atomicAdd(&sums[tid], el);
+    }
+    __syncthreads();
+    uint32_t at[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        uint32_t pre = s_base[l];
+        for (int w = 0; w < wave; ++w) pre += s_cnt[l][w];
+        at[l] = pre + below[l];
+    }
+    if (big) {
+        L.nb_start[at[0]] = st;
+        L.nb_len[at[0]] = size;
+    }
+    if (done) {
+        L.dn_start[at[1]] = st;
+        L.dn_len[at[1]] = size;
+        L.dn_par[at[1]] = (uint8_t)parity;
+    }
+    if (blk) L.blk[at[2]] = local_entry(st, size, hi, parity);
+    if (wav) L.wav[at[3]] = local_entry(st, size, hi, parity);
 }
 
 // tile + chunk tables of a bucket list (one thread per bucket)
@@ -541,20 +601,6 @@ static int grid_n(uint64_t n) { return (int)std::max<uint64_t>((n + 255) / 256, 
 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
 
-// scan per-tile histograms of the bucket list (nseg buckets, C chunks) into per-tile offsets
-static int scan_offsets(gk_ctx *c, uint32_t *tile_hist, uint32_t *chunk_hist, const uint32_t *c_first,
-                        const uint32_t *c_ntiles, uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks,
-                        const uint32_t *s_start, uint64_t nseg, uint32_t *seg_base, uint32_t *seg_cnt) {
-    hipLaunchKernelGGL(chunk_sum_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist, c_first,
-                       c_ntiles, chunk_hist);
-    hipLaunchKernelGGL(seg_scan_kernel<kGRadix>, dim3((unsigned)nseg), dim3(kGRadix), 0, c->stream, chunk_hist,
-                       s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
-    hipLaunchKernelGGL(tile_apply_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist, c_first,
-                       c_ntiles, chunk_hist);
-    GK_TRY_HIP(c, hipGetLastError());
-    return GK_OK;
-}
-
 // grow a device array to hold `need` entries, keeping the first `keep` entries
 template <typename T>
 static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t keep, T **p) {
@@ -580,232 +626,400 @@ static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t
     return hipSuccess;
 }
 
-// partition grid: 4 workgroups per CU (one resident at a time: LDS-bound), a multiple of 8 (equal
-// shares per XCD); measured 4% faster than exactly one per CU (profiles/r1/README.md)
 static unsigned cu_count(gk_ctx *c) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus < 8) cus = 256;
     return (unsigned)(cus / 8 * 8);
 }
 
-static int read_ctr(gk_ctx *c, const uint32_t *d, uint32_t *h, int count) {
-    GK_TRY_HIP(c, hipMemcpyAsync(h, d, 4 * count, hipMemcpyDeviceToHost, c->stream));
-    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    return GK_OK;
-}
-
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
 
-int msd_sort(gk_ctx *c, const KeySpec &ks) {
-    GK_TRY_HIP(c, msd_tables());
-    int total_slot, slot;
-    timer_begin(c, "msd_total", &total_slot);
-    const int B = ks.total_bits;
-    const uint64_t n = c->n, L = c->sba_len;
-    const unsigned cus = cu_count(c);
-    uint32_t *ctr, h[kCtrN];
-    GK_TRY_HIP(c, scratch(c, "msd_ctr", kCtrN, &ctr));
-    GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
-
-    // lists: big (ping-pong), done, and two generations of block/wave lists; a local round
-    // re-lists at most n / (kSmall + 1) sub-buckets
-    const uint64_t max_big = n / kBlockMax + 2, max_spill = n / (kSmall + 1) + 1024;
+// One MSD sort of one-word keys into keys[0] / vals[0] (+ group heads).  The first partition
+// comes from the sequence (run_l0) or from received buckets (first_level_from_pieces); the rest
+// -- global levels while buckets exceed kBlockMax, local rounds, done copies -- is common.
+struct MsdDriver {
+    gk_ctx *c;
+    KeySpec ks;
+    int B;
+    uint64_t n = 0;
+    unsigned cus, pgrid;
+    int slot = -1, total_slot = -1;
+    uint32_t *ctr = nullptr, h[kCtrN] = {0};
+    unsigned long long *sums = nullptr, hs[4] = {0};
     uint32_t *big_start[2], *big_len[2];
-    GK_TRY_HIP(c, scratch(c, "big_start0", max_big, &big_start[0]));
-    GK_TRY_HIP(c, scratch(c, "big_len0", max_big, &big_len[0]));
-    GK_TRY_HIP(c, scratch(c, "big_start1", max_big, &big_start[1]));
-    GK_TRY_HIP(c, scratch(c, "big_len1", max_big, &big_len[1]));
     uint32_t *dn_start, *dn_len;
     uint8_t *dn_par;
-    GK_TRY_HIP(c, grow_keep(c, "dn_start", 1024, 0, &dn_start));
-    GK_TRY_HIP(c, grow_keep(c, "dn_len", 1024, 0, &dn_len));
-    GK_TRY_HIP(c, grow_keep(c, "dn_par", 1024, 0, &dn_par));
     uint2 *blk[2], *wav[2];
-    GK_TRY_HIP(c, grow_keep(c, "blk0", 1024, 0, &blk[0]));
-    GK_TRY_HIP(c, grow_keep(c, "wav0", 1024, 0, &wav[0]));
-    uint8_t *heads;
-    GK_TRY_HIP(c, scratch(c, "msd_heads", n + 64, &heads));
-    auto lists = [&](int g, int bigsel) {
-        return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par, blk[g], wav[g]};
-    };
+    uint8_t *heads = nullptr;
+    uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
+    uint64_t nblk = 0, nwav = 0, ndone = 0, big_elems = 0, blk_elems = 0, wav_elems = 0;
+    uint32_t nbig = 0;
+    int cur_big = 0;
 
-    // ---- L0: one bucket (all k-mers), tiles over sba positions ----
-    const uint64_t nt0 = (L + kPTile - 1) / kPTile;
-    const uint64_t nc0 = (nt0 + kChunkTiles - 1) / kChunkTiles;
-    uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *s_misc, *seg_base, *seg_cnt;
-    GK_TRY_HIP(c, scratch(c, "tile_hist", nt0 * kGRadix, &tile_hist));
-    GK_TRY_HIP(c, scratch(c, "chunk_hist", nc0 * kGRadix, &chunk_hist));
-    GK_TRY_HIP(c, scratch(c, "c_first", nc0, &c_first));
-    GK_TRY_HIP(c, scratch(c, "c_ntiles", nc0, &c_ntiles));
-    GK_TRY_HIP(c, scratch(c, "s_misc", 4, &s_misc));
-    GK_TRY_HIP(c, scratch(c, "seg_base", kGRadix, &seg_base));
-    GK_TRY_HIP(c, scratch(c, "seg_cnt", kGRadix, &seg_cnt));
-    {
-        std::vector<uint32_t> cf(nc0), cn(nc0);
-        for (uint64_t j = 0; j < nc0; ++j) {
-            cf[j] = (uint32_t)(j * kChunkTiles);
-            cn[j] = (uint32_t)std::min<uint64_t>(kChunkTiles, nt0 - j * kChunkTiles);
-        }
-        const uint32_t misc[3] = {0, (uint32_t)nc0, 0};  // s_cfirst, s_nchunks, s_start
-        GK_TRY_HIP(c, hipMemcpyAsync(c_first, cf.data(), 4 * nc0, hipMemcpyHostToDevice, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(c_ntiles, cn.data(), 4 * nc0, hipMemcpyHostToDevice, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(s_misc, misc, 12, hipMemcpyHostToDevice, c->stream));
-        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    MsdDriver(gk_ctx *c_, const KeySpec &ks_) : c(c_), ks(ks_), B(ks_.total_bits) {
+        cus = cu_count(c);
+        pgrid = cus * 4;  // 4 workgroups per CU, one resident at a time (LDS); measured faster than 1
     }
-    const L0Args a{c->sba, ks.symbols, B};
-    const Dig d0 = dig_at(B, 0, kGR);
-    timer_begin(c, "msd_l0_count", &slot);
-    if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a, d0,
-                           tile_hist);
-    else
-        hipLaunchKernelGGL((msd0_count_kernel<4, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a, d0,
-                           tile_hist);
-    GK_TRY_HIP(c, hipGetLastError());
-    timer_end(c, slot);
-    timer_begin(c, "msd_scan", &slot);
-    int rc = scan_offsets(c, tile_hist, chunk_hist, c_first, c_ntiles, nc0, s_misc, s_misc + 1, s_misc + 2, 1,
-                          seg_base, seg_cnt);
-    if (rc != GK_OK) return rc;
-    timer_end(c, slot);
-    timer_begin(c, "msd_pass_l0", &slot);
-    const unsigned pgrid = cus * 4;
-    if (ks.bits == 2)
-        hipLaunchKernelGGL((msd0_scatter_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
-                           tile_hist, c->keys[0], c->vals[0], (uint32_t)nt0, n);
-    else
-        hipLaunchKernelGGL((msd0_scatter_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
-                           tile_hist, c->keys[0], c->vals[0], (uint32_t)nt0, n);
-    GK_TRY_HIP(c, hipGetLastError());
-    timer_end(c, slot);
 
-    // ---- classify L0's sub-buckets; then global levels while buckets exceed kBlockMax ----
-    uint64_t nblk = 0, nwav = 0, ndone = 0;
-    auto classify = [&](uint64_t nsub, int hi, int parity, int bigsel) -> int {
-        // capacity: every sub-bucket could land in any one list
+    Lists lists(int g, int bigsel) {
+        return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par, blk[g], wav[g]};
+    }
+
+    int init(uint64_t n_) {
+        n = n_;
+        GK_TRY_HIP(c, msd_tables());
+        GK_TRY_HIP(c, scratch(c, "msd_ctr", kCtrN, &ctr));
+        GK_TRY_HIP(c, scratch(c, "msd_sums", 4, &sums));
+        GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
+        const uint64_t max_big = n / kBlockMax + 2;
+        GK_TRY_HIP(c, scratch(c, "big_start0", max_big, &big_start[0]));
+        GK_TRY_HIP(c, scratch(c, "big_len0", max_big, &big_len[0]));
+        GK_TRY_HIP(c, scratch(c, "big_start1", max_big, &big_start[1]));
+        GK_TRY_HIP(c, scratch(c, "big_len1", max_big, &big_len[1]));
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", 1024, 0, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", 1024, 0, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", 1024, 0, &dn_par));
+        GK_TRY_HIP(c, grow_keep(c, "blk0", 1024, 0, &blk[0]));
+        GK_TRY_HIP(c, grow_keep(c, "wav0", 1024, 0, &wav[0]));
+        GK_TRY_HIP(c, scratch(c, "msd_heads", n + 64, &heads));
+        return GK_OK;
+    }
+
+    int read_ctr() {
+        GK_TRY_HIP(c, hipMemcpyAsync(h, ctr, 4 * 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(hs, sums, 8 * 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        return GK_OK;
+    }
+
+    // scan per-tile histograms of nseg buckets (C chunks) into per-tile offsets + sub-bucket tables
+    int scan_offsets(uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start,
+                     uint64_t nseg) {
+        timer_begin(c, "msd_scan", &slot);
+        hipLaunchKernelGGL(chunk_sum_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist,
+                           c_first, c_ntiles, chunk_hist);
+        hipLaunchKernelGGL(seg_scan_kernel<kGRadix>, dim3((unsigned)nseg), dim3(kGRadix), 0, c->stream, chunk_hist,
+                           s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
+        hipLaunchKernelGGL(tile_apply_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist,
+                           c_first, c_ntiles, chunk_hist);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        return GK_OK;
+    }
+
+    // tile / chunk tables: device buffers sized for T tiles, C chunks, nseg buckets
+    int tables(uint64_t T, uint64_t C, uint64_t nseg) {
+        GK_TRY_HIP(c, scratch(c, "tile_hist", T * kGRadix, &tile_hist));
+        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * kGRadix, &chunk_hist));
+        GK_TRY_HIP(c, scratch(c, "c_first", C, &c_first));
+        GK_TRY_HIP(c, scratch(c, "c_ntiles", C, &c_ntiles));
+        GK_TRY_HIP(c, scratch(c, "seg_base", nseg * kGRadix, &seg_base));
+        GK_TRY_HIP(c, scratch(c, "seg_cnt", nseg * kGRadix, &seg_cnt));
+        return GK_OK;
+    }
+
+    // L0: encode the k-mers starting in [lo, hi) and partition them by the top kGR key bits into
+    // kout / vout (capacity >= n + 1: element n is the scatter's sink).  seg_base / seg_cnt then
+    // hold the kGRadix buckets.  *count: k-mers found (checked against cap before the scatter).
+    int run_l0(uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout, uint64_t cap, uint64_t *count) {
+        const uint64_t span = hi > lo ? hi - lo : 0;
+        const uint64_t nt0 = std::max<uint64_t>((span + kPTile - 1) / kPTile, 1);
+        const uint64_t nc0 = (nt0 + kChunkTiles - 1) / kChunkTiles;
+        int rc = tables(nt0, nc0, 1);
+        if (rc != GK_OK) return rc;
+        uint32_t *s_misc;
+        GK_TRY_HIP(c, scratch(c, "s_misc", 4, &s_misc));
+        {
+            std::vector<uint32_t> cf(nc0), cn(nc0);
+            for (uint64_t j = 0; j < nc0; ++j) {
+                cf[j] = (uint32_t)(j * kChunkTiles);
+                cn[j] = (uint32_t)std::min<uint64_t>(kChunkTiles, nt0 - j * kChunkTiles);
+            }
+            const uint32_t misc[3] = {0, (uint32_t)nc0, 0};  // s_cfirst, s_nchunks, s_start
+            GK_TRY_HIP(c, hipMemcpyAsync(c_first, cf.data(), 4 * nc0, hipMemcpyHostToDevice, c->stream));
+            GK_TRY_HIP(c, hipMemcpyAsync(c_ntiles, cn.data(), 4 * nc0, hipMemcpyHostToDevice, c->stream));
+            GK_TRY_HIP(c, hipMemcpyAsync(s_misc, misc, 12, hipMemcpyHostToDevice, c->stream));
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        }
+        const L0Args a{c->sba, lo, hi, ks.symbols, B};
+        const Dig d0 = dig_at(B, 0, kGR);
+        timer_begin(c, "msd_l0_count", &slot);
+        if (ks.bits == 2)
+            hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
+                               d0, tile_hist);
+        else
+            hipLaunchKernelGGL((msd0_count_kernel<4, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
+                               d0, tile_hist);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        rc = scan_offsets(nc0, s_misc, s_misc + 1, s_misc + 2, 1);
+        if (rc != GK_OK) return rc;
+        // the bucket total = k-mers found (the last bucket's base + count)
+        uint32_t last[2];
+        GK_TRY_HIP(c, hipMemcpyAsync(&last[0], seg_base + kGRadix - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(&last[1], seg_cnt + kGRadix - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        *count = (uint64_t)last[0] + last[1];
+        if (*count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
+        timer_begin(c, "msd_pass_l0", &slot);
+        timer_units(c, slot, *count);
+        if (ks.bits == 2)
+            hipLaunchKernelGGL((msd0_scatter_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, (uint32_t)nt0, *count);
+        else
+            hipLaunchKernelGGL((msd0_scatter_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, (uint32_t)nt0, *count);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        return GK_OK;
+    }
+
+    // route nsub sub-buckets (seg_base / seg_cnt) of a level; hi = key bits sorted after it
+    int classify(uint64_t nsub, int hi, int parity, int bigsel) {
         GK_TRY_HIP(c, grow_keep(c, "blk0", nblk + nsub, nblk, &blk[0]));
         GK_TRY_HIP(c, grow_keep(c, "wav0", nwav + nsub, nwav, &wav[0]));
         GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nsub, ndone, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nsub, ndone, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nsub, ndone, &dn_par));
         GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * 4, c->stream));
         timer_begin(c, "msd_classify", &slot);
-        hipLaunchKernelGGL(classify_kernel, dim3(grid_n(nsub)), dim3(256), 0, c->stream, seg_base, seg_cnt, nsub, hi, B,
-                           parity, lists(0, bigsel), ctr);
+        hipLaunchKernelGGL(classify_kernel, dim3((unsigned)((nsub + kClassT - 1) / kClassT)), dim3(kClassT), 0,
+                           c->stream, seg_base, seg_cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        int r = read_ctr(c, ctr, h, 4);
+        int r = read_ctr();
         if (r != GK_OK) return r;
         nblk = h[kCtrBlock];
         nwav = h[kCtrWave];
         ndone = h[kCtrDone];
-        return GK_OK;
-    };
-    int cur_big = 0;
-    rc = classify(kGRadix, kGR, 0, cur_big);
-    if (rc != GK_OK) return rc;
-    uint32_t nbig = h[kCtrBig];
-    int level = 1, in = 0;
-    while (nbig > 0) {
-        const int out = in ^ 1;
-        const int hi = level * kGR;
-        uint32_t *ntl, *nch, *tfirst, *cfirst;
-        GK_TRY_HIP(c, scratch(c, "s_ntiles", nbig, &ntl));
-        GK_TRY_HIP(c, scratch(c, "s_nchunks", nbig, &nch));
-        GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
-        GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
-        hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big], nbig,
-                           (uint32_t)kPTile, ntl, nch);
-        GK_TRY_HIP(c, hipGetLastError());
-        uint64_t T = 0, C = 0;
-        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, ntl, nbig, tfirst, &T));
-        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, nch, nbig, cfirst, &C));
-        uint32_t *t_start, *t_count;
-        GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
-        GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));
-        GK_TRY_HIP(c, scratch(c, "tile_hist", T * kGRadix, &tile_hist));
-        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * kGRadix, &chunk_hist));
-        GK_TRY_HIP(c, scratch(c, "c_first", C, &c_first));
-        GK_TRY_HIP(c, scratch(c, "c_ntiles", C, &c_ntiles));
-        GK_TRY_HIP(c, scratch(c, "seg_base", (uint64_t)nbig * kGRadix, &seg_base));
-        GK_TRY_HIP(c, scratch(c, "seg_cnt", (uint64_t)nbig * kGRadix, &seg_cnt));
-        hipLaunchKernelGGL(tile_table_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
-                           big_len[cur_big], tfirst, cfirst, nbig, (uint32_t)kPTile, t_start, t_count, c_first,
-                           c_ntiles);
-        const Dig dl = dig_at(B, hi, kGR);
-        timer_begin(c, "msd_count", &slot);
-        hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
-                           c->keys[in], tile_hist);
-        GK_TRY_HIP(c, hipGetLastError());
-        timer_end(c, slot);
-        timer_begin(c, "msd_scan", &slot);
-        rc = scan_offsets(c, tile_hist, chunk_hist, c_first, c_ntiles, C, cfirst, nch, big_start[cur_big], nbig,
-                          seg_base, seg_cnt);
-        if (rc != GK_OK) return rc;
-        timer_end(c, slot);
-        timer_begin(c, kPassNames[level & 7], &slot);
-        hipLaunchKernelGGL((msd_scatter_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
-                           dl, tile_hist, c->keys[in], c->vals[in], c->keys[out], c->vals[out], (uint32_t)T, n);
-        GK_TRY_HIP(c, hipGetLastError());
-        timer_end(c, slot);
-        cur_big ^= 1;
-        rc = classify((uint64_t)nbig * kGRadix, hi + kGR, out, cur_big);
-        if (rc != GK_OK) return rc;
         nbig = h[kCtrBig];
-        ++level;
-        in = out;
+        big_elems = hs[kCtrBig];
+        blk_elems += hs[kCtrBlock];
+        wav_elems += hs[kCtrWave];
+        return GK_OK;
     }
 
-    // ---- local rounds: generation g lists -> re-listed sub-buckets in generation g ^ 1 ----
-    GK_TRY_HIP(c, grow_keep(c, "blk0", std::max<uint64_t>(nblk, max_spill), nblk, &blk[0]));
-    GK_TRY_HIP(c, grow_keep(c, "wav0", std::max<uint64_t>(nwav, max_spill), nwav, &wav[0]));
-    GK_TRY_HIP(c, grow_keep(c, "blk1", max_spill, 0, &blk[1]));
-    GK_TRY_HIP(c, grow_keep(c, "wav1", max_spill, 0, &wav[1]));
-    GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
-    GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
-    GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
-    int g = 0, round = 0;
-    while (nblk + nwav > 0) {
-        const int ng = g ^ 1;
-        // the re-list counters of this round start from 0 (the done count carries on)
-        const uint32_t zero2[2] = {0, 0};
-        GK_TRY_HIP(c, hipMemcpyAsync(ctr + kCtrBlock, zero2, 8, hipMemcpyHostToDevice, c->stream));
-        const Lists nl = lists(ng, 0);
-        if (nblk) {
-            timer_begin(c, round == 0 ? "msd_local_block" : "msd_local_block_r", &slot);
-            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>), dim3((unsigned)std::min<uint64_t>(nblk, cus * 8)),
-                               dim3(kBT), 0, c->stream, blk[g], (uint32_t)nblk, B, c->keys[0], c->vals[0], c->keys[1],
-                               c->vals[1], heads, nl, ctr);
-            GK_TRY_HIP(c, hipGetLastError());
-            timer_end(c, slot);
-        }
-        if (nwav) {
-            timer_begin(c, round == 0 ? "msd_local_wave" : "msd_local_wave_r", &slot);
-            hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, kWR>), dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)),
-                               dim3(kWT), 0, c->stream, wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1],
-                               c->vals[1], heads, nl, ctr);
-            GK_TRY_HIP(c, hipGetLastError());
-            timer_end(c, slot);
-        }
-        rc = read_ctr(c, ctr, h, 4);
-        if (rc != GK_OK) return rc;
-        nblk = h[kCtrBlock];
-        nwav = h[kCtrWave];
-        ndone = h[kCtrDone];
-        g = ng;
-        if (++round > 64) return fail(c, GK_E_HIP, "msd local rounds did not converge");
-    }
-    if (ndone > 0) {
-        hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len, dn_par,
-                           c->keys[1], c->vals[1], c->keys[0], c->vals[0], heads);
+    // one global partition level over tiles already in t_start / t_count (T tiles, C chunks,
+    // nseg buckets), reading kin / vin, writing keys[out] / vals[out]
+    int level_pass(int level, int hi, const uint32_t *t_start, const uint32_t *t_count, uint64_t T, uint64_t C,
+                   const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start, uint64_t nseg,
+                   const uint64_t *kin, const uint32_t *vin, int out) {
+        const Dig dl = dig_at(B, hi, kGR);
+        timer_begin(c, "msd_count", &slot);
+        timer_units(c, slot, big_elems);
+        hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl, kin,
+                           tile_hist);
         GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        int rc = scan_offsets(C, s_cfirst, s_nchunks, s_start, nseg);
+        if (rc != GK_OK) return rc;
+        timer_begin(c, kPassNames[level & 7], &slot);
+        timer_units(c, slot, big_elems);
+        hipLaunchKernelGGL((msd_scatter_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
+                           dl, tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        return GK_OK;
     }
-    timer_end(c, total_slot);
-    c->heads = heads;
-    c->heads_valid = true;
-    c->cur = 0;
+
+    // first level from received buckets: pieces (off, len) of kin / vin, grouped by top-kGR-bit
+    // bucket in ascending bucket order, pieces of a bucket in the order their elements must keep
+    int first_level_from_pieces(const uint64_t *kin, const uint32_t *vin, const uint64_t *poff, const uint64_t *plen,
+                                const uint32_t *pbucket, uint32_t np) {
+        std::vector<uint32_t> ts, tc, cf, cn, scf, snc, sst;
+        uint64_t out_base = 0;
+        for (uint32_t i = 0; i < np;) {
+            uint32_t j = i;
+            uint64_t tot = 0;
+            const uint64_t tile0 = ts.size();
+            while (j < np && pbucket[j] == pbucket[i]) {
+                for (uint64_t o = 0; o < plen[j]; o += kPTile) {
+                    ts.push_back((uint32_t)(poff[j] + o));
+                    tc.push_back((uint32_t)std::min<uint64_t>(kPTile, plen[j] - o));
+                }
+                tot += plen[j];
+                ++j;
+            }
+            if (tot > 0) {
+                const uint64_t nt = ts.size() - tile0;
+                scf.push_back((uint32_t)cf.size());
+                for (uint64_t t = 0; t < nt; t += kChunkTiles) {
+                    cf.push_back((uint32_t)(tile0 + t));
+                    cn.push_back((uint32_t)std::min<uint64_t>(kChunkTiles, nt - t));
+                }
+                snc.push_back((uint32_t)(cf.size() - scf.back()));
+                sst.push_back((uint32_t)out_base);
+                out_base += tot;
+            }
+            i = j;
+        }
+        if (out_base != n) return fail(c, GK_E_ARG, "piece lengths do not add up to n");
+        const uint64_t T = ts.size(), C = cf.size(), nseg = sst.size();
+        if (nseg == 0) return GK_OK;
+        int rc = tables(T, C, nseg);
+        if (rc != GK_OK) return rc;
+        uint32_t *t_start, *t_count, *s_cfirst, *s_nchunks, *s_st;
+        GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
+        GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));
+        GK_TRY_HIP(c, scratch(c, "s_cfirst", nseg, &s_cfirst));
+        GK_TRY_HIP(c, scratch(c, "s_nchunks", nseg, &s_nchunks));
+        GK_TRY_HIP(c, scratch(c, "s_pstart", nseg, &s_st));
+        GK_TRY_HIP(c, hipMemcpyAsync(t_start, ts.data(), 4 * T, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(t_count, tc.data(), 4 * T, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(c_first, cf.data(), 4 * C, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(c_ntiles, cn.data(), 4 * C, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(s_cfirst, scf.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(s_nchunks, snc.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(s_st, sst.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        big_elems = n;
+        rc = level_pass(1, kGR, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
+        if (rc != GK_OK) return rc;
+        cur_big = 0;
+        return classify(nseg * kGRadix, 2 * kGR, 0, cur_big);
+    }
+
+    // global levels while the next-level list is non-empty; `in` holds the current buffer
+    int levels(int level, int in) {
+        while (nbig > 0) {
+            const int out = in ^ 1;
+            const int hi = level * kGR;
+            uint32_t *ntl, *nch, *tfirst, *cfirst;
+            GK_TRY_HIP(c, scratch(c, "s_ntiles", nbig, &ntl));
+            GK_TRY_HIP(c, scratch(c, "s_nchunks", nbig, &nch));
+            GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
+            GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
+            hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big], nbig,
+                               (uint32_t)kPTile, ntl, nch);
+            GK_TRY_HIP(c, hipGetLastError());
+            uint64_t T = 0, C = 0;
+            GK_TRY_HIP(c, scan_u32_exclusive_pub(c, ntl, nbig, tfirst, &T));
+            GK_TRY_HIP(c, scan_u32_exclusive_pub(c, nch, nbig, cfirst, &C));
+            uint32_t *t_start, *t_count;
+            GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
+            GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));
+            int rc = tables(T, C, nbig);
+            if (rc != GK_OK) return rc;
+            hipLaunchKernelGGL(tile_table_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
+                               big_len[cur_big], tfirst, cfirst, nbig, (uint32_t)kPTile, t_start, t_count, c_first,
+                               c_ntiles);
+            rc = level_pass(level, hi, t_start, t_count, T, C, cfirst, nch, big_start[cur_big], nbig, c->keys[in],
+                            c->vals[in], out);
+            if (rc != GK_OK) return rc;
+            cur_big ^= 1;
+            rc = classify((uint64_t)nbig * kGRadix, hi + kGR, out, cur_big);
+            if (rc != GK_OK) return rc;
+            ++level;
+            in = out;
+        }
+        return GK_OK;
+    }
+
+    // local rounds (generation g lists -> re-listed sub-buckets in generation g ^ 1), done copies
+    int finish() {
+        const uint64_t max_spill = n / (kSmall + 1) + 1024;
+        GK_TRY_HIP(c, grow_keep(c, "blk0", std::max<uint64_t>(nblk, max_spill), nblk, &blk[0]));
+        GK_TRY_HIP(c, grow_keep(c, "wav0", std::max<uint64_t>(nwav, max_spill), nwav, &wav[0]));
+        GK_TRY_HIP(c, grow_keep(c, "blk1", max_spill, 0, &blk[1]));
+        GK_TRY_HIP(c, grow_keep(c, "wav1", max_spill, 0, &wav[1]));
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
+        int g = 0, round = 0;
+        while (nblk + nwav > 0) {
+            const int ng = g ^ 1;
+            // the re-list counters of this round start from 0 (the done count carries on)
+            GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBlock, 0, 8, c->stream));
+            const Lists nl = lists(ng, 0);
+            if (nblk) {
+                timer_begin(c, round == 0 ? "msd_local_block" : "msd_local_block_r", &slot);
+                if (round == 0) timer_units(c, slot, blk_elems);
+                hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
+                                   dim3((unsigned)std::min<uint64_t>(nblk, cus * 8)), dim3(kBT), 0, c->stream, blk[g],
+                                   (uint32_t)nblk, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1], heads, nl, ctr);
+                GK_TRY_HIP(c, hipGetLastError());
+                timer_end(c, slot);
+            }
+            if (nwav) {
+                timer_begin(c, round == 0 ? "msd_local_wave" : "msd_local_wave_r", &slot);
+                if (round == 0) timer_units(c, slot, wav_elems);
+                hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, kWR>),
+                                   dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(kWT), 0, c->stream, wav[g],
+                                   (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1], heads, nl, ctr);
+                GK_TRY_HIP(c, hipGetLastError());
+                timer_end(c, slot);
+            }
+            int rc = read_ctr();
+            if (rc != GK_OK) return rc;
+            nblk = h[kCtrBlock];
+            nwav = h[kCtrWave];
+            ndone = h[kCtrDone];
+            g = ng;
+            if (++round > 64) return fail(c, GK_E_HIP, "msd local rounds did not converge");
+        }
+        if (ndone > 0) {
+            hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len,
+                               dn_par, c->keys[1], c->vals[1], c->keys[0], c->vals[0], heads);
+            GK_TRY_HIP(c, hipGetLastError());
+        }
+        c->heads = heads;
+        c->heads_valid = true;
+        c->cur = 0;
+        return GK_OK;
+    }
+};
+
+// the enumerated k-mers of the whole sequence (gk_sort's fixed-length one-word path)
+int msd_sort(gk_ctx *c, const KeySpec &ks) {
+    MsdDriver d(c, ks);
+    timer_begin(c, "msd_total", &d.total_slot);
+    int rc = d.init(c->n);
+    if (rc != GK_OK) return rc;
+    uint64_t found = 0;
+    rc = d.run_l0(0, c->sba_len, c->keys[0], c->vals[0], c->elem_cap + 64, &found);
+    if (rc != GK_OK) return rc;
+    if (found != c->n) return fail(c, GK_E_HIP, "msd: k-mer count differs from the enumeration");
+    rc = d.classify(kGRadix, kGR, 0, 0);
+    if (rc != GK_OK) return rc;
+    rc = d.levels(1, 0);
+    if (rc != GK_OK) return rc;
+    rc = d.finish();
+    timer_end(c, d.total_slot);
+    return rc;
+}
+
+// multi-GPU send side: k-mers starting in [lo, hi) partitioned by their top kGR key bits
+int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,
+                        uint64_t cap, uint64_t *hist, uint64_t *count) {
+    MsdDriver d(c, ks);
+    GK_TRY_HIP(c, msd_tables());
+    int rc = d.run_l0(lo, hi, kout, vout, cap, count);
+    if (rc != GK_OK) return rc;
+    std::vector<uint32_t> hc(kGRadix);
+    GK_TRY_HIP(c, hipMemcpyAsync(hc.data(), d.seg_cnt, 4 * kGRadix, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));  // the caller's exchange reads kout / vout next
+    for (int i = 0; i < kGRadix; ++i) hist[i] = hc[i];
     return GK_OK;
 }
+
+// multi-GPU receive side: sort n received k-mers (buckets as pieces) into keys[0] / vals[0]
+int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint32_t *vin, const uint64_t *poff,
+                   const uint64_t *plen, const uint32_t *pbucket, uint32_t np) {
+    MsdDriver d(c, ks);
+    timer_begin(c, "msd_total", &d.total_slot);
+    int rc = d.init(c->n);
+    if (rc != GK_OK) return rc;
+    rc = d.first_level_from_pieces(kin, vin, poff, plen, pbucket, np);
+    if (rc != GK_OK) return rc;
+    rc = d.levels(2, 0);
+    if (rc != GK_OK) return rc;
+    rc = d.finish();
+    timer_end(c, d.total_slot);
+    return rc;
+}
+
+int msd_radix_bits() { return kGR; }
 
 }  // namespace gkm

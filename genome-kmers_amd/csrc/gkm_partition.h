@@ -89,7 +89,8 @@ struct PartSmem {
     static constexpr int kStage = kValOff + (kTile + 1) * 4;  // (slot kTile: sink for invalid items)
     static constexpr int kCounters = kWaves * kRadix * 4;     // per-wave digit counters (aliased)
     static constexpr int kUnion = kStage > kCounters ? kStage : kCounters;
-    static_assert(kRadix <= T, "one thread per digit");
+    static constexpr int kDPT = kRadix > T ? kRadix / T : 1;  // digits per thread in the scan
+    static_assert(kRadix <= T || kRadix % T == 0, "digits split evenly over threads");
 };
 
 // Stable partition of one tile (item i of lane l in wave w = tile element w*I*64 + i*64 + l) by
@@ -120,15 +121,24 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank);
     lds_barrier();
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
-    uint32_t total = 0, incl = 0;
-    if (tid < RADIX) {
+    // (thread t owns digits t*K .. t*K+K-1, K = kDPT)
+    constexpr int K = SM::kDPT;
+    constexpr int ACT = RADIX / K;  // threads taking part
+    uint32_t total[K], sum = 0, incl = 0;
+    if (tid < ACT) {
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t v = s_wc[w * RADIX + tid];
-            s_wc[w * RADIX + tid] = total;
-            total += v;
+        for (int k = 0; k < K; ++k) {
+            const int dgt = tid * K + k;
+            total[k] = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t v = s_wc[w * RADIX + dgt];
+                s_wc[w * RADIX + dgt] = total[k];
+                total[k] += v;
+            }
+            sum += total[k];
         }
-        incl = total;
+        incl = sum;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t y = __shfl_up(incl, off);
@@ -137,12 +147,18 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
         if (lane == 63) s_wsum[wave] = incl;
     }
     lds_barrier();
-    if (tid < RADIX) {
+    if (tid < ACT) {
         uint32_t pre = 0;
         for (int w = 0; w < wave; ++w) pre += s_wsum[w];
-        s_start[tid] = pre + incl - total;
-        if (s_toff) s_toff[tid] -= pre + incl - total;  // global offset of tile slot s = s_toff[digit] + s
-        if (tid == RADIX - 1) s_start[RADIX] = pre + incl;
+        uint32_t run = pre + incl - sum;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int dgt = tid * K + k;
+            s_start[dgt] = run;
+            if (s_toff) s_toff[dgt] -= run;  // global offset of tile slot s = s_toff[digit] + s
+            run += total[k];
+        }
+        if (tid == ACT - 1) s_start[RADIX] = run;
     }
     lds_barrier();
 #pragma unroll

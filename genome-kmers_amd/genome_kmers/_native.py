@@ -46,7 +46,8 @@ EXPORTED = (
     "gk_alphabet_is_acgt", "gk_enumerate", "gk_set_start_indices", "gk_sort", "gk_num_kmers",
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
     "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
-    "gk_profile_enable", "gk_profile_report", "gk_stream",
+    "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
+    "gk_shard_sort",
 )
 
 
@@ -110,6 +111,11 @@ _SIGS = {
     "gk_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "gk_profile_report": ([_P, ctypes.c_char_p, ctypes.c_uint64], ctypes.c_int),
     "gk_stream": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
+    "gk_shard_bucket_bits": ([], ctypes.c_int),
+    "gk_shard_partition": ([_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _P, _P, ctypes.c_uint64, _U64P,
+                            _U64P], ctypes.c_int),
+    "gk_shard_sort": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, _U64P, _U64P, _U32P, ctypes.c_uint32],
+                      ctypes.c_int),
 }
 
 
@@ -273,6 +279,31 @@ class Engine:
         self._check(self.lib.gk_copy_unique(self.ctx, _ptr(starts, ctypes.c_uint64), _ptr(counts, ctypes.c_uint32),
                                             g.value))
         return starts, counts
+
+    # ---- multi-GPU shards (genome_kmers.distributed) ------------------------------------------
+    def shard_bucket_bits(self) -> int:
+        return int(self.lib.gk_shard_bucket_bits())
+
+    def shard_partition(self, lo: int, hi: int, k: int, keys, starts):
+        """Encode + partition the k-mers starting in [lo, hi) into the device tensors ``keys``
+        (int64) / ``starts`` (int32); returns (bucket sizes as a numpy uint64 array, count)."""
+        hist = np.zeros(1 << self.shard_bucket_bits(), dtype=np.uint64)
+        n = ctypes.c_uint64(0)
+        cap = min(keys.numel(), starts.numel())
+        self._check(self.lib.gk_shard_partition(self.ctx, lo, hi, k, keys.data_ptr(), starts.data_ptr(), cap,
+                                                _ptr(hist, ctypes.c_uint64), ctypes.byref(n)))
+        return hist, n.value
+
+    def shard_sort(self, keys, starts, n: int, k: int, piece_off: np.ndarray, piece_len: np.ndarray,
+                   piece_bucket: np.ndarray):
+        """Sort n received (key, start) pairs held in device tensors, given as bucket pieces."""
+        off = np.ascontiguousarray(piece_off, dtype=np.uint64)
+        ln = np.ascontiguousarray(piece_len, dtype=np.uint64)
+        bk = np.ascontiguousarray(piece_bucket, dtype=np.uint32)
+        self._check(self.lib.gk_shard_sort(self.ctx, keys.data_ptr() if n else None, starts.data_ptr() if n else None,
+                                           n, k, _ptr(off, ctypes.c_uint64), _ptr(ln, ctypes.c_uint64),
+                                           _ptr(bk, ctypes.c_uint32), len(bk)))
+        self.n = n
 
     def unique_count_only(self) -> int:
         g = ctypes.c_uint64(0)

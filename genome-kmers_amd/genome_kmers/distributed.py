@@ -1,0 +1,176 @@
+"""Multi-GPU k-mer sort: one process per GPU under torch.distributed.
+
+The reference sorts in one process (``Kmers.sort``, kmers.py:1624-1652); this module is one rank's
+share of the same result on N GPUs.  Every rank holds the whole sequence byte array in HBM and
+owns the k-mers that START in its position range [lo_r, lo_r+1): ranges are cut at multiples of
+32 bases, and a k-mer near hi reads up to k-1 bases past it (the halo), so no k-mer is lost or
+duplicated.  One run:
+
+1. ``shard_partition``: the rank encodes its k-mers and partitions them stably by the top
+   ``bits`` (8) key bits -- the MSD sort's first level -- into a torch-owned send buffer;
+2. ``all_gather`` of the 256-bucket histograms: every rank derives the same split of the buckets
+   into N contiguous ranges of about n/N k-mers each (``split_buckets``);
+3. the exchange: every rank sends each other rank the buckets it owns, keys and starts, as one
+   group of point-to-point messages (ncclSend / ncclRecv over xGMI under RCCL);
+4. ``shard_sort``: the received buckets are sorted by the MSD levels below the top bits.  A bucket
+   arrives as one piece per source rank; pieces are listed in source-rank order, and ranks own
+   ascending positions, so equal keys stay in ascending start order;
+5. unique counts are local: the bucket ranges end on bucket boundaries, so equal keys never
+   straddle two ranks.
+
+The concatenation of the ranks' sorted starts, in rank order, is ``Kmers.sort``'s order with
+``break_ties=True`` (kmers.py:1710-1711) -- the single-GPU order.
+"""
+
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+
+def count_kmers(sba_len: int, seg_starts: np.ndarray, k: int) -> int:
+    """n = sum over contigs of max(0, len - k + 1) (kmers.py:837-861); contig s covers
+    [starts[s], starts[s+1] - 2], the last one ends at sba_len - 1."""
+    starts = np.asarray(seg_starts, dtype=np.int64)
+    ends = np.append(starts[1:] - 2, sba_len - 1)
+    return int(np.maximum(ends - starts + 1 - k + 1, 0).sum())
+
+
+def position_ranges(sba_len: int, world: int) -> list[int]:
+    """world + 1 boundaries of equal start-position ranges, cut at multiples of 32."""
+    return [(sba_len * r // world) // 32 * 32 for r in range(world)] + [sba_len]
+
+
+def split_buckets(totals: np.ndarray, world: int) -> list[int]:
+    """world + 1 bucket boundaries: rank r receives buckets [b_r, b_r+1), each range holding about
+    sum(totals) / world k-mers (b_r = first bucket whose exclusive prefix reaches r/world)."""
+    totals = np.asarray(totals, dtype=np.int64)
+    excl = np.concatenate(([0], np.cumsum(totals)[:-1]))
+    n = int(totals.sum())
+    nb = len(totals)
+    bounds = [0]
+    for r in range(1, world):
+        target = n * r // world
+        b = int(np.searchsorted(excl, target, side="left"))
+        bounds.append(min(max(b, bounds[-1]), nb))
+    bounds.append(nb)
+    return bounds
+
+
+def receive_pieces(H: np.ndarray, b0: int, b1: int, recv_counts: list[int]):
+    """Pieces (offset, length, bucket) of the receive buffer for buckets [b0, b1): source s's
+    chunk starts at the exclusive prefix of recv_counts and holds its buckets in order."""
+    world = H.shape[0]
+    recv_off = np.concatenate(([0], np.cumsum(recv_counts)[:-1])).astype(np.int64)
+    off, ln, bk = [], [], []
+    within = np.zeros(world, dtype=np.int64)
+    for b in range(b0, b1):
+        for s in range(world):
+            m = int(H[s, b])
+            if m:
+                off.append(int(recv_off[s] + within[s]))
+                ln.append(m)
+                bk.append(b)
+            within[s] += m
+    return (np.asarray(off, dtype=np.uint64), np.asarray(ln, dtype=np.uint64), np.asarray(bk, dtype=np.uint32))
+
+
+class ShardedKmerSort:
+    """One rank of the N-GPU sort of the fixed-length k-mers of a sequence (min = max = k).
+
+    ``engine`` defaults to a ``genome_kmers._native.Engine`` on ``device`` (HIP, no fallback);
+    ``torch_device`` is where the exchange buffers live (the GPU by default).
+    """
+
+    def __init__(self, sba: np.ndarray, seg_starts: np.ndarray, k: int, rank: int, world: int, device: int = 0,
+                 engine=None, torch_device=None, group=None, chunk: int = None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank, self.world, self.k = rank, world, k
+        self.dev = torch_device if torch_device is not None else torch.device("cuda", device)
+        if engine is None:
+            from genome_kmers import _native
+
+            engine = _native.Engine(device)
+        self.engine = engine
+        t0 = time.perf_counter()
+        self.engine.set_sequence(sba, seg_starts)
+        self.engine.sync()
+        self.h2d_ms = (time.perf_counter() - t0) * 1e3
+        bounds = position_ranges(len(sba), world)
+        self.lo, self.hi = bounds[rank], bounds[rank + 1]
+        self.total_kmers = count_kmers(len(sba), seg_starts, k)
+        self.nb = 1 << self.engine.shard_bucket_bits()
+        cap = self.hi - self.lo + 64
+        self.send_k = torch.empty(cap, dtype=torch.int64, device=self.dev)
+        self.send_v = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.recv_k = torch.empty(0, dtype=torch.int64, device=self.dev)
+        self.recv_v = torch.empty(0, dtype=torch.int32, device=self.dev)
+        self.local_kmers = 0
+        self.bucket_bounds = None
+        if chunk:
+            self.CHUNK_BYTES = chunk
+
+    def _ensure_recv(self, n: int):
+        if self.recv_k.numel() < n + 64:
+            size = n + n // 8 + 64
+            self.recv_k = self.torch.empty(size, dtype=self.torch.int64, device=self.dev)
+            self.recv_v = self.torch.empty(size, dtype=self.torch.int32, device=self.dev)
+
+    # bytes per point-to-point message: RCCL mis-copies messages of 2^31 bytes and more (measured
+    # with world-1 all_to_all_single: half the elements wrong at >= 2 GiB, tools/a2a_probe.py)
+    CHUNK_BYTES = 1 << 30
+
+    def _exchange(self, send, recv, send_counts, recv_counts):
+        """The all-to-all of the per-destination segments of ``send`` into the per-source segments
+        of ``recv``: one group of point-to-point sends / receives (ncclSend / ncclRecv over xGMI
+        under RCCL), each message at most CHUNK_BYTES; the rank's own segment is a local copy."""
+        dist = self.dist
+        so = np.concatenate(([0], np.cumsum(send_counts)[:-1])).astype(np.int64)
+        ro = np.concatenate(([0], np.cumsum(recv_counts)[:-1])).astype(np.int64)
+        step = max(1, self.CHUNK_BYTES // send.element_size())
+        me = self.rank
+        ops = []
+        for r in range(self.world):
+            if r == me:
+                continue
+            for a in range(0, int(send_counts[r]), step):
+                m = min(step, int(send_counts[r]) - a)
+                ops.append(dist.P2POp(dist.isend, send[so[r] + a:so[r] + a + m], r, group=self.group))
+            for a in range(0, int(recv_counts[r]), step):
+                m = min(step, int(recv_counts[r]) - a)
+                ops.append(dist.P2POp(dist.irecv, recv[ro[r] + a:ro[r] + a + m], r, group=self.group))
+        m = int(send_counts[me])
+        if m:
+            recv[ro[me]:ro[me] + m].copy_(send[so[me]:so[me] + m])
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+    def run(self) -> int:
+        """One sort; returns this rank's number of distinct k-mers."""
+        torch, dist = self.torch, self.dist
+        hist, n = self.engine.shard_partition(self.lo, self.hi, self.k, self.send_k, self.send_v)
+        h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to(self.dev)
+        gathered = [torch.empty_like(h) for _ in range(self.world)]
+        dist.all_gather(gathered, h, group=self.group)
+        H = torch.stack(gathered).cpu().numpy()
+        bounds = split_buckets(H.sum(axis=0), self.world)
+        self.bucket_bounds = bounds
+        b0, b1 = bounds[self.rank], bounds[self.rank + 1]
+        mine = np.asarray(hist, dtype=np.int64)
+        send_counts = [int(mine[bounds[r]:bounds[r + 1]].sum()) for r in range(self.world)]
+        recv_counts = [int(H[s, b0:b1].sum()) for s in range(self.world)]
+        R = sum(recv_counts)
+        self._ensure_recv(R)
+        self._exchange(self.send_k, self.recv_k, send_counts, recv_counts)
+        self._exchange(self.send_v, self.recv_v, send_counts, recv_counts)
+        off, ln, bk = receive_pieces(H, b0, b1, recv_counts)
+        if self.recv_k.is_cuda:  # the engine works on its own stream: the exchange must be done
+            torch.cuda.current_stream(self.dev).synchronize()
+        self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk)
+        self.local_kmers = R
+        return self.engine.unique_count_only()

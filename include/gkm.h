@@ -18,6 +18,8 @@
  *                          (kmers.py:869-992)
  *   gk_unique_counts       the (unique k-mer, multiplicity) view of the sorted groups (kmers.py:597-625)
  *   gk_copy_keys           encoded k-mers (no reference counterpart: the reference compares bytes)
+ *   gk_shard_partition,    one GPU's share of Kmers.sort under torch.distributed (no reference
+ *   gk_shard_sort          counterpart: the reference is single-process, kmers.py:1644-1648)
  *
  * Conventions: every function returns GK_OK (0) or a negative gk_status; gk_last_error(ctx)
  * describes the last failure.  Host pointers are borrowed for the duration of the call only.
@@ -146,6 +148,30 @@ int gk_profile_enable(gk_ctx *ctx, int on);
 int gk_profile_report(gk_ctx *ctx, char *buf, uint64_t buflen);
 /* stream handle of the context (hipStream_t), for interop */
 int gk_stream(gk_ctx *ctx, void **stream);
+
+/* ---- multi-GPU shards (one process per GPU; the exchange is the caller's all-to-all) --------- */
+/* number of top key bits the shard buckets are cut on (buckets = 1 << bits) */
+int gk_shard_bucket_bits(void);
+/*
+ * Send side: encode the fixed-length k-mers (length k, no '$') that start in sequence positions
+ * [lo, hi) (lo a multiple of 32) and partition them stably by their top gk_shard_bucket_bits()
+ * key bits into the caller's DEVICE buffers d_keys / d_starts (capacity cap >= count + 1), in
+ * ascending bucket order.  h_hist[1 << bits] receives the bucket sizes, *n_out the count.
+ * Returns after the device work is complete (the buffers can go straight to another stream).
+ */
+int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint64_t *d_keys, uint32_t *d_starts,
+                       uint64_t cap, uint64_t *h_hist, uint64_t *n_out);
+/*
+ * Receive side: sort n received (key, start) pairs in DEVICE buffers, given as npieces pieces
+ * (offset, length, bucket) listed in ascending bucket order; the pieces of one bucket are listed
+ * in ascending start order (source rank order).  The context then holds the sorted k-mers as if
+ * gk_sort(k) had run on them: starts, keys, unique counts and group passes work as usual.
+ * The buffers must be complete when the call is made (work queued on another stream must have
+ * been synchronised by the caller).
+ */
+int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
+                  const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
+                  uint32_t npieces);
 
 #ifdef __cplusplus
 }

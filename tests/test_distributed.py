@@ -1,0 +1,232 @@
+"""Multi-GPU path (genome_kmers.distributed): host logic, a world_size-2 gloo run on CPU, and the
+device shard entry points with the exchange done in one process on one GPU.
+
+The CPU run drives the real orchestration (histogram all_gather, bucket split, the exchange with
+uneven splits in chunked point-to-point messages, receive pieces) with ``NumpyShardEngine``, a
+test double that restates the engine's shard contract with numpy; the result is checked against
+the oracle's break_ties=True order (oracle/, kmers.py:1654-1731).  The GPU test runs libgkm's gk_shard_partition /
+gk_shard_sort for two ranks and checks the concatenation against gk_sort on the whole input.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from genome_kmers import distributed as D
+
+K = 11
+
+
+def _random_sba(L, seed, contigs=1):
+    rng = np.random.default_rng(seed)
+    parts = [np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L // contigs)] for _ in range(contigs)]
+    sba = parts[0]
+    starts = [0]
+    for p in parts[1:]:
+        starts.append(len(sba) + 1)
+        sba = np.concatenate([sba, np.frombuffer(b"$", dtype=np.uint8), p])
+    return np.ascontiguousarray(sba), np.asarray(starts, dtype=np.uint32)
+
+
+def _keys(sba, starts, k):
+    code = np.zeros(256, dtype=np.uint64)
+    for i, ch in enumerate(b"ACGT"):
+        code[ch] = i
+    key = np.zeros(len(starts), dtype=np.uint64)
+    for j in range(k):
+        key = (key << np.uint64(2)) | code[sba[starts + j]]
+    return key
+
+
+def _valid_starts(sba, seg, k, lo, hi):
+    s = np.arange(lo, min(hi, len(sba)), dtype=np.int64)
+    ok = np.ones(len(s), dtype=bool)
+    for j in range(k):
+        p = s + j
+        inside = p < len(sba)
+        ok &= inside
+        ok[inside] &= sba[p[inside]] != 36
+    return s[ok]
+
+
+class NumpyShardEngine:
+    """Test double of the engine's shard contract (include/gkm.h gk_shard_*), numpy on the host."""
+
+    bits = 8
+
+    def set_sequence(self, sba, seg):
+        self.sba, self.seg = np.asarray(sba), np.asarray(seg)
+
+    def sync(self):
+        pass
+
+    def shard_bucket_bits(self):
+        return self.bits
+
+    def shard_partition(self, lo, hi, k, keys_t, starts_t):
+        s = _valid_starts(self.sba, self.seg, k, lo, hi)
+        key = _keys(self.sba, s, k)
+        top = (key >> np.uint64(2 * k - self.bits)).astype(np.int64)
+        order = np.argsort(top, kind="stable")
+        n = len(s)
+        keys_t[:n] = __import__("torch").from_numpy(key[order].view(np.int64))
+        starts_t[:n] = __import__("torch").from_numpy(s[order].astype(np.int32))
+        return np.bincount(top, minlength=1 << self.bits).astype(np.uint64), n
+
+    def shard_sort(self, keys_t, starts_t, n, k, off, ln, bk):
+        assert np.all(np.diff(bk.astype(np.int64)) >= 0), "pieces must come in bucket order"
+        key = keys_t[:n].numpy().view(np.uint64)
+        st = starts_t[:n].numpy().astype(np.int64)
+        idx = np.concatenate([np.arange(o, o + m) for o, m in zip(off.astype(np.int64), ln.astype(np.int64))]) \
+            if len(off) else np.zeros(0, dtype=np.int64)
+        key, st = key[idx], st[idx]
+        order = np.argsort(key, kind="stable")  # the device sort is stable in piece order
+        self.keys, self.starts = key[order], st[order]
+
+    def unique_count_only(self):
+        return int(len(np.unique(self.keys)))
+
+
+# ---- host logic --------------------------------------------------------------------------------
+def test_count_kmers_matches_enumeration():
+    sba, seg = _random_sba(3000, 1, contigs=3)
+    assert D.count_kmers(len(sba), seg, K) == len(_valid_starts(sba, seg, K, 0, len(sba)))
+
+
+def test_position_ranges_cover_and_align():
+    for L, w in [(10_000, 2), (10_001, 3), (5, 4), (3_100_000_000, 8)]:
+        b = D.position_ranges(L, w)
+        assert b[0] == 0 and b[-1] == L and len(b) == w + 1
+        assert all(x % 32 == 0 for x in b[:-1])
+        assert all(b[i] <= b[i + 1] for i in range(w))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_split_buckets_balanced_and_contiguous(world):
+    rng = np.random.default_rng(world)
+    totals = rng.integers(0, 1000, 256)
+    b = D.split_buckets(totals, world)
+    assert b[0] == 0 and b[-1] == 256 and all(b[i] <= b[i + 1] for i in range(world))
+    share = [totals[b[r]:b[r + 1]].sum() for r in range(world)]
+    assert sum(share) == totals.sum()
+    assert max(share) <= totals.sum() / world + totals.max() + 1
+
+
+def test_split_buckets_skewed():
+    totals = np.zeros(256, dtype=np.int64)
+    totals[7] = 10_000
+    b = D.split_buckets(totals, 4)
+    assert b[0] == 0 and b[-1] == 256 and sum(totals[b[r]:b[r + 1]].sum() for r in range(4)) == 10_000
+
+
+def test_receive_pieces_layout():
+    H = np.array([[1, 2, 0, 3], [4, 0, 5, 6]])
+    # rank owning buckets [1, 4): source 0 sends 2+0+3, source 1 sends 0+5+6
+    off, ln, bk = D.receive_pieces(H, 1, 4, [5, 11])
+    assert list(bk) == [1, 2, 3, 3]
+    assert list(ln) == [2, 5, 3, 6]
+    assert list(off) == [0, 5, 2, 10]
+
+
+# ---- world_size 2 over gloo on CPU -------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, sba, seg, k, q, chunk):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        job = D.ShardedKmerSort(sba, seg, k, rank, world, engine=NumpyShardEngine(), torch_device=torch.device("cpu"),
+                                chunk=chunk)
+        n_unique = job.run()
+        q.put((rank, job.engine.starts.tolist(), n_unique, job.total_kmers, job.local_kmers))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("contigs,chunk", [(1, None), (3, None), (1, 5000)])
+def test_gloo_world2_matches_oracle(contigs, chunk):
+    import torch.multiprocessing as mp
+
+    from oracle import oracle
+
+    sba, seg = _random_sba(6000, 7 + contigs, contigs)
+    # planted repeats: equal k-mers on both ranks (tie order across ranks)
+    sba[4100:4200] = sba[100:200]  # (inside a contig: the '$' separators stay)
+    sba[5000:5030] = sba[100:130]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sba, seg, K, q, chunk)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = np.concatenate([np.asarray(r[1], dtype=np.uint32) for r in res])
+    starts = oracle.enumerate_starts(sba, seg, K)
+    want = oracle.quicksort(sba, starts, K, K, break_ties=True)
+    assert res[0][3] == len(starts)
+    assert sum(r[4] for r in res) == len(starts)
+    np.testing.assert_array_equal(got, want)
+    assert sum(r[2] for r in res) == len(np.unique(_keys(sba, starts.astype(np.int64), K)))
+
+
+# ---- device shard entry points, two ranks in one process ---------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs", [(2, 1), (3, 4)])
+def test_gpu_shards_concatenate_to_single_sort(world, contigs):
+    import torch
+
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(200_000 + 17, 3 + world, contigs)
+    sba[150_100:151_000] = sba[1000:1900]  # repeats across ranks (inside a contig)
+    k = 31
+    engines = [_native.Engine(0) for _ in range(world)]
+    bounds = D.position_ranges(len(sba), world)
+    dev = torch.device("cuda", 0)
+    sends, hists = [], []
+    for r, e in enumerate(engines):
+        e.set_sequence(sba, seg)
+        cap = bounds[r + 1] - bounds[r] + 64
+        sk = torch.empty(cap, dtype=torch.int64, device=dev)
+        sv = torch.empty(cap, dtype=torch.int32, device=dev)
+        hist, n = e.shard_partition(bounds[r], bounds[r + 1], k, sk, sv)
+        sends.append((sk, sv, n))
+        hists.append(np.asarray(hist, dtype=np.int64))
+    H = np.stack(hists)
+    bb = D.split_buckets(H.sum(axis=0), world)
+    got, uniq = [], 0
+    for r, e in enumerate(engines):
+        parts_k, parts_v, recv_counts = [], [], []
+        for s in range(world):
+            lo = int(H[s, :bb[r]].sum())
+            m = int(H[s, bb[r]:bb[r + 1]].sum())
+            parts_k.append(sends[s][0][lo:lo + m])
+            parts_v.append(sends[s][1][lo:lo + m])
+            recv_counts.append(m)
+        R = sum(recv_counts)
+        rk = torch.cat(parts_k + [torch.empty(64, dtype=torch.int64, device=dev)])
+        rv = torch.cat(parts_v + [torch.empty(64, dtype=torch.int32, device=dev)])
+        off, ln, bk = D.receive_pieces(H, bb[r], bb[r + 1], recv_counts)
+        torch.cuda.current_stream(dev).synchronize()
+        e.shard_sort(rk, rv, R, k, off, ln, bk)
+        got.append(e.copy_starts())
+        uniq += e.unique_count_only()
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(k)
+    ref.sort(k)
+    np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
+    assert uniq == ref.unique_count_only()

@@ -29,12 +29,16 @@ def main():
     f, w = per_kernel(fetch), per_kernel(write)
     res = {"_label": label, "_convention": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024, averaged per launch"}
     for k in sorted(set(f) | set(w)):
-        fk = sum(f.get(k, [0])) / max(len(f.get(k, [])), 1)
-        wk = sum(w.get(k, [0])) / max(len(w.get(k, [])), 1)
+        fl, wl = f.get(k, [0]), w.get(k, [0])
+        fk = sum(fl) / max(len(fl), 1)
+        wk = sum(wl) / max(len(wl), 1)
+        # the largest launch (launches pair up in order: same command, same dispatch sequence)
+        per = [a * 1024 * 2 + b * 1024 for a, b in zip(fl, wl)]
         short = k.split("::")[-1].split("<")[0]
-        res[short] = {"kernel": k, "launches": max(len(f.get(k, [])), len(w.get(k, []))),
+        res[short] = {"kernel": k, "launches": max(len(fl), len(wl)),
                       "fetch_bytes_per_launch": fk * 1024 * 2, "write_bytes_per_launch": wk * 1024,
-                      "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024}
+                      "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024,
+                      "hbm_bytes_max_launch": max(per) if per else None}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for k, v in res.items():

@@ -182,13 +182,19 @@ def main():
         if b and v["total_ms"] > 0:
             kernels[name] = {"ms_per_launch": round(v["total_ms"] / v["count"], 4),
                              "gbs": round(b / (v["total_ms"] * 1e-3) / 1e9, 1)}
-    # dominant kernel: the largest partition pass (msd_scatter_kernel, level >= 1) or, when a
-    # genome needs none, the L0 pass
+    # dominant kernel: msd_scatter_kernel, the partition pass of every level >= 1 (averaged over
+    # its launches, as rocprofv3 --stats averages it); the L0 pass when a genome needs none
     cands = [n for n in report if n.startswith("msd_pass_l") and n != "msd_pass_l0" and report[n]["units"]]
-    dom = max(cands, key=lambda n: report[n]["total_ms"]) if cands else "msd_pass_l0"
-    rp = report.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
+    if cands:
+        dom = "msd_pass_l1.."
+        rp = {k: sum(report[n][k] for n in cands) for k in ("count", "total_ms", "units")}
+        dom_bytes = 24 * rp["units"]
+    else:
+        dom = "msd_pass_l0"
+        rp = report.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
+        dom_bytes = stage_bytes(dom, rp)
     avg_ms = rp["total_ms"] / max(rp["count"], 1)
-    bytes_per_launch = stage_bytes(dom, rp) / max(rp["count"], 1)
+    bytes_per_launch = dom_bytes / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
     kname = "msd_scatter_kernel" if dom != "msd_pass_l0" else "msd0_scatter_kernel"

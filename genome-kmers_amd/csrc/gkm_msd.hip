@@ -26,7 +26,7 @@ namespace gkm {
 
 constexpr int kGR = 8;                  // global digit bits
 constexpr int kGRadix = 1 << kGR;
-constexpr int kPT = 1024, kPI = 12;     // global partition tile: 1024 threads x 12 keys
+constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
 constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk
 constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
@@ -201,6 +201,121 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
         const uint32_t cnt = s_start[RADIX];
         if (t + walk.step < walk.end) load(t + walk.step);
         partition_store<T, I, R, 0>(d0, s_raw, s_toff, cnt, sink, kout, vout);
+    }
+}
+
+// software-pipelined L0 (see msd_pipe_kernel): the previous tile's stores overlap this tile's
+// packing, key extraction and ranking; the next tile's bytes are loaded after the staging
+template <int BITS, int T, int I, int R>
+__global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
+                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                      uint32_t ntiles, uint64_t sink) {
+    constexpr int TILE = T * I;
+    constexpr int RADIX = 1 << R;
+    constexpr int NW = T / 64;
+    constexpr int PRE = (I + 2) / 3;
+    using P = L0Pack<BITS, TILE>;
+    using SM = PipeSmem<T, I>;
+    static_assert(T >= RADIX, "one thread per digit");
+    __shared__ __attribute__((aligned(16))) unsigned char s_stage[SM::kStage];
+    __shared__ uint32_t s_wc[NW * RADIX];
+    __shared__ uint64_t s_code[P::kCodeWords];
+    __shared__ uint32_t s_dol[P::kGroups];
+    __shared__ uint32_t s_toff[2][RADIX];
+    __shared__ uint32_t s_start[RADIX + 1];
+    __shared__ uint32_t s_wsum[RADIX / 64];
+    __shared__ uint8_t s_lut4[256];
+    uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_stage);
+    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_stage + SM::kValOff);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    const TileWalk walk(ntiles);
+    uint4 ra, rb;
+    uint32_t toff = 0;
+    auto load = [&](uint32_t t) {
+        toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];
+        l0_load<BITS, TILE>(a.sba + a.lo + (uint64_t)t * TILE, ra, rb);
+    };
+    uint32_t pcnt = 0;
+    int cur = 0;
+    if (walk.first < walk.end) load(walk.first);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        uint32_t *wc = s_wc + wave * RADIX;
+#pragma unroll
+        for (int u = 0; u < (RADIX + 63) / 64; ++u)
+            if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
+        if (tid < RADIX) s_toff[cur][tid] = toff;
+        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+        const uint32_t *ptoff = s_toff[cur ^ 1];
+#pragma unroll
+        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        lds_barrier();  // packed codes visible
+        const uint64_t P0 = a.lo + (uint64_t)t * TILE;
+        uint64_t key[I];
+        uint32_t val[I], dig[I], rank[I];
+        bool valid[I];
+        uint32_t p0 = wave * (I * 64) + lane;
+        asm volatile("" : "+v"(p0));
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = p0 + i * 64;
+            valid[i] = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi;
+            key[i] = l0_key<BITS>(s_code, p, a.total_bits);
+            val[i] = (uint32_t)(P0 + p);
+        }
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            dig[i] = dg_of(key[i], d0);
+            const uint64_t peers = match_peers<R>(dig[i], valid[i]);
+            const uint32_t rank_in = lanes_below(peers);
+            const uint32_t old = wc[dig[i]];
+            if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
+            rank[i] = old + rank_in;
+            if (PRE + i < I) pipe_store<T, I, R, 0>(PRE + i, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        }
+        lds_barrier();  // ranks final; the previous tile's staging has been read out
+        uint32_t total = 0, incl = 0;
+        if (tid < RADIX) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t v = s_wc[w * RADIX + tid];
+                s_wc[w * RADIX + tid] = total;
+                total += v;
+            }
+            incl = total;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            if (lane == 63) s_wsum[wave] = incl;
+        }
+        lds_barrier();
+        if (tid < RADIX) {
+            uint32_t pre = 0;
+            for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+            const uint32_t st = pre + incl - total;
+            s_start[tid] = st;
+            s_toff[cur][tid] -= st;
+            if (tid == RADIX - 1) s_start[RADIX] = pre + incl;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t sl = valid[i] ? s_start[dig[i]] + wc[dig[i]] + rank[i] : (uint32_t)TILE;
+            s_keys[sl] = key[i];
+            s_vals[sl] = val[i];
+        }
+        pcnt = s_start[RADIX];
+        lds_barrier();  // staging complete; counters and codes read
+        if (t + walk.step < walk.end) load(t + walk.step);
+        cur ^= 1;
+    }
+    if (walk.first < walk.end) {
+        const uint32_t *ptoff = s_toff[cur ^ 1];
+#pragma unroll
+        for (int g = 0; g < I; ++g) pipe_store<T, I, R, 0>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
     }
 }
 
@@ -765,10 +880,10 @@ struct MsdDriver {
         timer_begin(c, "msd_pass_l0", &slot);
         timer_units(c, slot, *count);
         if (ks.bits == 2)
-            hipLaunchKernelGGL((msd0_scatter_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
                                tile_hist, kout, vout, (uint32_t)nt0, *count);
         else
-            hipLaunchKernelGGL((msd0_scatter_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
+            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
                                tile_hist, kout, vout, (uint32_t)nt0, *count);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
@@ -817,7 +932,7 @@ struct MsdDriver {
         if (rc != GK_OK) return rc;
         timer_begin(c, kPassNames[level & 7], &slot);
         timer_units(c, slot, big_elems);
-        hipLaunchKernelGGL((msd_scatter_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
+        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
                            dl, tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);

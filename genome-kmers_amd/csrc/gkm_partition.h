@@ -101,11 +101,13 @@ struct PartSmem {
 // Barriers inside: all T threads must call.
 // s_start[RADIX + 1] receives the tile-local digit starts (s_start[RADIX] = item count) and
 // slot[] each item's staging slot (invalid items: the sink slot kTile); s_toff may be null.
-template <int T, int I, int R>
+// PROF (timing builds of tools/radix_bench only): thread 0 adds the clock ticks of each phase to
+// prof[0..3] (rank, scan, slots, staging).
+template <int T, int I, int R, bool PROF = false>
 __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const uint32_t (&val)[I],
                                                 const bool (&valid)[I], Dig d, unsigned char *s_raw,
                                                 uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_start,
-                                                uint32_t (&slot)[I]) {
+                                                uint32_t (&slot)[I], unsigned long long *prof = nullptr) {
     using SM = PartSmem<T, I, R>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -115,11 +117,20 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_raw);
     uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
 
+    uint64_t t0 = PROF ? clock64() : 0;
+    auto mark = [&](int ph) {
+        if (PROF && tid == 0) {
+            const uint64_t t1 = clock64();
+            atomicAdd(&prof[ph], (unsigned long long)(t1 - t0));
+            t0 = t1;
+        }
+    };
     uint32_t dig[I], rank[I];
 #pragma unroll
     for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
     rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank);
     lds_barrier();
+    mark(0);
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
     // (thread t owns digits t*K .. t*K+K-1, K = kDPT)
     constexpr int K = SM::kDPT;
@@ -161,16 +172,19 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
         if (tid == ACT - 1) s_start[RADIX] = run;
     }
     lds_barrier();
+    mark(1);
 #pragma unroll
     for (int i = 0; i < I; ++i)
         slot[i] = valid[i] ? s_start[dig[i]] + s_wc[wave * RADIX + dig[i]] + rank[i] : (uint32_t)TILE;
     lds_barrier();  // counters consumed: the staging area is reused
+    mark(2);
 #pragma unroll
     for (int i = 0; i < I; ++i) {  // branch-free: invalid items go to the sink slot
         s_keys[slot[i]] = key[i];
         s_vals[slot[i]] = val[i];
     }
     lds_barrier();
+    mark(3);
 }
 
 // Branch-free and fully unrolled, so the compiler's count of stores in flight is static (it can
@@ -182,16 +196,29 @@ __device__ __forceinline__ void partition_store(Dig d, const unsigned char *s_ra
                                                 uint32_t *__restrict__ vout, uint64_t seq_base = 0) {
     const uint64_t *s_keys = reinterpret_cast<const uint64_t *>(s_raw);
     const uint32_t *s_vals = reinterpret_cast<const uint32_t *>(s_raw + PartSmem<T, I, R>::kValOff);
+    // in groups of G slots: all key / start reads, then all digit-offset reads, then the stores,
+    // so each group pays the LDS latency twice instead of every slot
+    constexpr int G = (I % 6 == 0) ? 6 : ((I % 4 == 0) ? 4 : 1);
 #pragma unroll
-    for (int j = 0; j < I; ++j) {
-        const uint32_t s = min(threadIdx.x + j * T, cnt - 1);  // cnt == 0: s stays in the tile
-        const uint64_t k = s_keys[s];
-        const uint32_t v = s_vals[s];
-        uint64_t o = cnt ? (uint64_t)(s_toff[dg_of(k, d)] + s) : sink;
-        if (MODE == 3) o = seq_base + s;  // timing only: perfectly sequential runs
-        if (MODE != 1 || o == 0xFFFFFFFFu) {
-            kout[o] = k;
-            vout[o] = v;
+    for (int j0 = 0; j0 < I; j0 += G) {
+        uint32_t s[G], v[G], o[G];
+        uint64_t k[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            s[g] = min(threadIdx.x + (j0 + g) * T, cnt - 1);  // cnt == 0: s stays in the tile
+            k[g] = s_keys[s[g]];
+            v[g] = s_vals[s[g]];
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) o[g] = s_toff[dg_of(k[g], d)] + s[g];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            uint64_t oo = cnt ? (uint64_t)o[g] : sink;
+            if (MODE == 3) oo = seq_base + s[g];  // timing only: perfectly sequential runs
+            if (MODE != 1 || oo == 0xFFFFFFFFu) {
+                kout[oo] = k[g];
+                vout[oo] = v[g];
+            }
         }
     }
 }
@@ -230,14 +257,15 @@ __global__ __launch_bounds__(256) void msd_count_kernel(const uint32_t *__restri
 
 // persistent: grid = a multiple of 8 blocks, each walks its XCD's tiles; the next tile's keys
 // and starts are loaded while the current tile's runs are stored
-template <int T, int I, int R, int MODE = 0>
+template <int T, int I, int R, int MODE = 0, bool PROF = false>
 __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restrict__ t_start,
                                                         const uint32_t *__restrict__ t_count, Dig dl,
                                                         const uint32_t *__restrict__ tile_off,
                                                         const uint64_t *__restrict__ kin,
                                                         const uint32_t *__restrict__ vin, uint64_t *__restrict__ kout,
                                                         uint32_t *__restrict__ vout, uint32_t ntiles,
-                                                        uint64_t sink) {
+                                                        uint64_t sink, unsigned long long *prof = nullptr,
+                                                        int stagger = 0) {
     using SM = PartSmem<T, I, R>;
     constexpr int RADIX = SM::kRadix;
     __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
@@ -262,24 +290,182 @@ __global__ __launch_bounds__(T) void msd_scatter_kernel(const uint32_t *__restri
             val[i] = vin[e];
         }
     };
+    // stagger (experiments): the second half of the grid starts later, so workgroups sharing a CU
+    // run their compute and memory phases out of step
+    if (stagger && blockIdx.x >= gridDim.x / 2)
+        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
     if (walk.first < walk.end) load(walk.first);
     // drain the prologue loads so the loop-entry wait state equals the back-edge one (loads done,
     // stores of the previous tile in flight): the compiler then never waits for stores in the loop
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    uint64_t tp = PROF ? clock64() : 0;
     for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
         lds_barrier();  // the previous tile's runs have been read out of LDS
+        if (PROF && tid == 0) {  // phase 5: previous store loop issue + this top barrier
+            const uint64_t t1 = clock64();
+            atomicAdd(&prof[5], (unsigned long long)(t1 - tp));
+            tp = t1;
+        }
         for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
         if (tid < RADIX) s_toff[tid] = toff;
         lds_barrier();
+        if (PROF && tid == 0) {  // phase 4: counter reset (+ the wait for this tile's loads)
+            const uint64_t t1 = clock64();
+            atomicAdd(&prof[4], (unsigned long long)(t1 - tp));
+            tp = t1;
+        }
         bool valid[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
         uint32_t slot[I];
-        partition_stage<T, I, R>(key, val, valid, dl, s_raw, s_toff, s_wsum, s_start, slot);
+        partition_stage<T, I, R, PROF>(key, val, valid, dl, s_raw, s_toff, s_wsum, s_start, slot, prof);
+        if (PROF) tp = clock64();
         const uint32_t cnt = s_start[RADIX];
         const uint64_t seq = (uint64_t)t * (T * I);
         if (t + walk.step < walk.end) load(t + walk.step);
         partition_store<T, I, R, MODE>(dl, s_raw, s_toff, cnt, sink, kout, vout, seq);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Software-pipelined partition: the previous tile's stores overlap this tile's load wait and its
+// ranking.  Digit counters have their own LDS (not aliased with the staging area), so the staged
+// previous tile can be stored while this tile is ranked:
+//   top    zero this wave's counters; digit offsets of this tile into s_toff[cur]
+//   B      PRE store groups of the previous tile (this tile's loads are still in flight), then
+//          rank item i interleaved with store group PRE + i
+//   C      scan -> tile digit starts, s_toff[cur] -= start          (barrier before and after)
+//   D      slots, staging of this tile (its count kept for the next iteration), barrier
+//   E      loads of the next tile
+// The last tile's stores follow the loop.  R-bit digits, one thread per digit (T >= 2^R).
+// ---------------------------------------------------------------------------------------------
+template <int T, int I>
+struct PipeSmem {
+    static constexpr int kTile = T * I;
+    static constexpr int kWaves = T / 64;
+    static constexpr int kValOff = (kTile + 2) * 8;
+    static constexpr int kStage = kValOff + (kTile + 1) * 4;
+};
+
+template <int T, int I, int R, int MODE>
+__device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys, const uint32_t *s_vals,
+                                           const uint32_t *toff, uint32_t cnt, uint64_t sink,
+                                           uint64_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+    const uint32_t s = min((uint32_t)(threadIdx.x + g * T), cnt - 1);  // cnt == 0: stays in the tile
+    const uint64_t k = s_keys[s];
+    const uint32_t v = s_vals[s];
+    const uint64_t o = cnt ? (uint64_t)(toff[dg_of(k, d)] + s) : sink;
+    if (MODE != 1 || o == 0xFFFFFFFFu) {
+        kout[o] = k;
+        vout[o] = v;
+    }
+}
+
+template <int T, int I, int R = 8, int MODE = 0>
+__global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict__ t_start,
+                                                     const uint32_t *__restrict__ t_count, Dig dl,
+                                                     const uint32_t *__restrict__ tile_off,
+                                                     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                     uint32_t ntiles, uint64_t sink) {
+    using SM = PipeSmem<T, I>;
+    constexpr int NW = SM::kWaves;
+    constexpr int TILE = SM::kTile;
+    constexpr int PRE = (I + 2) / 3;  // store groups issued before the ranking starts
+    constexpr int RADIX = 1 << R;
+    static_assert(T >= RADIX, "one thread per digit");
+    __shared__ __attribute__((aligned(16))) unsigned char s_stage[SM::kStage];
+    __shared__ uint32_t s_wc[NW * RADIX];
+    __shared__ uint32_t s_toff[2][RADIX];
+    __shared__ uint32_t s_start[RADIX + 1];
+    __shared__ uint32_t s_wsum[RADIX / 64 > 0 ? RADIX / 64 : 1];
+    uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_stage);
+    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_stage + SM::kValOff);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const TileWalk walk(ntiles);
+    uint64_t key[I];
+    uint32_t val[I], m = 0, toff = 0;
+    auto load = [&](uint32_t t) {
+        toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // first: waiting for it leaves the keys in flight
+        const uint64_t b = t_start[t];
+        m = t_count[t];  // >= 1
+        uint32_t q0 = wave * (I * 64) + lane;
+        asm volatile("" : "+v"(q0));
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint64_t e = b + min(q0 + i * 64, m - 1);
+            key[i] = kin[e];
+            val[i] = vin[e];
+        }
+    };
+    uint32_t pcnt = 0;  // staged elements of the previous tile (0: none -> stores go to the sink)
+    int cur = 0;
+    if (walk.first < walk.end) load(walk.first);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        uint32_t *wc = s_wc + wave * RADIX;
+#pragma unroll
+        for (int u = 0; u < (RADIX + 63) / 64; ++u)
+            if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
+        if (tid < RADIX) s_toff[cur][tid] = toff;
+        const uint32_t *ptoff = s_toff[cur ^ 1];
+#pragma unroll
+        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, MODE>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        bool valid[I];
+        uint32_t dig[I], rank[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
+            dig[i] = dg_of(key[i], dl);
+            const uint64_t peers = match_peers<R>(dig[i], valid[i]);
+            const uint32_t rank_in = lanes_below(peers);
+            const uint32_t old = wc[dig[i]];
+            if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
+            rank[i] = old + rank_in;
+            if (PRE + i < I) pipe_store<T, I, R, MODE>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        }
+        lds_barrier();  // ranks final; the previous tile's staging has been read out
+        uint32_t total = 0, incl = 0;
+        if (tid < RADIX) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t v = s_wc[w * RADIX + tid];
+                s_wc[w * RADIX + tid] = total;
+                total += v;
+            }
+            incl = total;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            if (lane == 63) s_wsum[wave] = incl;
+        }
+        lds_barrier();
+        if (tid < RADIX) {
+            uint32_t pre = 0;
+            for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+            const uint32_t st = pre + incl - total;
+            s_start[tid] = st;
+            s_toff[cur][tid] -= st;
+            if (tid == RADIX - 1) s_start[RADIX] = pre + incl;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t sl = valid[i] ? s_start[dig[i]] + wc[dig[i]] + rank[i] : (uint32_t)TILE;
+            s_keys[sl] = key[i];
+            s_vals[sl] = val[i];
+        }
+        pcnt = s_start[RADIX];
+        lds_barrier();  // staging complete; counters read
+        if (t + walk.step < walk.end) load(t + walk.step);
+        cur ^= 1;
+    }
+    if (walk.first < walk.end) {
+        const uint32_t *ptoff = s_toff[cur ^ 1];
+#pragma unroll
+        for (int g = 0; g < I; ++g) pipe_store<T, I, R, MODE>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
     }
 }
 

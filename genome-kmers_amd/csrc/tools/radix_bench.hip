@@ -81,11 +81,13 @@ struct Bufs {
 struct MsdTables {
     uint32_t *t_start = nullptr, *t_count = nullptr, *tile_off = nullptr;
     uint64_t tiles = 0;
-    int tile = 0;
+    int tile = 0, rbits = 8;
 };
 
-static void msd_tables_for(Bufs &b, hipStream_t st, int tile, MsdTables &m) {
-    if (m.tile == tile) return;
+static void msd_tables_for(Bufs &b, hipStream_t st, int tile, MsdTables &m, int rbits = 8) {
+    if (m.tile == tile && m.rbits == rbits) return;
+    m.rbits = rbits;
+    const int RADIX = 1 << rbits;
     if (m.t_start) {
         CK(hipFree(m.t_start));
         CK(hipFree(m.t_count));
@@ -100,35 +102,39 @@ static void msd_tables_for(Bufs &b, hipStream_t st, int tile, MsdTables &m) {
     }
     CK(hipMalloc(&m.t_start, 4 * m.tiles));
     CK(hipMalloc(&m.t_count, 4 * m.tiles));
-    CK(hipMalloc(&m.tile_off, 4 * 256 * m.tiles));
+    CK(hipMalloc(&m.tile_off, 4 * RADIX * m.tiles));
     CK(hipMemcpy(m.t_start, ts.data(), 4 * m.tiles, hipMemcpyHostToDevice));
     CK(hipMemcpy(m.t_count, tc.data(), 4 * m.tiles, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(msd_count_kernel<8>, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count, Dig{54, 255u},
-                       b.k[0], m.tile_off);
+    if (rbits == 8)
+        hipLaunchKernelGGL(msd_count_kernel<8>, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count,
+                           Dig{54, 255u}, b.k[0], m.tile_off);
+    else
+        hipLaunchKernelGGL(msd_count_kernel<7>, dim3((unsigned)m.tiles), dim3(256), 0, st, m.t_start, m.t_count,
+                           Dig{55, 127u}, b.k[0], m.tile_off);
     CK(hipStreamSynchronize(st));
-    std::vector<uint32_t> h(256 * m.tiles);
-    CK(hipMemcpy(h.data(), m.tile_off, 4 * 256 * m.tiles, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> tot(256, 0);
+    std::vector<uint32_t> h((size_t)RADIX * m.tiles);
+    CK(hipMemcpy(h.data(), m.tile_off, 4 * RADIX * m.tiles, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> tot(RADIX, 0);
     for (uint64_t j = 0; j < m.tiles; ++j)
-        for (int d = 0; d < 256; ++d) tot[d] += h[j * 256 + d];
-    std::vector<uint64_t> run(256);
+        for (int d = 0; d < RADIX; ++d) tot[d] += h[j * RADIX + d];
+    std::vector<uint64_t> run(RADIX);
     uint64_t r = 0;
-    for (int d = 0; d < 256; ++d) {
+    for (int d = 0; d < RADIX; ++d) {
         run[d] = r;
         r += tot[d];
     }
     for (uint64_t j = 0; j < m.tiles; ++j)
-        for (int d = 0; d < 256; ++d) {
-            const uint32_t c = h[j * 256 + d];
-            h[j * 256 + d] = (uint32_t)run[d];
+        for (int d = 0; d < RADIX; ++d) {
+            const uint32_t c = h[j * RADIX + d];
+            h[j * RADIX + d] = (uint32_t)run[d];
             run[d] += c;
         }
-    CK(hipMemcpy(m.tile_off, h.data(), 4 * 256 * m.tiles, hipMemcpyHostToDevice));
+    CK(hipMemcpy(m.tile_off, h.data(), 4 * (size_t)RADIX * m.tiles, hipMemcpyHostToDevice));
 }
 
 template <int T, int I, int MODE>
 static void run_msd(Bufs &b, MsdTables &m, const char *name, hipStream_t st, unsigned long long ref_sum,
-                    unsigned grid = 256) {
+                    unsigned grid = 256, int stagger = 0) {
     msd_tables_for(b, st, T * I, m);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -137,8 +143,9 @@ static void run_msd(Bufs &b, MsdTables &m, const char *name, hipStream_t st, uns
     const int R = 4;
     for (int r = 0; r <= R; ++r) {
         CK(hipEventRecord(e0, st));
-        hipLaunchKernelGGL((msd_scatter_kernel<T, I, 8, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
-                           Dig{54, 255u}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n);
+        hipLaunchKernelGGL((msd_scatter_kernel<T, I, 8, MODE, false>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+                           Dig{54, 255u}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n,
+                           nullptr, stagger);
         CK(hipEventRecord(e1, st));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -153,13 +160,71 @@ static void run_msd(Bufs &b, MsdTables &m, const char *name, hipStream_t st, uns
         unsigned long long *d;
         CK(hipMalloc(&d, 16));
         CK(hipMemset(d, 0, 16));
-        hipLaunchKernelGGL(check_kernel, dim3(2048), dim3(256), 0, st, b.k[1], b.v[1], b.n, 54, d, d + 1);
+        hipLaunchKernelGGL(check_kernel, dim3(2048), dim3(256), 0, st, b.k[1], b.v[1], b.n, 62 - R, d, d + 1);
         unsigned long long hh[2];
         CK(hipMemcpy(hh, d, 16, hipMemcpyDeviceToHost));
         CK(hipFree(d));
         verdict = (hh[0] == 0 && hh[1] == ref_sum) ? "sorted" : "WRONG";
     }
     std::printf("%-34s tile %6d  avg %8.3f ms  best %8.3f ms  %7.1f GB/s (24 B/key)  %s\n", name, T * I, tot / R, best,
+                b.n * 24.0 / (best * 1e-3) / 1e9, verdict);
+}
+
+// phase profile of the production partition kernel (timing build): clock ticks per tile
+template <int T, int I>
+static void profile_msd(Bufs &b, MsdTables &m, hipStream_t st, unsigned grid) {
+    msd_tables_for(b, st, T * I, m);
+    unsigned long long *prof;
+    CK(hipMalloc(&prof, 8 * 8));
+    CK(hipMemset(prof, 0, 64));
+    hipLaunchKernelGGL((msd_scatter_kernel<T, I, 8, 0, true>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+                       Dig{54, 255u}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n, prof);
+    CK(hipStreamSynchronize(st));
+    unsigned long long h[8];
+    CK(hipMemcpy(h, prof, 64, hipMemcpyDeviceToHost));
+    const char *names[6] = {"rank", "scan", "slots", "stage", "reset", "store+top"};
+    unsigned long long tot = 0;
+    for (int i = 0; i < 6; ++i) tot += h[i];
+    std::printf("phase profile T%d I%d grid %u (clock ticks per tile, thread 0):", T, I, grid);
+    for (int i = 0; i < 6; ++i) std::printf("  %s %.0f (%.0f%%)", names[i], (double)h[i] / m.tiles, 100.0 * h[i] / tot);
+    std::printf("\n");
+    CK(hipFree(prof));
+}
+
+template <int T, int I, int R, int MODE>
+static void run_pipe(Bufs &b, MsdTables &m, const char *name, hipStream_t st, unsigned long long ref_sum,
+                     unsigned grid) {
+    msd_tables_for(b, st, T * I, m, R);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float tot = 0, best = 1e30f;
+    const int RR = 4;
+    for (int r = 0; r <= RR; ++r) {
+        CK(hipEventRecord(e0, st));
+        hipLaunchKernelGGL((msd_pipe_kernel<T, I, R, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+                           Dig{62 - R, (1u << R) - 1}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r) {
+            tot += ms;
+            best = std::min(best, ms);
+        }
+    }
+    const char *verdict = "-";
+    if (MODE == 0) {
+        unsigned long long *d;
+        CK(hipMalloc(&d, 16));
+        CK(hipMemset(d, 0, 16));
+        hipLaunchKernelGGL(check_kernel, dim3(2048), dim3(256), 0, st, b.k[1], b.v[1], b.n, 62 - R, d, d + 1);
+        unsigned long long hh[2];
+        CK(hipMemcpy(hh, d, 16, hipMemcpyDeviceToHost));
+        CK(hipFree(d));
+        verdict = (hh[0] == 0 && hh[1] == ref_sum) ? "sorted" : "WRONG";
+    }
+    std::printf("%-34s tile %6d  avg %8.3f ms  best %8.3f ms  %7.1f GB/s (24 B/key)  %s\n", name, T * I, tot / RR, best,
                 b.n * 24.0 / (best * 1e-3) / 1e9, verdict);
 }
 
@@ -311,11 +376,11 @@ int main(int argc, char **argv) {
     run_scatter<98304>(b, st);
     MsdTables m;
     run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12", st, ref_sum, 1024);
-    run_msd<1024, 12, 1>(b, m, "msd pass T1024 I12 no-store", st, ref_sum, 1024);
-    run_msd<512, 12, 0>(b, m, "msd pass T512 I12 grid 512", st, ref_sum, 512);
-    run_msd<512, 12, 0>(b, m, "msd pass T512 I12 grid 2048", st, ref_sum, 2048);
-    run_msd<512, 8, 0>(b, m, "msd pass T512 I8 grid 2048", st, ref_sum, 2048);
-    run_msd<256, 16, 0>(b, m, "msd pass T256 I16 grid 2048", st, ref_sum, 2048);
+    run_pipe<1024, 11, 8, 0>(b, m, "pipe T1024 I11 R8 grid 1024", st, ref_sum, 1024);
+    run_pipe<1024, 11, 7, 0>(b, m, "pipe T1024 I11 R7 grid 1024", st, ref_sum, 1024);
+    run_pipe<1024, 11, 7, 1>(b, m, "pipe T1024 I11 R7 no-store", st, ref_sum, 1024);
+    run_pipe<1024, 8, 7, 0>(b, m, "pipe T1024 I8 R7 grid 1024", st, ref_sum, 1024);
+    run_pipe<512, 11, 7, 0>(b, m, "pipe T512 I11 R7 grid 2048", st, ref_sum, 2048);
     if (argc > 2) return 0;
     const int R = 4;
     run_variant<256, 16, true>(b, "onesweep T256 I16 (current)", st, R, ref_sum);

@@ -206,10 +206,10 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
 
 // software-pipelined L0 (see msd_pipe_kernel): the previous tile's stores overlap this tile's
 // packing, key extraction and ranking; the next tile's bytes are loaded after the staging
-template <int BITS, int T, int I, int R>
+template <int BITS, int T, int I, int R, bool ND>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                      uint32_t ntiles, uint64_t sink) {
+                                                      uint32_t ntiles, uint64_t sink, NextDigits nd) {
     constexpr int TILE = T * I;
     constexpr int RADIX = 1 << R;
     constexpr int NW = T / 64;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
-        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         lds_barrier();  // packed codes visible
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         uint64_t key[I];
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             const uint32_t old = wc[dig[i]];
             if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
             rank[i] = old + rank_in;
-            if (PRE + i < I) pipe_store<T, I, R, 0>(PRE + i, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+            if (PRE + i < I) pipe_store<T, I, R, 0, ND>(PRE + i, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         }
         lds_barrier();  // ranks final; the previous tile's staging has been read out
         uint32_t total = 0, incl = 0;
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     if (walk.first < walk.end) {
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
-        for (int g = 0; g < I; ++g) pipe_store<T, I, R, 0>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        for (int g = 0; g < I; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
     }
 }
 
@@ -623,16 +623,21 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         uint32_t slot[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < len;
-        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot);
+        // items of this wave holding elements (wave-uniform)
+        const int wbase = wave * (I * 64);
+        const int live = (int)len > wbase ? min(I, ((int)len - wbase + 63) >> 6) : 0;
+        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live);
 
         // 2. final position and head flag of every element
         uint32_t out[I];
         uint8_t hd[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) {
+            out[i] = slot[i];
+            hd[i] = 0;
+            if (i >= live) continue;  // wave-uniform
             const uint32_t dg = dg_of(key[i], dd);
             const uint32_t sb = s_start[dg], size = s_start[dg + 1] - sb;
-            out[i] = slot[i];
             hd[i] = slot[i] == sb;  // singleton or equal keys: the first is the head
             if (valid[i] && size > 1 && !last) {
                 if (size <= (uint32_t)kSmall) {
@@ -669,6 +674,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         }
 #pragma unroll
         for (int i = 0; i < I; ++i) {  // invalid items: out = sink slot
+            if (i >= live) continue;
             s_k[out[i]] = key[i];
             s_v[out[i]] = val[i];
             s_hd[out[i]] = hd[i] == 1;
@@ -767,6 +773,8 @@ struct MsdDriver {
     uint8_t *dn_par;
     uint2 *blk[2], *wav[2];
     uint8_t *heads = nullptr;
+    uint8_t *nd = nullptr;  // next-level digit per element of the last pass's output
+    bool nd_ready = false;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
     uint64_t nblk = 0, nwav = 0, ndone = 0, big_elems = 0, blk_elems = 0, wav_elems = 0;
     uint32_t nbig = 0;
@@ -879,14 +887,31 @@ struct MsdDriver {
         if (*count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
         timer_begin(c, "msd_pass_l0", &slot);
         timer_units(c, slot, *count);
-        if (ks.bits == 2)
-            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, (uint32_t)nt0, *count);
+        // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
+        // exchange, so they do not)
+        const bool with_nd = kout == c->keys[0];
+        NextDigits ndg{dig_at(B, kGR, kGR), nullptr};
+        if (with_nd) {
+            GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
+            ndg.out = nd;
+        }
+        const unsigned g = pgrid;
+        const uint32_t nt = (uint32_t)nt0;
+        if (ks.bits == 2 && with_nd)
+            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, nt, *count, ndg);
+        else if (ks.bits == 2)
+            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR, false>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, nt, *count, ndg);
+        else if (with_nd)
+            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, nt, *count, ndg);
         else
-            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, (uint32_t)nt0, *count);
+            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR, false>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, nt, *count, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
+        nd_ready = with_nd;
         return GK_OK;
     }
 
@@ -922,20 +947,27 @@ struct MsdDriver {
                    const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start, uint64_t nseg,
                    const uint64_t *kin, const uint32_t *vin, int out) {
         const Dig dl = dig_at(B, hi, kGR);
-        timer_begin(c, "msd_count", &slot);
+        timer_begin(c, nd_ready ? "msd_count_nd" : "msd_count", &slot);
         timer_units(c, slot, big_elems);
-        hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl, kin,
-                           tile_hist);
+        if (nd_ready)  // the previous pass wrote this level's digits
+            hipLaunchKernelGGL(msd_count_nd_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count,
+                               nd, tile_hist);
+        else
+            hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
+                               kin, tile_hist);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         int rc = scan_offsets(C, s_cfirst, s_nchunks, s_start, nseg);
         if (rc != GK_OK) return rc;
         timer_begin(c, kPassNames[level & 7], &slot);
         timer_units(c, slot, big_elems);
-        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, kGR>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start, t_count,
-                           dl, tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n);
+        GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
+        const NextDigits ndg{dig_at(B, hi + kGR, kGR), nd};
+        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, kGR, 0, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
+                           t_count, dl, tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
+        nd_ready = true;
         return GK_OK;
     }
 

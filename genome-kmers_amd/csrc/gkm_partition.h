@@ -28,6 +28,7 @@ struct Dig {
 };
 
 __host__ __device__ inline Dig dig_at(int B, int hi, int w) {
+    if (hi >= B) return Dig{0, 0u};  // no bits left: every key has digit 0
     int lo = B - hi - w;
     if (lo < 0) lo = 0;
     return Dig{lo, (uint32_t)((1ull << (B - hi - lo)) - 1)};
@@ -69,9 +70,11 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // one wave complete in order, so item i+1 reads item i's update.
 template <int I, int R>
 __device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool (&valid)[I], uint32_t *s_wc_wave,
-                                           uint32_t (&rank)[I]) {
+                                           uint32_t (&rank)[I], int live = I) {
 #pragma unroll
     for (int i = 0; i < I; ++i) {
+        rank[i] = 0;
+        if (i >= live) continue;  // wave-uniform: no valid item in this or later slots
         const uint64_t peers = match_peers<R>(dig[i], valid[i]);
         const uint32_t rank_in = lanes_below(peers);
         const uint32_t old = s_wc_wave[dig[i]];
@@ -101,13 +104,15 @@ struct PartSmem {
 // Barriers inside: all T threads must call.
 // s_start[RADIX + 1] receives the tile-local digit starts (s_start[RADIX] = item count) and
 // slot[] each item's staging slot (invalid items: the sink slot kTile); s_toff may be null.
+// live (wave-uniform): items >= live of this wave hold no valid element and are skipped.
 // PROF (timing builds of tools/radix_bench only): thread 0 adds the clock ticks of each phase to
 // prof[0..3] (rank, scan, slots, staging).
 template <int T, int I, int R, bool PROF = false>
 __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const uint32_t (&val)[I],
                                                 const bool (&valid)[I], Dig d, unsigned char *s_raw,
                                                 uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_start,
-                                                uint32_t (&slot)[I], unsigned long long *prof = nullptr) {
+                                                uint32_t (&slot)[I], unsigned long long *prof = nullptr,
+                                                int live = I) {
     using SM = PartSmem<T, I, R>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -128,7 +133,7 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     uint32_t dig[I], rank[I];
 #pragma unroll
     for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
-    rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank);
+    rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank, live);
     lds_barrier();
     mark(0);
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
@@ -179,7 +184,8 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     lds_barrier();  // counters consumed: the staging area is reused
     mark(2);
 #pragma unroll
-    for (int i = 0; i < I; ++i) {  // branch-free: invalid items go to the sink slot
+    for (int i = 0; i < I; ++i) {  // invalid items go to the sink slot
+        if (i >= live) continue;
         s_keys[slot[i]] = key[i];
         s_vals[slot[i]] = val[i];
     }
@@ -251,6 +257,37 @@ __global__ __launch_bounds__(256) void msd_count_kernel(const uint32_t *__restri
     const uint64_t b = t_start[blockIdx.x];
     const uint32_t m = t_count[blockIdx.x];
     for (uint32_t i = t; i < m; i += 256) atomicAdd(&s_hist[dg_of(kin[b + i], dl)], 1u);
+    lds_barrier();
+    for (int i = t; i < RADIX; i += 256) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
+}
+
+// the count pass when the previous pass wrote the digits (NextDigits): 1 byte per key
+template <int R>
+__global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__restrict__ t_start,
+                                                           const uint32_t *__restrict__ t_count,
+                                                           const uint8_t *__restrict__ nd,
+                                                           uint32_t *__restrict__ tile_hist) {
+    constexpr int RADIX = 1 << R;
+    __shared__ uint32_t s_hist[RADIX];
+    const int t = threadIdx.x;
+    for (int i = t; i < RADIX; i += 256) s_hist[i] = 0;
+    lds_barrier();
+    const uint64_t b = t_start[blockIdx.x];
+    const uint32_t m = t_count[blockIdx.x];
+    // 4 digits per load where the run is 4-byte aligned, bytes at the ragged ends
+    const uint32_t head = min<uint32_t>((uint32_t)((4 - (b & 3)) & 3), m);
+    const uint32_t words = (m - head) >> 2;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(nd + b + head);
+    if (t < (int)head) atomicAdd(&s_hist[nd[b + t]], 1u);
+    for (uint32_t i = t; i < words; i += 256) {
+        const uint32_t x = w[i];
+        atomicAdd(&s_hist[x & 0xFF], 1u);
+        atomicAdd(&s_hist[(x >> 8) & 0xFF], 1u);
+        atomicAdd(&s_hist[(x >> 16) & 0xFF], 1u);
+        atomicAdd(&s_hist[x >> 24], 1u);
+    }
+    const uint32_t tail0 = head + 4 * words;
+    if (tail0 + t < m) atomicAdd(&s_hist[nd[b + tail0 + t]], 1u);
     lds_barrier();
     for (int i = t; i < RADIX; i += 256) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
 }
@@ -347,10 +384,18 @@ struct PipeSmem {
     static constexpr int kStage = kValOff + (kTile + 1) * 4;
 };
 
-template <int T, int I, int R, int MODE>
+// the next level's digit of every stored key, one byte per element at the key's output index, so
+// that level's count pass reads 1 byte per key instead of 8 (ND = false: not written)
+struct NextDigits {
+    Dig d;
+    uint8_t *out;
+};
+
+template <int T, int I, int R, int MODE, bool ND>
 __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys, const uint32_t *s_vals,
                                            const uint32_t *toff, uint32_t cnt, uint64_t sink,
-                                           uint64_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+                                           uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                           NextDigits nd) {
     const uint32_t s = min((uint32_t)(threadIdx.x + g * T), cnt - 1);  // cnt == 0: stays in the tile
     const uint64_t k = s_keys[s];
     const uint32_t v = s_vals[s];
@@ -358,16 +403,17 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     if (MODE != 1 || o == 0xFFFFFFFFu) {
         kout[o] = k;
         vout[o] = v;
+        if (ND) nd.out[o] = (uint8_t)dg_of(k, nd.d);
     }
 }
 
-template <int T, int I, int R = 8, int MODE = 0>
+template <int T, int I, int R = 8, int MODE = 0, bool ND = false>
 __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict__ t_start,
                                                      const uint32_t *__restrict__ t_count, Dig dl,
                                                      const uint32_t *__restrict__ tile_off,
                                                      const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                     uint32_t ntiles, uint64_t sink) {
+                                                     uint32_t ntiles, uint64_t sink, NextDigits nd = {}) {
     using SM = PipeSmem<T, I>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -410,7 +456,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
         if (tid < RADIX) s_toff[cur][tid] = toff;
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
-        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, MODE>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, MODE, ND>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         bool valid[I];
         uint32_t dig[I], rank[I];
 #pragma unroll
@@ -422,7 +468,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
             const uint32_t old = wc[dig[i]];
             if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
             rank[i] = old + rank_in;
-            if (PRE + i < I) pipe_store<T, I, R, MODE>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+            if (PRE + i < I) pipe_store<T, I, R, MODE, ND>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         }
         lds_barrier();  // ranks final; the previous tile's staging has been read out
         uint32_t total = 0, incl = 0;
@@ -465,7 +511,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
     if (walk.first < walk.end) {
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
-        for (int g = 0; g < I; ++g) pipe_store<T, I, R, MODE>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout);
+        for (int g = 0; g < I; ++g) pipe_store<T, I, R, MODE, ND>(g, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
     }
 }
 

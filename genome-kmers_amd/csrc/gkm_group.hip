@@ -97,39 +97,31 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
-// Striped: thread t of the tile owns positions base + 256 k + t (k < 16), so the selected
-// positions of a row are ranked with one ballot per wave and written as contiguous runs.
+// Thread t loads the 16 flags of positions 16t..16t+15 (one 16-B load), writes its selected
+// positions to LDS after a block scan, and the tile's list is then copied out as one contiguous
+// run.  The LDS index is XOR-swizzled within 32-word rows: dense flags (every k-mer distinct)
+// would otherwise put 32 lanes of one store on two banks.
+__device__ __forceinline__ uint32_t sel_swz(uint32_t o) { return (o & ~31u) | ((o ^ (o >> 5)) & 31u); }
+
 __global__ __launch_bounds__(kScanThreads) void flag_select_kernel(const uint8_t *__restrict__ f, uint64_t n,
                                                                    const uint32_t *__restrict__ tile_off,
                                                                    uint32_t *__restrict__ out) {
-    constexpr int NW = kScanThreads / 64;
-    __shared__ uint32_t s_cnt[kScanItems][NW];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
-    bool sel[kScanItems];
-    uint32_t below[kScanItems];
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    __shared__ uint32_t s_idx[kScanTile];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint8_t v[16];
+    load16_flags(f, n, at, v);
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        const uint64_t p = base + (uint64_t)k * kScanThreads;
-        sel[k] = p < n && f[p] != 0;
-        const uint64_t m = __ballot(sel[k]);
-        below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (lane == 0) s_cnt[k][wave] = (uint32_t)__popcll(m);
-    }
+    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
+    uint32_t tot;
+    uint32_t o = block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (v[k]) s_idx[sel_swz(o++)] = (uint32_t)(at + k);
     __syncthreads();
-    uint32_t run = tile_off[blockIdx.x];
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        uint32_t pre = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t x = s_cnt[k][w];
-            pre += w < wave ? x : 0u;
-            tot += x;
-        }
-        if (sel[k]) out[run + pre + below[k]] = (uint32_t)(base + (uint64_t)k * kScanThreads);
-        run += tot;
-    }
+    uint32_t *dst = out + tile_off[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < tot; j += kScanThreads) dst[j] = s_idx[sel_swz(j)];
 }
 
 __global__ __launch_bounds__(kScanThreads) void flag_scan_incl_kernel(const uint8_t *__restrict__ f, uint64_t n,

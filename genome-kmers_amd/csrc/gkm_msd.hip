@@ -31,7 +31,7 @@ constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk
 constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
 constexpr int kBlockMax = kBT * kBI;    // 4096
-constexpr int kWT = 64, kWI = 4, kWR = 8;    // wave-local: 64 threads x 4 keys, 8-bit digit
+constexpr int kWT = 64, kWI = 4;         // wave-local: 64 threads x 4 keys (msd_wave_kernel)
 constexpr int kWaveMax = kWT * kWI;     // 256
 constexpr int kSmall = 24;              // sub-buckets <= this: rank-by-count
 
@@ -695,6 +695,169 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     }
 }
 
+// Single-wave finishing kernel for buckets of <= 256 elements (the common case: ~185 at C3).
+// Same contract as msd_local_kernel<64, 4, 8>, with a cheaper stable ranking: instead of 8
+// ballots per item, each lane ORs its bit into an LDS mask of its digit, reads the mask back
+// (its peers) and zeroes it; the first peer of each item adds the item's count to the digit's
+// counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
+// in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
+// -- the ranks are stable.  About 12 VALU per item instead of about 50.
+constexpr int kWaveItems = 4;
+
+__global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
+                                                      uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                      const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
+                                                      uint32_t *__restrict__ ctr) {
+    constexpr int I = kWaveItems;
+    constexpr int CAP = 64 * I;
+    __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
+    __shared__ uint32_t s_v[CAP + 1];
+    __shared__ uint64_t s_mask[256];
+    __shared__ uint32_t s_cnt[257];  // digit counts, then exclusive starts (s_cnt[256] = total)
+    __shared__ uint8_t s_hd[CAP + 1];
+    const int lane = threadIdx.x;
+    const uint64_t me_bit = 1ull << lane;
+    uint32_t idx = blockIdx.x;
+    if (idx >= count) return;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;
+    uint2 e = list[idx];
+    uint64_t key[I];
+    uint32_t val[I];
+    local_load<64, I>(e, k0, v0, k1, v1, key, val);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (; idx < count; idx += gridDim.x) {
+        const uint2 ce = e;
+        const uint64_t st = ce.x;
+        const uint32_t len = ce.y >> 8;
+        const int hi = (ce.y >> 1) & 127;
+        const Dig dd = dig_at(B, hi, 8);
+        const int nhi = hi + 8;
+        const bool last = nhi >= B;
+        if (idx + gridDim.x < count) e = list[idx + gridDim.x];
+        const int live = min(I, (int)((len + 63) >> 6));
+
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s_cnt[u * 64 + lane] = 0;
+        bool valid[I];
+        uint32_t dig[I];
+        uint64_t peers[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            valid[i] = (uint32_t)(i * 64 + lane) < len;
+            dig[i] = dg_of(key[i], dd);
+            peers[i] = 0;
+            if (i >= live) continue;
+            if (valid[i]) atomicOr((unsigned long long *)&s_mask[dig[i]], (unsigned long long)me_bit);
+            peers[i] = s_mask[dig[i]];
+            s_mask[dig[i]] = 0;  // every lane of the digit writes 0 after the wave's read
+        }
+        uint32_t rank_in[I], old[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            old[i] = 0;
+            rank_in[i] = lanes_below(peers[i]);
+            if (i < live && valid[i] && rank_in[i] == 0) old[i] = atomicAdd(&s_cnt[dig[i]], (uint32_t)__popcll(peers[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            if (i >= live) continue;
+            const int leader = valid[i] ? __ffsll((unsigned long long)peers[i]) - 1 : lane;
+            old[i] = __shfl(old[i], leader);
+        }
+        // exclusive starts over the 256 digits (4 per lane)
+        {
+            uint32_t c4[4], s4 = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                c4[u] = s_cnt[lane * 4 + u];
+                s4 += c4[u];
+            }
+            uint32_t incl = s4;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            uint32_t run = incl - s4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s_cnt[lane * 4 + u] = run;
+                run += c4[u];
+            }
+            if (lane == 63) s_cnt[256] = run;
+        }
+        uint32_t slot[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            slot[i] = CAP;
+            if (i >= live) continue;
+            slot[i] = valid[i] ? s_cnt[dig[i]] + old[i] + rank_in[i] : (uint32_t)CAP;
+            s_k[slot[i]] = key[i];
+        }
+
+        // final position and head flag of every element (reads precede writes: one wave)
+        uint32_t out[I];
+        uint8_t hd[I];
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            out[i] = slot[i];
+            hd[i] = 0;
+            if (i >= live) continue;
+            const uint32_t sb = s_cnt[dig[i]], size = s_cnt[dig[i] + 1] - sb;
+            hd[i] = slot[i] == sb;
+            if (valid[i] && size > 1 && !last) {
+                if (size <= (uint32_t)kSmall) {
+                    const uint32_t me = slot[i] - sb;
+                    uint32_t lt = 0, eq = 0;
+                    // 4 keys per step (their LDS reads in flight together); indices past the
+                    // sub-bucket are clamped and not counted
+                    for (uint32_t j0 = 0; j0 < size; j0 += 4) {
+                        uint64_t kj[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) kj[u] = s_k[min(sb + j0 + u, (uint32_t)CAP)];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t j = j0 + u;
+                            lt += j < size && kj[u] < key[i];
+                            eq += j < me && kj[u] == key[i];
+                        }
+                    }
+                    out[i] = sb + lt + eq;
+                    hd[i] = eq == 0;
+                } else {
+                    hd[i] = 2;
+                    any = true;
+                }
+            }
+        }
+        if (__ballot(any)) {  // re-list the large sub-buckets (rare)
+#pragma unroll
+            for (int i = 0; i < I; ++i) {
+                const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
+                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : 0;
+                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            if (i >= live) continue;
+            s_k[out[i]] = key[i];
+            s_v[out[i]] = val[i];
+            s_hd[out[i]] = hd[i] == 1;
+        }
+        local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket's loads fly now
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = min((uint32_t)(i * 64 + lane), len - 1);
+            k0[st + p] = s_k[p];
+            v0[st + p] = s_v[p];
+            heads[st + p] = s_hd[p];
+        }
+    }
+}
+
 // sub-buckets whose key bits are exhausted: in order already (copied to buffer 0 if needed);
 // all keys equal, so the only head is the first element
 __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restrict__ dn_start,
@@ -1092,9 +1255,16 @@ struct MsdDriver {
             if (nwav) {
                 timer_begin(c, round == 0 ? "msd_local_wave" : "msd_local_wave_r", &slot);
                 if (round == 0) timer_units(c, slot, wav_elems);
-                hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, kWR>),
-                                   dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(kWT), 0, c->stream, wav[g],
-                                   (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1], heads, nl, ctr);
+                static const bool old_wave = std::getenv("GKM_WAVE_STAGE") != nullptr;  // A/B experiments
+                if (old_wave)
+                    hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, 8>),
+                                       dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(kWT), 0, c->stream,
+                                       wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1],
+                                       heads, nl, ctr);
+                else
+                    hipLaunchKernelGGL(msd_wave_kernel, dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(64), 0,
+                                       c->stream, wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1],
+                                       c->vals[1], heads, nl, ctr);
                 GK_TRY_HIP(c, hipGetLastError());
                 timer_end(c, slot);
             }

@@ -182,7 +182,7 @@ def main():
         if b and v["total_ms"] > 0:
             kernels[name] = {"ms_per_launch": round(v["total_ms"] / v["count"], 4),
                              "gbs": round(b / (v["total_ms"] * 1e-3) / 1e9, 1)}
-    # dominant kernel: msd_scatter_kernel, the partition pass of every level >= 1 (averaged over
+    # dominant kernel: msd_pipe_kernel, the partition pass of every level >= 1 (averaged over
     # its launches, as rocprofv3 --stats averages it); the L0 pass when a genome needs none
     cands = [n for n in report if n.startswith("msd_pass_l") and n != "msd_pass_l0" and report[n]["units"]]
     if cands:
@@ -197,11 +197,11 @@ def main():
     bytes_per_launch = dom_bytes / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
-    kname = "msd_scatter_kernel" if dom != "msd_pass_l0" else "msd0_scatter_kernel"
+    kname = "msd_pipe_kernel" if dom != "msd_pass_l0" else "msd0_pipe_kernel"
     traffic = load_traffic(args.traffic, kname)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"{kname}<1024,12,8> ({dom}: one stable 8-bit MSD partition pass)",
+                "kernel": f"{kname}<1024,11,8> ({dom}: one stable 8-bit MSD partition pass)",
                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "units_per_launch": int(rp["units"] / max(rp["count"], 1)), "bytes_per_unit": 24,
                 "stages": kernels}

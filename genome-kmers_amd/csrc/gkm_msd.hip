@@ -31,9 +31,12 @@ constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk
 constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
 constexpr int kBlockMax = kBT * kBI;    // 4096
-constexpr int kWT = 64, kWI = 4;         // wave-local: 64 threads x 4 keys (msd_wave_kernel)
-constexpr int kWaveMax = kWT * kWI;     // 256
-constexpr int kSmall = 24;              // sub-buckets <= this: rank-by-count
+// local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
+// 4 or 16 keys (msd_local_kernel)
+constexpr int kLocal = 4;
+constexpr int kWaveMax = 256;
+constexpr int kSmall = 24;
+constexpr int kMaxLevels = 16;              // sub-buckets <= this: rank-by-count
 
 __constant__ uint8_t c_code4_msd[256];
 static bool g_msd_tables = false;
@@ -416,39 +419,50 @@ __device__ __forceinline__ uint32_t wave_append(bool flag, uint32_t *counter, in
     return base + (uint32_t)__popcll(m & lt_mask);
 }
 
-// list counters (device, one array): next global level, done, block-local, wave-local lists
-enum { kCtrBig = 0, kCtrDone = 1, kCtrBlock = 2, kCtrWave = 3, kCtrN = 8 };
+// list counters (device, one array): next global level, done, then the local classes
+enum { kCtrBig = 0, kCtrDone = 1, kCtrLoc = 2, kLists = kCtrLoc + kLocal, kCtrN = 8 };
 
 struct Lists {
     uint32_t *nb_start, *nb_len;                 // buckets for the next global level
     uint32_t *dn_start, *dn_len;                 // key bits exhausted: final as they stand
     uint8_t *dn_par;
-    uint2 *blk, *wav;                            // block-local / wave-local entries
+    uint2 *loc[kLocal];                          // local entries by class
 };
+
+// local class of a bucket of <= kBlockMax elements
+__host__ __device__ constexpr uint32_t local_cap(int cls) { return cls == 0 ? 256 : cls == 1 ? 512 : cls == 2 ? 1024 : 4096; }
+
+// list of a live sub-bucket of `size` elements (kCtr* index)
+__device__ __forceinline__ int list_of(uint32_t size, int hi, int B, bool allow_big) {
+    if (hi >= B) return kCtrDone;
+    if (size > (uint32_t)kBlockMax && allow_big) return kCtrBig;
+    return kCtrLoc + (size <= local_cap(0) ? 0 : size <= local_cap(1) ? 1 : size <= local_cap(2) ? 2 : 3);
+}
+
+// entry `at` of list l for a sub-bucket
+__device__ __forceinline__ void put_entry(const Lists &L, int l, uint32_t at, uint32_t st, uint32_t size, int hi,
+                                          int parity) {
+    if (l == kCtrBig) {
+        L.nb_start[at] = st;
+        L.nb_len[at] = size;
+    } else if (l == kCtrDone) {
+        L.dn_start[at] = st;
+        L.dn_len[at] = size;
+        L.dn_par[at] = (uint8_t)parity;
+    } else {
+        L.loc[l - kCtrLoc][at] = local_entry(st, size, hi, parity);
+    }
+}
 
 // route one sub-bucket (size >= 1) by size; hi = key bits sorted once it is cut out
 __device__ __forceinline__ void route(uint32_t st, uint32_t size, int hi, int B, int parity, bool allow_big,
                                       const Lists &L, uint32_t *ctr, int lane) {
-    const bool live = size >= 1;
-    const bool done = live && hi >= B;
-    const bool big = live && !done && size > (uint32_t)kBlockMax && allow_big;
-    const bool blk = live && !done && !big && size > (uint32_t)kWaveMax;
-    const bool wav = live && !done && !big && !blk;
-    const uint32_t a = wave_append(big, &ctr[kCtrBig], lane);
-    if (big) {
-        L.nb_start[a] = st;
-        L.nb_len[a] = size;
+    const int li = size >= 1 ? list_of(size, hi, B, allow_big) : -1;
+#pragma unroll
+    for (int l = 0; l < kLists; ++l) {
+        const uint32_t at = wave_append(li == l, &ctr[l], lane);
+        if (li == l) put_entry(L, l, at, st, size, hi, parity);
     }
-    const uint32_t b = wave_append(done, &ctr[kCtrDone], lane);
-    if (done) {
-        L.dn_start[b] = st;
-        L.dn_len[b] = size;
-        L.dn_par[b] = (uint8_t)parity;
-    }
-    const uint32_t c = wave_append(blk, &ctr[kCtrBlock], lane);
-    if (blk) L.blk[c] = local_entry(st, size, hi, parity);
-    const uint32_t d = wave_append(wav, &ctr[kCtrWave], lane);
-    if (wav) L.wav[d] = local_entry(st, size, hi, parity);
 }
 
 // The sub-buckets of one global level, one per thread: a workgroup-aggregated append (one
@@ -461,21 +475,19 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
                                                            int B, int parity, Lists L, uint32_t *__restrict__ ctr,
                                                            unsigned long long *__restrict__ sums) {
     constexpr int NW = kClassT / 64;
-    __shared__ uint32_t s_cnt[4][NW];
-    __shared__ uint32_t s_elems[4][NW];
-    __shared__ uint32_t s_base[4];
+    __shared__ uint32_t s_cnt[kLists][NW];
+    __shared__ uint32_t s_elems[kLists][NW];
+    __shared__ uint32_t s_base[kLists];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kClassT + tid;
     const uint32_t size = i < nsub ? seg_cnt[i] : 0, st = i < nsub ? seg_base[i] : 0;
-    const bool live = size >= 1;
-    const bool done = live && hi >= B;
-    const bool big = live && !done && size > (uint32_t)kBlockMax;
-    const bool blk = live && !done && !big && size > (uint32_t)kWaveMax;
-    const bool wav = live && !done && !big && !blk;
-    const bool f[4] = {big, done, blk, wav};  // list order = kCtrBig, kCtrDone, kCtrBlock, kCtrWave
-    uint32_t below[4];
+    const int li = size >= 1 ? list_of(size, hi, B, true) : -1;
+    bool f[kLists];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
+    for (int l = 0; l < kLists; ++l) f[l] = li == l;
+    uint32_t below[kLists];
+#pragma unroll
+    for (int l = 0; l < kLists; ++l) {
         const uint64_t m = __ballot(f[l]);
         below[l] = lanes_below(m);
         uint32_t e = f[l] ? size : 0;
@@ -487,7 +499,7 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
         }
     }
     __syncthreads();
-    if (tid < 4) {
+    if (tid < kLists) {
         uint32_t tot = 0;
         unsigned long long el = 0;
         for (int w = 0; w < NW; ++w) {
@@ -498,24 +510,16 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
         if (el) atomicAdd(&sums[tid], el);
     }
     __syncthreads();
-    uint32_t at[4];
+    uint32_t at[kLists];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
+    for (int l = 0; l < kLists; ++l) {
         uint32_t pre = s_base[l];
         for (int w = 0; w < wave; ++w) pre += s_cnt[l][w];
         at[l] = pre + below[l];
     }
-    if (big) {
-        L.nb_start[at[0]] = st;
-        L.nb_len[at[0]] = size;
-    }
-    if (done) {
-        L.dn_start[at[1]] = st;
-        L.dn_len[at[1]] = size;
-        L.dn_par[at[1]] = (uint8_t)parity;
-    }
-    if (blk) L.blk[at[2]] = local_entry(st, size, hi, parity);
-    if (wav) L.wav[at[3]] = local_entry(st, size, hi, parity);
+#pragma unroll
+    for (int l = 0; l < kLists; ++l)
+        if (li == l) put_entry(L, l, at[l], st, size, hi, parity);
 }
 
 // tile + chunk tables of a bucket list (one thread per bucket)
@@ -594,12 +598,14 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     __shared__ uint32_t s_start[RADIX + 1];
     __shared__ uint8_t s_hd[TILE + 1];
     __shared__ uint32_t s_any;
+    __shared__ uint64_t s_mask[SM::kWaves * RADIX];  // ranking masks (zero between uses)
     uint64_t *s_k = reinterpret_cast<uint64_t *>(s_raw);
     uint32_t *s_v = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t idx = blockIdx.x;
     if (idx >= count) return;
+    for (int i = tid; i < SM::kWaves * RADIX; i += T) s_mask[i] = 0;
     uint2 e = list[idx];
     uint64_t key[I];
     uint32_t val[I];
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         // items of this wave holding elements (wave-uniform)
         const int wbase = wave * (I * 64);
         const int live = (int)len > wbase ? min(I, ((int)len - wbase + 63) >> 6) : 0;
-        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live);
+        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live, s_mask);
 
         // 2. final position and head flag of every element
         uint32_t out[I];
@@ -702,13 +708,11 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 // counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
 // in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
 // -- the ranks are stable.  About 12 VALU per item instead of about 50.
-constexpr int kWaveItems = 4;
-
+template <int I>
 __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
                                                       uint32_t *__restrict__ ctr) {
-    constexpr int I = kWaveItems;
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
     __shared__ uint32_t s_v[CAP + 1];
@@ -916,6 +920,12 @@ static unsigned cu_count(gk_ctx *c) {
     return (unsigned)(cus / 8 * 8);
 }
 
+static const char *kLocName[kLocal][2] = {{"loc0a", "loc0b"}, {"loc1a", "loc1b"}, {"loc2a", "loc2b"},
+                                          {"loc3a", "loc3b"}};
+static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_r"},
+                                           {"msd_local_wave8", "msd_local_wave8_r"},
+                                           {"msd_local_wave16", "msd_local_wave16_r"},
+                                           {"msd_local_block16", "msd_local_block16_r"}};
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
 
@@ -930,33 +940,56 @@ struct MsdDriver {
     unsigned cus, pgrid;
     int slot = -1, total_slot = -1;
     uint32_t *ctr = nullptr, h[kCtrN] = {0};
-    unsigned long long *sums = nullptr, hs[4] = {0};
+    unsigned long long *sums = nullptr, hs[kLists] = {0};
     uint32_t *big_start[2], *big_len[2];
     uint32_t *dn_start, *dn_len;
     uint8_t *dn_par;
-    uint2 *blk[2], *wav[2];
+    uint2 *loc[kLocal][2];
+    int wsched[kMaxLevels];  // digit bits of global level l (L0: 7..8 for 2-bit keys, else 8; l >= 1: 6..8)
+    int width(int level) const { return wsched[std::min(level, kMaxLevels - 1)]; }
     uint8_t *heads = nullptr;
     uint8_t *nd = nullptr;  // next-level digit per element of the last pass's output
     bool nd_ready = false;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
-    uint64_t nblk = 0, nwav = 0, ndone = 0, big_elems = 0, blk_elems = 0, wav_elems = 0;
+    uint64_t nloc[kLocal] = {0}, loc_elems[kLocal] = {0}, ndone = 0, big_elems = 0;
     uint32_t nbig = 0;
     int cur_big = 0;
 
     MsdDriver(gk_ctx *c_, const KeySpec &ks_) : c(c_), ks(ks_), B(ks_.total_bits) {
         cus = cu_count(c);
         pgrid = cus * 4;  // 4 workgroups per CU, one resident at a time (LDS); measured faster than 1
+        set_widths(std::getenv("GKM_LEVEL_BITS"));
+    }
+
+    // level digit widths "w0,w1,w2,..." (the last one repeats).  Default 7,8,8,...: for 2-bit
+    // keys a 7-bit L0 is ~10% faster than an 8-bit one (longer runs per tile), and after 23 bits
+    // the C3 buckets (~370) fit the one-wave finishing kernel; 4-bit keys keep an 8-bit L0.
+    void set_widths(const char *spec) {
+        for (int l = 0; l < kMaxLevels; ++l) wsched[l] = kGR;
+        if (ks.bits == 2) wsched[0] = 7;
+        if (!spec) return;
+        int l = 0, w = kGR;
+        for (const char *p = spec; *p && l < kMaxLevels;) {
+            w = std::min(8, std::max(6, std::atoi(p)));
+            wsched[l++] = w;
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+        for (; l < kMaxLevels; ++l) wsched[l] = w;
+        if (ks.bits != 2) wsched[0] = kGR;
+        wsched[0] = std::max(wsched[0], 7);
     }
 
     Lists lists(int g, int bigsel) {
-        return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par, blk[g], wav[g]};
+        return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par,
+                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g]}};
     }
 
     int init(uint64_t n_) {
         n = n_;
         GK_TRY_HIP(c, msd_tables());
         GK_TRY_HIP(c, scratch(c, "msd_ctr", kCtrN, &ctr));
-        GK_TRY_HIP(c, scratch(c, "msd_sums", 4, &sums));
+        GK_TRY_HIP(c, scratch(c, "msd_sums", kLists, &sums));
         GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
         const uint64_t max_big = n / kBlockMax + 2;
         GK_TRY_HIP(c, scratch(c, "big_start0", max_big, &big_start[0]));
@@ -966,29 +999,36 @@ struct MsdDriver {
         GK_TRY_HIP(c, grow_keep(c, "dn_start", 1024, 0, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", 1024, 0, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", 1024, 0, &dn_par));
-        GK_TRY_HIP(c, grow_keep(c, "blk0", 1024, 0, &blk[0]));
-        GK_TRY_HIP(c, grow_keep(c, "wav0", 1024, 0, &wav[0]));
+        for (int k = 0; k < kLocal; ++k) GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], 1024, 0, &loc[k][0]));
         GK_TRY_HIP(c, scratch(c, "msd_heads", n + 64, &heads));
         return GK_OK;
     }
 
     int read_ctr() {
-        GK_TRY_HIP(c, hipMemcpyAsync(h, ctr, 4 * 4, hipMemcpyDeviceToHost, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(hs, sums, 8 * 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(h, ctr, 4 * kLists, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(hs, sums, 8 * kLists, hipMemcpyDeviceToHost, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         return GK_OK;
     }
 
     // scan per-tile histograms of nseg buckets (C chunks) into per-tile offsets + sub-bucket tables
-    int scan_offsets(uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start,
+    template <int RADIX>
+    void scan_launch(uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start,
+                     uint64_t nseg) {
+        hipLaunchKernelGGL(chunk_sum_kernel<RADIX>, dim3((unsigned)C), dim3(RADIX), 0, c->stream, tile_hist, c_first,
+                           c_ntiles, chunk_hist);
+        hipLaunchKernelGGL(seg_scan_kernel<RADIX>, dim3((unsigned)nseg), dim3(RADIX), 0, c->stream, chunk_hist,
+                           s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
+        hipLaunchKernelGGL(tile_apply_kernel<RADIX>, dim3((unsigned)C), dim3(RADIX), 0, c->stream, tile_hist,
+                           c_first, c_ntiles, chunk_hist);
+    }
+
+    int scan_offsets(int R, uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start,
                      uint64_t nseg) {
         timer_begin(c, "msd_scan", &slot);
-        hipLaunchKernelGGL(chunk_sum_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist,
-                           c_first, c_ntiles, chunk_hist);
-        hipLaunchKernelGGL(seg_scan_kernel<kGRadix>, dim3((unsigned)nseg), dim3(kGRadix), 0, c->stream, chunk_hist,
-                           s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
-        hipLaunchKernelGGL(tile_apply_kernel<kGRadix>, dim3((unsigned)C), dim3(kGRadix), 0, c->stream, tile_hist,
-                           c_first, c_ntiles, chunk_hist);
+        if (R == 8) scan_launch<256>(C, s_cfirst, s_nchunks, s_start, nseg);
+        else if (R == 7) scan_launch<128>(C, s_cfirst, s_nchunks, s_start, nseg);
+        else scan_launch<64>(C, s_cfirst, s_nchunks, s_start, nseg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         return GK_OK;
@@ -1029,9 +1069,13 @@ struct MsdDriver {
             GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         }
         const L0Args a{c->sba, lo, hi, ks.symbols, B};
-        const Dig d0 = dig_at(B, 0, kGR);
+        const int w0 = width(0);
+        const Dig d0 = dig_at(B, 0, w0);
         timer_begin(c, "msd_l0_count", &slot);
-        if (ks.bits == 2)
+        if (ks.bits == 2 && w0 == 7)
+            hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, 7>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
+                               d0, tile_hist);
+        else if (ks.bits == 2)
             hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
                                d0, tile_hist);
         else
@@ -1039,12 +1083,12 @@ struct MsdDriver {
                                d0, tile_hist);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        rc = scan_offsets(nc0, s_misc, s_misc + 1, s_misc + 2, 1);
+        rc = scan_offsets(w0, nc0, s_misc, s_misc + 1, s_misc + 2, 1);
         if (rc != GK_OK) return rc;
         // the bucket total = k-mers found (the last bucket's base + count)
         uint32_t last[2];
-        GK_TRY_HIP(c, hipMemcpyAsync(&last[0], seg_base + kGRadix - 1, 4, hipMemcpyDeviceToHost, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(&last[1], seg_cnt + kGRadix - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(&last[0], seg_base + (1 << w0) - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(&last[1], seg_cnt + (1 << w0) - 1, 4, hipMemcpyDeviceToHost, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         *count = (uint64_t)last[0] + last[1];
         if (*count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
@@ -1053,14 +1097,17 @@ struct MsdDriver {
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
         const bool with_nd = kout == c->keys[0];
-        NextDigits ndg{dig_at(B, kGR, kGR), nullptr};
+        NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
         if (with_nd) {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
         const unsigned g = pgrid;
         const uint32_t nt = (uint32_t)nt0;
-        if (ks.bits == 2 && with_nd)
+        if (ks.bits == 2 && with_nd && w0 == 7)
+            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, 7, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist, kout, vout, nt, *count, ndg);
+        else if (ks.bits == 2 && with_nd)
             hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
                                tile_hist, kout, vout, nt, *count, ndg);
         else if (ks.bits == 2)
@@ -1080,13 +1127,13 @@ struct MsdDriver {
 
     // route nsub sub-buckets (seg_base / seg_cnt) of a level; hi = key bits sorted after it
     int classify(uint64_t nsub, int hi, int parity, int bigsel) {
-        GK_TRY_HIP(c, grow_keep(c, "blk0", nblk + nsub, nblk, &blk[0]));
-        GK_TRY_HIP(c, grow_keep(c, "wav0", nwav + nsub, nwav, &wav[0]));
+        for (int k = 0; k < kLocal; ++k)
+            GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], nloc[k] + nsub, nloc[k], &loc[k][0]));
         GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nsub, ndone, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nsub, ndone, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nsub, ndone, &dn_par));
         GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
-        GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * 4, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * kLists, c->stream));
         timer_begin(c, "msd_classify", &slot);
         hipLaunchKernelGGL(classify_kernel, dim3((unsigned)((nsub + kClassT - 1) / kClassT)), dim3(kClassT), 0,
                            c->stream, seg_base, seg_cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums);
@@ -1094,40 +1141,59 @@ struct MsdDriver {
         timer_end(c, slot);
         int r = read_ctr();
         if (r != GK_OK) return r;
-        nblk = h[kCtrBlock];
-        nwav = h[kCtrWave];
+        for (int k = 0; k < kLocal; ++k) {
+            nloc[k] = h[kCtrLoc + k];
+            loc_elems[k] += hs[kCtrLoc + k];
+        }
         ndone = h[kCtrDone];
         nbig = h[kCtrBig];
         big_elems = hs[kCtrBig];
-        blk_elems += hs[kCtrBlock];
-        wav_elems += hs[kCtrWave];
         return GK_OK;
     }
 
-    // one global partition level over tiles already in t_start / t_count (T tiles, C chunks,
-    // nseg buckets), reading kin / vin, writing keys[out] / vals[out]
+    // one global partition level (R-bit digits below the top hi bits) over tiles already in
+    // t_start / t_count (T tiles, C chunks, nseg buckets), reading kin / vin, writing keys[out] /
+    // vals[out] and the next level's digit bytes
+    template <int R>
+    void level_launch(int hi, int nw, const uint32_t *t_start, const uint32_t *t_count, uint64_t T,
+                      const uint64_t *kin, const uint32_t *vin, int out, bool count) {
+        if (count) {
+            if (nd_ready)  // the previous pass wrote this level's digits
+                hipLaunchKernelGGL(msd_count_nd_kernel<R>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start,
+                                   t_count, nd, tile_hist);
+            else
+                hipLaunchKernelGGL(msd_count_kernel<R>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count,
+                                   dig_at(B, hi, R), kin, tile_hist);
+            return;
+        }
+        const NextDigits ndg{dig_at(B, hi + R, nw), nd};
+        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 0, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
+                           t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n,
+                           ndg);
+    }
+
+    void level_dispatch(int level, int hi, const uint32_t *t_start, const uint32_t *t_count, uint64_t T,
+                        const uint64_t *kin, const uint32_t *vin, int out, bool count) {
+        const int w = width(level), nw = width(level + 1);
+        if (w == 8) level_launch<8>(hi, nw, t_start, t_count, T, kin, vin, out, count);
+        else if (w == 7) level_launch<7>(hi, nw, t_start, t_count, T, kin, vin, out, count);
+        else level_launch<6>(hi, nw, t_start, t_count, T, kin, vin, out, count);
+    }
+
     int level_pass(int level, int hi, const uint32_t *t_start, const uint32_t *t_count, uint64_t T, uint64_t C,
                    const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start, uint64_t nseg,
                    const uint64_t *kin, const uint32_t *vin, int out) {
-        const Dig dl = dig_at(B, hi, kGR);
         timer_begin(c, nd_ready ? "msd_count_nd" : "msd_count", &slot);
         timer_units(c, slot, big_elems);
-        if (nd_ready)  // the previous pass wrote this level's digits
-            hipLaunchKernelGGL(msd_count_nd_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count,
-                               nd, tile_hist);
-        else
-            hipLaunchKernelGGL(msd_count_kernel<kGR>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count, dl,
-                               kin, tile_hist);
+        level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, true);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        int rc = scan_offsets(C, s_cfirst, s_nchunks, s_start, nseg);
+        int rc = scan_offsets(width(level), C, s_cfirst, s_nchunks, s_start, nseg);
         if (rc != GK_OK) return rc;
         timer_begin(c, kPassNames[level & 7], &slot);
         timer_units(c, slot, big_elems);
         GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
-        const NextDigits ndg{dig_at(B, hi + kGR, kGR), nd};
-        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, kGR, 0, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
-                           t_count, dl, tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n, ndg);
+        level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, false);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = true;
@@ -1188,14 +1254,14 @@ struct MsdDriver {
         rc = level_pass(1, kGR, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
         if (rc != GK_OK) return rc;
         cur_big = 0;
-        return classify(nseg * kGRadix, 2 * kGR, 0, cur_big);
+        return classify(nseg << width(1), kGR + width(1), 0, cur_big);
     }
 
-    // global levels while the next-level list is non-empty; `in` holds the current buffer
-    int levels(int level, int in) {
+    // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
+    // key bits are sorted
+    int levels(int level, int hi, int in) {
         while (nbig > 0) {
             const int out = in ^ 1;
-            const int hi = level * kGR;
             uint32_t *ntl, *nch, *tfirst, *cfirst;
             GK_TRY_HIP(c, scratch(c, "s_ntiles", nbig, &ntl));
             GK_TRY_HIP(c, scratch(c, "s_nchunks", nbig, &nch));
@@ -1219,9 +1285,10 @@ struct MsdDriver {
                             c->vals[in], out);
             if (rc != GK_OK) return rc;
             cur_big ^= 1;
-            rc = classify((uint64_t)nbig * kGRadix, hi + kGR, out, cur_big);
+            rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big);
             if (rc != GK_OK) return rc;
             ++level;
+            hi += width(level - 1);
             in = out;
         }
         return GK_OK;
@@ -1230,48 +1297,62 @@ struct MsdDriver {
     // local rounds (generation g lists -> re-listed sub-buckets in generation g ^ 1), done copies
     int finish() {
         const uint64_t max_spill = n / (kSmall + 1) + 1024;
-        GK_TRY_HIP(c, grow_keep(c, "blk0", std::max<uint64_t>(nblk, max_spill), nblk, &blk[0]));
-        GK_TRY_HIP(c, grow_keep(c, "wav0", std::max<uint64_t>(nwav, max_spill), nwav, &wav[0]));
-        GK_TRY_HIP(c, grow_keep(c, "blk1", max_spill, 0, &blk[1]));
-        GK_TRY_HIP(c, grow_keep(c, "wav1", max_spill, 0, &wav[1]));
+        uint64_t pending = 0;
+        for (int k = 0; k < kLocal; ++k) {
+            GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], std::max<uint64_t>(nloc[k], max_spill), nloc[k], &loc[k][0]));
+            GK_TRY_HIP(c, grow_keep(c, kLocName[k][1], max_spill, 0, &loc[k][1]));
+            pending += nloc[k];
+        }
         GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
         int g = 0, round = 0;
-        while (nblk + nwav > 0) {
+        while (pending > 0) {
             const int ng = g ^ 1;
             // the re-list counters of this round start from 0 (the done count carries on)
-            GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBlock, 0, 8, c->stream));
+            GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrLoc, 0, 4 * kLocal, c->stream));
             const Lists nl = lists(ng, 0);
-            if (nblk) {
-                timer_begin(c, round == 0 ? "msd_local_block" : "msd_local_block_r", &slot);
-                if (round == 0) timer_units(c, slot, blk_elems);
-                hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
-                                   dim3((unsigned)std::min<uint64_t>(nblk, cus * 8)), dim3(kBT), 0, c->stream, blk[g],
-                                   (uint32_t)nblk, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1], heads, nl, ctr);
-                GK_TRY_HIP(c, hipGetLastError());
-                timer_end(c, slot);
-            }
-            if (nwav) {
-                timer_begin(c, round == 0 ? "msd_local_wave" : "msd_local_wave_r", &slot);
-                if (round == 0) timer_units(c, slot, wav_elems);
-                static const bool old_wave = std::getenv("GKM_WAVE_STAGE") != nullptr;  // A/B experiments
-                if (old_wave)
-                    hipLaunchKernelGGL((msd_local_kernel<kWT, kWI, 8>),
-                                       dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(kWT), 0, c->stream,
-                                       wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1], c->vals[1],
-                                       heads, nl, ctr);
-                else
-                    hipLaunchKernelGGL(msd_wave_kernel, dim3((unsigned)std::min<uint64_t>(nwav, cus * 32)), dim3(64), 0,
-                                       c->stream, wav[g], (uint32_t)nwav, B, c->keys[0], c->vals[0], c->keys[1],
-                                       c->vals[1], heads, nl, ctr);
+            for (int k = 0; k < kLocal; ++k) {
+                if (!nloc[k]) continue;
+                timer_begin(c, round == 0 ? kLocTimer[k][0] : kLocTimer[k][1], &slot);
+                if (round == 0) timer_units(c, slot, loc_elems[k]);
+                const uint32_t cnt = (uint32_t)nloc[k];
+                uint64_t *k0 = c->keys[0], *k1 = c->keys[1];
+                uint32_t *v0 = c->vals[0], *v1 = c->vals[1];
+                const uint2 *lst = loc[k][g];
+                switch (k) {
+                case 0:
+                    hipLaunchKernelGGL(msd_wave_kernel<4>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
+                                       0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+                    break;
+                case 1:
+                    hipLaunchKernelGGL(msd_wave_kernel<8>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
+                                       0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+                    break;
+                case 2:
+                    if (std::getenv("GKM_LOC2_BLOCK"))  // A/B experiment
+                        hipLaunchKernelGGL((msd_local_kernel<kBT, 4, kBR>),
+                                           dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(kBT), 0, c->stream,
+                                           lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+                    else
+                        hipLaunchKernelGGL(msd_wave_kernel<16>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
+                                           dim3(64), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+                    break;
+                default:
+                    hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
+                                       dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(kBT), 0, c->stream, lst,
+                                       cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+                }
                 GK_TRY_HIP(c, hipGetLastError());
                 timer_end(c, slot);
             }
             int rc = read_ctr();
             if (rc != GK_OK) return rc;
-            nblk = h[kCtrBlock];
-            nwav = h[kCtrWave];
+            pending = 0;
+            for (int k = 0; k < kLocal; ++k) {
+                nloc[k] = h[kCtrLoc + k];
+                pending += nloc[k];
+            }
             ndone = h[kCtrDone];
             g = ng;
             if (++round > 64) return fail(c, GK_E_HIP, "msd local rounds did not converge");
@@ -1298,9 +1379,9 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     rc = d.run_l0(0, c->sba_len, c->keys[0], c->vals[0], c->elem_cap + 64, &found);
     if (rc != GK_OK) return rc;
     if (found != c->n) return fail(c, GK_E_HIP, "msd: k-mer count differs from the enumeration");
-    rc = d.classify(kGRadix, kGR, 0, 0);
+    rc = d.classify(1u << d.width(0), d.width(0), 0, 0);
     if (rc != GK_OK) return rc;
-    rc = d.levels(1, 0);
+    rc = d.levels(1, d.width(0), 0);
     if (rc != GK_OK) return rc;
     rc = d.finish();
     timer_end(c, d.total_slot);
@@ -1311,6 +1392,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,
                         uint64_t cap, uint64_t *hist, uint64_t *count) {
     MsdDriver d(c, ks);
+    d.wsched[0] = kGR;  // the exchange splits by kGR-bit buckets (msd_radix_bits)
     GK_TRY_HIP(c, msd_tables());
     int rc = d.run_l0(lo, hi, kout, vout, cap, count);
     if (rc != GK_OK) return rc;
@@ -1325,12 +1407,13 @@ int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, 
 int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint32_t *vin, const uint64_t *poff,
                    const uint64_t *plen, const uint32_t *pbucket, uint32_t np) {
     MsdDriver d(c, ks);
+    d.wsched[0] = kGR;  // pieces are kGR-bit buckets
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
     rc = d.first_level_from_pieces(kin, vin, poff, plen, pbucket, np);
     if (rc != GK_OK) return rc;
-    rc = d.levels(2, 0);
+    rc = d.levels(2, kGR + d.width(1), 0);
     if (rc != GK_OK) return rc;
     rc = d.finish();
     timer_end(c, d.total_slot);

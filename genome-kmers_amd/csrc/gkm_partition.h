@@ -20,6 +20,8 @@ __device__ __forceinline__ void lds_barrier() {
 
 // s_waitcnt immediate (gfx9 encoding) for vmcnt(0) with expcnt/lgkmcnt left at their maximum
 constexpr int kVmcnt0 = 0x0F70;
+// ... and for vmcnt(v), v < 64 (vmcnt bits [3:0] and [15:14])
+constexpr int vmcnt_imm(int v) { return kVmcnt0 | (v & 15) | ((v >> 4) << 14); }
 
 // A digit is `w` bits of a B-bit key below its top `hi` bits (the bits already sorted).
 struct Dig {
@@ -83,6 +85,41 @@ __device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool 
     }
 }
 
+// The same ranking with LDS masks instead of ballots (msd_wave_kernel's scheme): per item, each
+// valid lane ORs its bit into s_mask_wave[digit], reads the mask back (its peers) and zeroes it;
+// the first peer adds the item's count to the counter with a returning atomic and broadcasts the
+// old value.  s_mask_wave (RADIX u64) must be zero on entry and is zero on exit.
+template <int I, int R>
+__device__ __forceinline__ void rank_items_mask(const uint32_t (&dig)[I], const bool (&valid)[I],
+                                                uint32_t *s_wc_wave, uint64_t *s_mask_wave, uint32_t (&rank)[I],
+                                                int live = I) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long me_bit = 1ull << lane;
+    uint64_t peers[I];
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+        peers[i] = 0;
+        if (i >= live) continue;  // wave-uniform
+        if (valid[i]) atomicOr((unsigned long long *)&s_mask_wave[dig[i]], me_bit);
+        peers[i] = s_mask_wave[dig[i]];
+        s_mask_wave[dig[i]] = 0;  // all lanes of the digit, after the wave's read
+    }
+    uint32_t old[I], rin[I];
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+        old[i] = 0;
+        rin[i] = lanes_below(peers[i]);
+        if (i < live && valid[i] && rin[i] == 0) old[i] = atomicAdd(&s_wc_wave[dig[i]], (uint32_t)__popcll(peers[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+        rank[i] = 0;
+        if (i >= live) continue;
+        const int leader = valid[i] ? __ffsll((unsigned long long)peers[i]) - 1 : lane;
+        rank[i] = __shfl(old[i], leader) + rin[i];
+    }
+}
+
 template <int T, int I, int R>
 struct PartSmem {
     static constexpr int kTile = T * I;
@@ -105,6 +142,7 @@ struct PartSmem {
 // s_start[RADIX + 1] receives the tile-local digit starts (s_start[RADIX] = item count) and
 // slot[] each item's staging slot (invalid items: the sink slot kTile); s_toff may be null.
 // live (wave-uniform): items >= live of this wave hold no valid element and are skipped.
+// s_mask (optional, kWaves * RADIX u64, zero): rank with LDS masks instead of ballots.
 // PROF (timing builds of tools/radix_bench only): thread 0 adds the clock ticks of each phase to
 // prof[0..3] (rank, scan, slots, staging).
 template <int T, int I, int R, bool PROF = false>
@@ -112,7 +150,7 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
                                                 const bool (&valid)[I], Dig d, unsigned char *s_raw,
                                                 uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_start,
                                                 uint32_t (&slot)[I], unsigned long long *prof = nullptr,
-                                                int live = I) {
+                                                int live = I, uint64_t *s_mask = nullptr) {
     using SM = PartSmem<T, I, R>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -133,7 +171,10 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     uint32_t dig[I], rank[I];
 #pragma unroll
     for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
-    rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank, live);
+    if (s_mask)  // LDS-mask ranking (per-wave masks of RADIX u64)
+        rank_items_mask<I, R>(dig, valid, s_wc + wave * RADIX, s_mask + wave * RADIX, rank, live);
+    else
+        rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank, live);
     lds_barrier();
     mark(0);
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits

@@ -375,11 +375,15 @@ int main(int argc, char **argv) {
     run_scatter<49152>(b, st);
     run_scatter<98304>(b, st);
     MsdTables m;
-    run_msd<1024, 12, 0>(b, m, "msd pass T1024 I12", st, ref_sum, 1024);
     run_pipe<1024, 11, 8, 0>(b, m, "pipe T1024 I11 R8 grid 1024", st, ref_sum, 1024);
+    run_pipe<1024, 11, 8, 1>(b, m, "pipe T1024 I11 R8 no-store", st, ref_sum, 1024);
+    run_pipe<512, 11, 8, 0>(b, m, "pipe T512 I11 R8 grid 1024", st, ref_sum, 1024);
+    run_pipe<512, 11, 8, 0>(b, m, "pipe T512 I11 R8 grid 2048", st, ref_sum, 2048);
+    run_pipe<512, 11, 8, 1>(b, m, "pipe T512 I11 R8 no-store g2048", st, ref_sum, 2048);
+    run_pipe<256, 11, 8, 0>(b, m, "pipe T256 I11 R8 grid 4096", st, ref_sum, 4096);
+    run_pipe<256, 22, 8, 0>(b, m, "pipe T256 I22 R8 grid 2048", st, ref_sum, 2048);
+    run_pipe<512, 22, 8, 0>(b, m, "pipe T512 I22 R8 grid 1024", st, ref_sum, 1024);
     run_pipe<1024, 11, 7, 0>(b, m, "pipe T1024 I11 R7 grid 1024", st, ref_sum, 1024);
-    run_pipe<1024, 11, 7, 1>(b, m, "pipe T1024 I11 R7 no-store", st, ref_sum, 1024);
-    run_pipe<1024, 8, 7, 0>(b, m, "pipe T1024 I8 R7 grid 1024", st, ref_sum, 1024);
     run_pipe<512, 11, 7, 0>(b, m, "pipe T512 I11 R7 grid 2048", st, ref_sum, 2048);
     if (argc > 2) return 0;
     const int R = 4;

@@ -193,6 +193,28 @@ def test_homopolymer_genome_all_ties():
     oracle_check(seqs, 21, 21)
 
 
+# MSD depth: inputs whose buckets stay above the local limit (4096) for several global levels
+# (the random cases above finish after L0 / L1), at every level digit width (GKM_LEVEL_BITS)
+@pytest.mark.parametrize("level_bits", ["8", "8,7", "8,6", "8,7,8", "7,8,8"])
+def test_low_entropy_deep_levels_vs_oracle(level_bits, monkeypatch):
+    monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    rng = np.random.default_rng(11)
+    # 1 bit per base: L0 leaves 16 buckets of ~150K, L1 ~10K each, L2 below the local limit
+    oracle_check(random_genome(rng, [1_600_000, 800_000], alphabet=b"AC"), 31, 31)
+
+
+@pytest.mark.parametrize("level_bits", ["8", "8,7,8", "7,8,8"])
+def test_sparse_variation_all_levels_vs_oracle(level_bits, monkeypatch):
+    monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    rng = np.random.default_rng(12)
+    # mostly 'A' with a random base every ~40: huge equal-prefix buckets down to the last key bit,
+    # exhausted (all-equal) buckets far above the local limit, long runs of ties
+    s = np.full(600_000, ord("A"), dtype=np.uint8)
+    at = rng.integers(0, len(s), len(s) // 40)
+    s[at] = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, len(at))]
+    oracle_check([("a", s[:450_000].tobytes().decode()), ("b", s[450_000:].tobytes().decode())], 31, 31)
+
+
 def test_iupac_k31_vs_oracle():
     rng = np.random.default_rng(4)
     oracle_check(random_genome(rng, [120_000, 60_000], alphabet=b"ACGTACGTACGTNRY"), 31, 31)

@@ -398,6 +398,16 @@ static int presort_by_start(gk_ctx *c) {
     return radix_sort(c, 1, 32, false);
 }
 
+int gkm::ensure_keys(gk_ctx *c) {
+    if (!c->keys_valid || !c->keys_stale) return GK_OK;
+    int slot;
+    timer_begin(c, "reencode_keys", &slot);
+    GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
+    timer_end(c, slot);
+    c->keys_stale = false;
+    return GK_OK;
+}
+
 static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     int rc = ensure_elems(c, c->n, ks.words);
     if (rc != GK_OK) return rc;
@@ -408,6 +418,7 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         if (rc != GK_OK) return rc;
         c->spec = ks;
         c->keys_valid = true;
+        c->keys_stale = true;  // the MSD sort keeps the start order, not the keys
         c->keys_are_ranks = false;
         return GK_OK;
     }
@@ -430,6 +441,7 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     if (rc != GK_OK) return rc;
     c->spec = ks;
     c->keys_valid = true;
+    c->keys_stale = false;
     c->keys_are_ranks = false;
     return GK_OK;
 }
@@ -534,6 +546,7 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     }
     c->spec = KeySpec{0, 0, 0, (int)m, 1, 64};
     c->keys_valid = true;
+    c->keys_stale = false;
     c->keys_are_ranks = true;
     return GK_OK;
 }
@@ -624,6 +637,7 @@ extern "C" int gk_key_layout(gk_ctx *c, uint32_t *words, uint32_t *bits, uint32_
 extern "C" int gk_copy_keys(gk_ctx *c, uint64_t *dst, uint64_t n_words) {
     if (!c) return GK_E_ARG;
     if (!c->keys_valid) return fail(c, GK_E_STATE, "no encoded keys: sort first");
+    if (int rc = ensure_keys(c)) return rc;
     const uint64_t W = (uint64_t)c->spec.words;
     if (n_words != W * c->n) return fail(c, GK_E_ARG, "n_words differs from words_per_key * n");
     if (!n_words) return GK_OK;
@@ -652,6 +666,8 @@ extern "C" int gk_set_filter_mask(gk_ctx *c, const uint8_t *mask, uint64_t n) {
 extern "C" int gk_device_views(gk_ctx *c, void **starts, void **keys, uint64_t *n, uint32_t *words) {
     if (!c) return GK_E_ARG;
     if (int rc = materialize_starts(c)) return rc;
+    if (keys && c->keys_valid)
+        if (int rc = ensure_keys(c)) return rc;
     if (starts) *starts = c->vals[c->cur];
     if (keys) *keys = c->keys[c->cur];
     if (n) *n = c->n;
@@ -764,6 +780,7 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     }
     c->spec = ks;
     c->keys_valid = true;
+    c->keys_stale = n > 0;  // the MSD sort keeps the start order, not the keys
     c->keys_are_ranks = false;
     c->sorted = true;
     c->sort_len = k;

@@ -503,6 +503,8 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
             for (int w = 0; w < ks.words; ++w) km.m[w] = ~0ull;
             use_keys = true;
         }
+        if (use_keys)
+            if (int rc = ensure_keys(c)) return rc;
         int slot;
         timer_begin(c, "group_heads", &slot);
         const uint64_t *keys = c->keys[c->cur];

@@ -81,6 +81,7 @@ struct gk_ctx {
     bool sorted = false;
     uint32_t sort_len = 0;     // max_kmer_len of the last sort (0 = None)
     bool keys_valid = false;   // keys[cur] encode the k-mers of vals[cur] (sort order)
+    bool keys_stale = false;   // ... once re-encoded from vals[cur]: the MSD sort does not keep them (ensure_keys)
     bool keys_are_ranks = false;
     gkm::KeySpec spec{};
 
@@ -151,6 +152,8 @@ inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) 
     *out = static_cast<T *>(e.first);
     return r;
 }
+// re-encode keys[cur] from vals[cur] when the sort left them stale (gk_ctx::keys_stale)
+int ensure_keys(gk_ctx *c);
 // MSD sort of one-word keys from the enumerated positions (gkm_msd.hip)
 int msd_sort(gk_ctx *c, const KeySpec &ks);
 // multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the

@@ -36,6 +36,9 @@ constexpr int kBlockMax = kBT * kBI;    // 4096
 constexpr int kLocal = 4;
 constexpr int kWaveMax = 256;
 constexpr int kSmall = 24;
+// The local rounds write back the keys of a bucket only when some of its elements are re-listed
+// (rare): the sort's product is the start order (+ group heads), and keys are re-encoded from the
+// sorted starts when an API call needs them (gk_ctx::keys_stale).
 constexpr int kMaxLevels = 16;              // sub-buckets <= this: rank-by-count
 
 __constant__ uint8_t c_code4_msd[256];
@@ -670,7 +673,8 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         }
         if (any) s_any = 1;
         lds_barrier();  // also: every rank-by-count read is done before the staging is overwritten
-        if (s_any) {
+        const bool relist = s_any != 0;
+        if (relist) {
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const uint32_t dg = dg_of(key[i], dd);
@@ -683,7 +687,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
             if (i >= live) continue;
             s_k[out[i]] = key[i];
             s_v[out[i]] = val[i];
-            s_hd[out[i]] = hd[i] == 1;
+            s_hd[out[i]] = hd[i];  // 0 / 1: final (not) a group head; 2: re-listed
         }
         // the next bucket's loads fly while this one is written back
         local_load<T, I>(e, k0, v0, k1, v1, key, val);  // unconditional: static load count
@@ -693,9 +697,9 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = min((uint32_t)(i * T + tid), len - 1);
-            k0[st + p] = s_k[p];
+            if (relist) k0[st + p] = s_k[p];  // keys only for a bucket with re-listed elements
             v0[st + p] = s_v[p];
-            heads[st + p] = s_hd[p];
+            heads[st + p] = s_hd[p] & 1;
         }
         lds_barrier();  // the write-back has read LDS before the next bucket's staging
     }
@@ -836,7 +840,8 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
                 }
             }
         }
-        if (__ballot(any)) {  // re-list the large sub-buckets (rare)
+        const bool relist = __ballot(any) != 0;
+        if (relist) {  // re-list the large sub-buckets (rare)
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
@@ -849,15 +854,15 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
             if (i >= live) continue;
             s_k[out[i]] = key[i];
             s_v[out[i]] = val[i];
-            s_hd[out[i]] = hd[i] == 1;
+            s_hd[out[i]] = hd[i];  // 0 / 1: final (not) a group head; 2: re-listed
         }
         local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket's loads fly now
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = min((uint32_t)(i * 64 + lane), len - 1);
-            k0[st + p] = s_k[p];
+            if (relist) k0[st + p] = s_k[p];  // keys only for a bucket with re-listed elements
             v0[st + p] = s_v[p];
-            heads[st + p] = s_hd[p];
+            heads[st + p] = s_hd[p] & 1;
         }
     }
 }
@@ -866,18 +871,14 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
 // all keys equal, so the only head is the first element
 __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restrict__ dn_start,
                                                         const uint32_t *__restrict__ dn_len,
-                                                        const uint8_t *__restrict__ dn_par, const uint64_t *__restrict__ k1,
-                                                        const uint32_t *__restrict__ v1, uint64_t *__restrict__ k0,
+                                                        const uint8_t *__restrict__ dn_par, const uint32_t *__restrict__ v1,
                                                         uint32_t *__restrict__ v0, uint8_t *__restrict__ heads) {
     const uint32_t s = blockIdx.x;
     const uint64_t st = dn_start[s];
     const uint32_t len = dn_len[s];
     const bool copy = dn_par[s];
-    for (uint32_t i = threadIdx.x; i < len; i += 256) {
-        if (copy) {
-            k0[st + i] = k1[st + i];
-            v0[st + i] = v1[st + i];
-        }
+    for (uint32_t i = threadIdx.x; i < len; i += 256) {  // (keys are not kept: see kSmall)
+        if (copy) v0[st + i] = v1[st + i];
         heads[st + i] = i == 0;
     }
 }
@@ -949,7 +950,7 @@ struct MsdDriver {
     int width(int level) const { return wsched[std::min(level, kMaxLevels - 1)]; }
     uint8_t *heads = nullptr;
     uint8_t *nd = nullptr;  // next-level digit per element of the last pass's output
-    bool nd_ready = false;
+    bool nd_ready = false, nd_next = true;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
     uint64_t nloc[kLocal] = {0}, loc_elems[kLocal] = {0}, ndone = 0, big_elems = 0;
     uint32_t nbig = 0;
@@ -1167,9 +1168,14 @@ struct MsdDriver {
             return;
         }
         const NextDigits ndg{dig_at(B, hi + R, nw), nd};
-        hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 0, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
-                           t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out], (uint32_t)T, n,
-                           ndg);
+        if (nd_next)
+            hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 0, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
+                               t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
+                               (uint32_t)T, n, ndg);
+        else
+            hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 0, false>), dim3(pgrid), dim3(kPT), 0, c->stream,
+                               t_start, t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
+                               (uint32_t)T, n, ndg);
     }
 
     void level_dispatch(int level, int hi, const uint32_t *t_start, const uint32_t *t_count, uint64_t T,
@@ -1193,10 +1199,13 @@ struct MsdDriver {
         timer_begin(c, kPassNames[level & 7], &slot);
         timer_units(c, slot, big_elems);
         GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
+        // the next level's digit bytes, unless this level's sub-buckets will most likely all be
+        // local (mean under kBlockMax / 8); a next level then counts from the keys
+        nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax / 8;
         level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, false);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        nd_ready = true;
+        nd_ready = nd_next;
         return GK_OK;
     }
 
@@ -1359,7 +1368,7 @@ struct MsdDriver {
         }
         if (ndone > 0) {
             hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len,
-                               dn_par, c->keys[1], c->vals[1], c->keys[0], c->vals[0], heads);
+                               dn_par, c->vals[1], c->vals[0], heads);
             GK_TRY_HIP(c, hipGetLastError());
         }
         c->heads = heads;

@@ -436,11 +436,11 @@ template <int T, int I, int R, int MODE, bool ND>
 __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys, const uint32_t *s_vals,
                                            const uint32_t *toff, uint32_t cnt, uint64_t sink,
                                            uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                           NextDigits nd) {
+                                           NextDigits nd, uint32_t base = 0) {
     const uint32_t s = min((uint32_t)(threadIdx.x + g * T), cnt - 1);  // cnt == 0: stays in the tile
     const uint64_t k = s_keys[s];
     const uint32_t v = s_vals[s];
-    const uint64_t o = cnt ? (uint64_t)(toff[dg_of(k, d)] + s) : sink;
+    const uint64_t o = cnt ? (uint64_t)(toff[dg_of(k, d)] + base + s) : sink;
     if (MODE != 1 || o == 0xFFFFFFFFu) {
         kout[o] = k;
         vout[o] = v;
@@ -448,7 +448,7 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     }
 }
 
-template <int T, int I, int R = 8, int MODE = 0, bool ND = false>
+template <int T, int I, int R = 8, int MODE = 0, bool ND = false, int PRE_ = 0>
 __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict__ t_start,
                                                      const uint32_t *__restrict__ t_count, Dig dl,
                                                      const uint32_t *__restrict__ tile_off,
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
     using SM = PipeSmem<T, I>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
-    constexpr int PRE = (I + 2) / 3;  // store groups issued before the ranking starts
+    constexpr int PRE = PRE_ ? PRE_ : (I + 2) / 3;  // store groups issued before the ranking starts
     constexpr int RADIX = 1 << R;
     static_assert(T >= RADIX, "one thread per digit");
     __shared__ __attribute__((aligned(16))) unsigned char s_stage[SM::kStage];

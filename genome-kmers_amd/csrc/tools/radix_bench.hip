@@ -191,7 +191,7 @@ static void profile_msd(Bufs &b, MsdTables &m, hipStream_t st, unsigned grid) {
     CK(hipFree(prof));
 }
 
-template <int T, int I, int R, int MODE>
+template <int T, int I, int R, int MODE, int PRE = 0>
 static void run_pipe(Bufs &b, MsdTables &m, const char *name, hipStream_t st, unsigned long long ref_sum,
                      unsigned grid) {
     msd_tables_for(b, st, T * I, m, R);
@@ -202,7 +202,7 @@ static void run_pipe(Bufs &b, MsdTables &m, const char *name, hipStream_t st, un
     const int RR = 4;
     for (int r = 0; r <= RR; ++r) {
         CK(hipEventRecord(e0, st));
-        hipLaunchKernelGGL((msd_pipe_kernel<T, I, R, MODE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
+        hipLaunchKernelGGL((msd_pipe_kernel<T, I, R, MODE, false, PRE>), dim3(grid), dim3(T), 0, st, m.t_start, m.t_count,
                            Dig{62 - R, (1u << R) - 1}, m.tile_off, b.k[0], b.v[0], b.k[1], b.v[1], (uint32_t)m.tiles, b.n);
         CK(hipEventRecord(e1, st));
         CK(hipEventSynchronize(e1));
@@ -376,15 +376,7 @@ int main(int argc, char **argv) {
     run_scatter<98304>(b, st);
     MsdTables m;
     run_pipe<1024, 11, 8, 0>(b, m, "pipe T1024 I11 R8 grid 1024", st, ref_sum, 1024);
-    run_pipe<1024, 11, 8, 1>(b, m, "pipe T1024 I11 R8 no-store", st, ref_sum, 1024);
-    run_pipe<512, 11, 8, 0>(b, m, "pipe T512 I11 R8 grid 1024", st, ref_sum, 1024);
-    run_pipe<512, 11, 8, 0>(b, m, "pipe T512 I11 R8 grid 2048", st, ref_sum, 2048);
-    run_pipe<512, 11, 8, 1>(b, m, "pipe T512 I11 R8 no-store g2048", st, ref_sum, 2048);
-    run_pipe<256, 11, 8, 0>(b, m, "pipe T256 I11 R8 grid 4096", st, ref_sum, 4096);
-    run_pipe<256, 22, 8, 0>(b, m, "pipe T256 I22 R8 grid 2048", st, ref_sum, 2048);
-    run_pipe<512, 22, 8, 0>(b, m, "pipe T512 I22 R8 grid 1024", st, ref_sum, 1024);
     run_pipe<1024, 11, 7, 0>(b, m, "pipe T1024 I11 R7 grid 1024", st, ref_sum, 1024);
-    run_pipe<512, 11, 7, 0>(b, m, "pipe T512 I11 R7 grid 2048", st, ref_sum, 2048);
     if (argc > 2) return 0;
     const int R = 4;
     run_variant<256, 16, true>(b, "onesweep T256 I16 (current)", st, R, ref_sum);

@@ -34,7 +34,6 @@ constexpr int kBlockMax = kBT * kBI;    // 4096
 // local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
 // 4 or 16 keys (msd_local_kernel)
 constexpr int kLocal = 4;
-constexpr int kWaveMax = 256;
 constexpr int kSmall = 24;
 // The local rounds write back the keys of a bucket only when some of its elements are re-listed
 // (rare): the sort's product is the start order (+ group heads), and keys are re-encoded from the

@@ -20,6 +20,9 @@ GK_E_STATE = -6
 GK_E_FILTER = -7
 GK_E_LIMIT = -8
 GK_E_NO_BASES = -9
+GK_E_IO = -10
+GK_E_FASTA_NAME = -11
+GK_E_FASTA_LAYOUT = -12
 
 # gk_filter_kind
 FILTER_KEEP_ALL = 0
@@ -47,7 +50,7 @@ EXPORTED = (
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
     "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
-    "gk_shard_sort",
+    "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close",
 )
 
 
@@ -116,6 +119,9 @@ _SIGS = {
                             _U64P], ctypes.c_int),
     "gk_shard_sort": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, _U64P, _U64P, _U32P, ctypes.c_uint32],
                       ctypes.c_int),
+    "gk_fasta_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P), _U64P, _U64P, _U64P], ctypes.c_int),
+    "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
+    "gk_fasta_close": ([_P], None),
 }
 
 
@@ -136,6 +142,45 @@ def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
     _lib = lib
     return lib
+
+
+class FastaLayoutError(Exception):
+    """gk_fasta_fill found bytes that would not fill the sba exactly (the reference asserts)."""
+
+
+def read_fasta(path, n_threads: int = 0):
+    """FASTA -> (sba uint8, seg_starts uint32, names list[str], bad byte values) with libgkm's
+    multithreaded host parser (gk_fasta_open / gk_fasta_fill); the caller applies the reference's
+    checks.  The sba length is total_seq_len + num_records - 1, allocated exactly as
+    sequence_collection.py:531-533 does (so an empty file fails the same way)."""
+    lib = load_library()
+    with open(path, "rb"):  # the reference's open(): FileNotFoundError etc. with its messages
+        pass
+    h = _P()
+    nrec, total, nbytes = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib.gk_fasta_open(str(path).encode(), int(n_threads), ctypes.byref(h), ctypes.byref(nrec),
+                           ctypes.byref(total), ctypes.byref(nbytes))
+    if rc != GK_OK:
+        raise OSError(f"cannot map {path} (libgkm error {rc})")
+    try:
+        sba_len = int(total.value) + int(nrec.value) - 1
+        sba = np.zeros(sba_len, dtype=np.uint8)
+        seg_starts = np.zeros(int(nrec.value), dtype=np.uint32)
+        names = ctypes.create_string_buffer(max(int(nbytes.value), 1))
+        bad = np.zeros(256, dtype=np.uint8)
+        rc = lib.gk_fasta_fill(h, _ptr(sba, ctypes.c_uint8), sba_len, _ptr(seg_starts, ctypes.c_uint32), names,
+                               _ptr(bad, ctypes.c_uint8))
+    finally:
+        lib.gk_fasta_close(h)
+    if rc == GK_E_FASTA_NAME:
+        raise IndexError("list index out of range")  # line[1:].strip().split()[0] on an empty name
+    if rc == GK_E_FASTA_LAYOUT:
+        raise FastaLayoutError()
+    if rc != GK_OK:
+        raise GkError(rc, "gk_fasta_fill failed")
+    raw = names.raw[: int(nbytes.value)]
+    name_list = [b.decode("utf-8") for b in raw.split(b"\0")[:-1]] if nrec.value else []
+    return sba, seg_starts, name_list, set(np.flatnonzero(bad).tolist())
 
 
 def _ptr(arr: np.ndarray, ctype):

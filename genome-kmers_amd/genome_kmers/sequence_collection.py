@@ -186,40 +186,28 @@ class SequenceCollection:
             bad = set(np.unique(sba[~_ALLOWED_LUT[sba]]).tolist())
             raise ValueError(f"Sequence contains non-allowed characters! ({bad})")
 
-    def _load_forward_sba_from_fasta(self, fasta_file_path: Path, num_records: int, total_seq_len: int):
-        sba_len = total_seq_len + num_records - 1
-        seg_starts = np.zeros(num_records, dtype=np.uint32)
-        sba = np.zeros(sba_len, dtype=np.uint8)
-        names = []
-        at = 0
-        rec = -1
-        with open(fasta_file_path, "r") as fh:
-            for line in fh:
-                if line.startswith(">"):
-                    rec += 1
-                    if at != 0:
-                        sba[at] = DOLLAR
-                        at += 1
-                    seg_starts[rec] = at
-                    names.append(SequenceCollection._get_fasta_record_name(line))
-                else:
-                    chunk = np.frombuffer(line.strip().upper().encode("utf-8"), dtype=np.uint8)
-                    sba[at : at + chunk.size] = chunk
-                    at += chunk.size
-        if at != sba_len:
-            raise AssertionError("After parsing the fasta file, we expect sba to be full")
+    def _load_forward_sba_from_fasta(self, fasta_file_path: Path, num_records: int = None, total_seq_len: int = None):
+        """The reference's per-line loop (sequence_collection.py:517-576) as libgkm's multithreaded
+        host parser (gkm_fasta.cpp: memory-mapped, chunked at line starts, one scan + one parallel
+        fill); same bytes, then the reference's checks in its order."""
+        from genome_kmers import _native
+
+        try:
+            sba, seg_starts, names, bad = _native.read_fasta(fasta_file_path)
+        except _native.FastaLayoutError:
+            raise AssertionError("After parsing the fasta file, we expect sba to be full") from None
         if (np.diff(seg_starts.astype(np.int64)) < 2).any():
             raise ValueError(f"At least one empty sequence was found in the input file ({fasta_file_path})")
         SequenceCollection._verify_record_names_are_unique(names)
-        self._check_alphabet(sba)
+        if bad:
+            raise ValueError(f"Sequence contains non-allowed characters! ({bad})")
         return sba, seg_starts, names
 
     def _initialize_from_fasta(self, fasta_file_path: Path, strands_to_load: str) -> None:
         if strands_to_load not in ("forward", "reverse_complement", "both"):
             raise ValueError(f"strands_to_load not recognized ({strands_to_load})")
-        num_records, total = self._get_fasta_stats(fasta_file_path)
         self.forward_sba, self._forward_sba_seg_starts, self.forward_record_names = (
-            self._load_forward_sba_from_fasta(fasta_file_path, num_records, total)
+            self._load_forward_sba_from_fasta(fasta_file_path)
         )
         self._strands_loaded = "forward"
         self._finish_strands(strands_to_load)

@@ -20,6 +20,8 @@
  *   gk_copy_keys           encoded k-mers (no reference counterpart: the reference compares bytes)
  *   gk_shard_partition,    one GPU's share of Kmers.sort under torch.distributed (no reference
  *   gk_shard_sort          counterpart: the reference is single-process, kmers.py:1644-1648)
+ *   gk_fasta_open,         SequenceCollection._get_fasta_stats + _load_forward_sba_from_fasta
+ *   gk_fasta_fill          (sequence_collection.py:476-576): FASTA -> sba on the host, multithreaded
  *
  * Conventions: every function returns GK_OK (0) or a negative gk_status; gk_last_error(ctx)
  * describes the last failure.  Host pointers are borrowed for the duration of the call only.
@@ -38,6 +40,7 @@ extern "C" {
 #endif
 
 typedef struct gk_ctx gk_ctx;
+typedef struct gk_fasta gk_fasta;
 
 enum gk_status {
     GK_OK = 0,
@@ -50,6 +53,9 @@ enum gk_status {
     GK_E_FILTER = -7,       /* a built-in filter raised (see gk_filter_error)                */
     GK_E_LIMIT = -8,        /* more than 2^32-1 k-mers (kmers.py:805-808)                     */
     GK_E_NO_BASES = -9,     /* comparator found no valid base (kmers.py:368-369)             */
+    GK_E_IO = -10,          /* a file could not be opened / mapped                           */
+    GK_E_FASTA_NAME = -11,  /* a header line with no name token (IndexError in the reference) */
+    GK_E_FASTA_LAYOUT = -12,/* the sba would not be exactly full (sequence_collection.py:565)   */
 };
 
 /* built-in k-mer filters (kmers.py:14-259); evaluated on the device */
@@ -172,6 +178,22 @@ int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint64
 int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
                   const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
                   uint32_t npieces);
+
+/* ---- FASTA ingest (host; no context, no device) ------------------------------------------
+ * gk_fasta_open maps `path` and scans it once with n_threads threads (<= 0: up to 16): the
+ * number of records ('>' lines), the sequence bytes left after each line's strip(), and the bytes
+ * of the record names (each NUL-terminated) -- _get_fasta_stats (sequence_collection.py:476-515).
+ * The caller allocates sba[total_seq_len + num_records - 1], seg_starts[num_records] and
+ * names[names_bytes]; gk_fasta_fill writes them as _load_forward_sba_from_fasta does (:517-566):
+ * upper-cased bytes, '$' between records, segment starts, names in record order.  bad_bytes[256]
+ * (optional, zeroed by the caller) flags every sequence byte outside ACGTRYSWKMBDHVN$, for the
+ * reference's alphabet error (:571-574).  GK_E_FASTA_NAME: a header without a name;
+ * GK_E_FASTA_LAYOUT: the bytes do not fill sba exactly.  gk_fasta_close unmaps. */
+int gk_fasta_open(const char *path, int n_threads, gk_fasta **out, uint64_t *num_records, uint64_t *total_seq_len,
+                  uint64_t *names_bytes);
+int gk_fasta_fill(gk_fasta *f, uint8_t *sba, uint64_t sba_len, uint32_t *seg_starts, char *names,
+                  uint8_t *bad_bytes);
+void gk_fasta_close(gk_fasta *f);
 
 #ifdef __cplusplus
 }

@@ -625,6 +625,48 @@ extern "C" int gk_copy_start_range(gk_ctx *c, uint64_t offset, uint32_t *dst, ui
     return GK_OK;
 }
 
+// start index and segment of selected k-mers: starts[kmer_num[i]] and bisect_right(seg, start) - 1
+// (sequence_collection.py:76-97), one thread per k-mer, binary search over the resident seg_starts
+__global__ __launch_bounds__(256) void locate_kernel(const uint32_t *__restrict__ starts, uint64_t n,
+                                                     const uint32_t *__restrict__ seg, uint32_t nseg,
+                                                     const uint64_t *__restrict__ nums, uint64_t m,
+                                                     uint32_t *__restrict__ sba_idx, uint32_t *__restrict__ seg_of) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = nums[i];
+    const uint32_t s = k < n ? starts[k] : 0xFFFFFFFFu;
+    uint32_t lo = 0, hi = nseg;  // first segment start > s
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg[mid] <= s) lo = mid + 1;
+        else hi = mid;
+    }
+    sba_idx[i] = s;
+    seg_of[i] = lo - 1;  // nseg >= 1 and seg[0] == 0, so lo >= 1 for every valid start
+}
+
+extern "C" int gk_locate(gk_ctx *c, const uint64_t *kmer_nums, uint64_t m, uint32_t *sba_idx, uint32_t *seg) {
+    if (!c) return GK_E_ARG;
+    if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers");
+    if (m == 0) return GK_OK;
+    if (!kmer_nums || !sba_idx || !seg) return fail(c, GK_E_ARG, "null array");
+    if (int rc = materialize_starts(c)) return rc;
+    for (uint64_t i = 0; i < m; ++i)
+        if (kmer_nums[i] >= c->n) return fail(c, GK_E_ARG, "kmer_num out of range");
+    uint64_t *d_nums;
+    uint32_t *d_out;
+    GK_TRY_HIP(c, scratch(c, "locate_nums", m, &d_nums));
+    GK_TRY_HIP(c, scratch(c, "locate_out", 2 * m, &d_out));
+    GK_TRY_HIP(c, hipMemcpyAsync(d_nums, kmer_nums, 8 * m, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(locate_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, c->vals[c->cur], c->n,
+                       c->seg, (uint32_t)c->nseg, d_nums, m, d_out, d_out + m);
+    GK_TRY_HIP(c, hipGetLastError());
+    GK_TRY_HIP(c, hipMemcpyAsync(sba_idx, d_out, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipMemcpyAsync(seg, d_out + m, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
 extern "C" int gk_key_layout(gk_ctx *c, uint32_t *words, uint32_t *bits, uint32_t *symbols) {
     if (!c) return GK_E_ARG;
     if (!c->keys_valid) return fail(c, GK_E_STATE, "no encoded keys: sort first");

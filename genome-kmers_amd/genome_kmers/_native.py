@@ -50,7 +50,7 @@ EXPORTED = (
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
     "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
-    "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close",
+    "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate",
 )
 
 
@@ -122,6 +122,7 @@ _SIGS = {
     "gk_fasta_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P), _U64P, _U64P, _U64P], ctypes.c_int),
     "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
     "gk_fasta_close": ([_P], None),
+    "gk_locate": ([_P, _U64P, ctypes.c_uint64, _U32P, _U32P], ctypes.c_int),
 }
 
 
@@ -324,6 +325,17 @@ class Engine:
         self._check(self.lib.gk_copy_unique(self.ctx, _ptr(starts, ctypes.c_uint64), _ptr(counts, ctypes.c_uint32),
                                             g.value))
         return starts, counts
+
+    def locate(self, kmer_nums: np.ndarray):
+        """(start sba index, segment) of each kmer_num, on the device (gk_locate)."""
+        nums = np.ascontiguousarray(kmer_nums, dtype=np.uint64)
+        m = len(nums)
+        sba_idx = np.empty(m, dtype=np.uint32)
+        seg = np.empty(m, dtype=np.uint32)
+        if m:
+            self._check(self.lib.gk_locate(self.ctx, _ptr(nums, ctypes.c_uint64), m, _ptr(sba_idx, ctypes.c_uint32),
+                                           _ptr(seg, ctypes.c_uint32)))
+        return sba_idx, seg
 
     # ---- multi-GPU shards (genome_kmers.distributed) ------------------------------------------
     def shard_bucket_bits(self) -> int:

@@ -551,10 +551,46 @@ class Kmers:
             for t in zip(nums.tolist(), yielded.tolist(), totals.tolist()):
                 yield t
             return
-        info = self.generate_get_kmer_info_func(one_based_seq_index)
-        starts = self.kmer_sba_start_indices
-        for num, y, t in zip(nums.tolist(), yielded.tolist(), totals.tolist()):
-            yield info(num, starts, self.seq_coll.forward_sba, kmer_len, y, t)
+        yield from self._full_info(nums, yielded, totals, kmer_len, one_based_seq_index)
+
+    def _full_info(self, nums, yielded, totals, kmer_len, one_based):
+        """get_kmer_info (kmers.py:1180-1264) for every yielded k-mer at once: the starts and their
+        segments come from the device (gk_locate), the rest is vectorised here; a k-mer whose
+        kmer_len runs past its segment raises at its turn, as the reference's generator does."""
+        sc = self.seq_coll
+        sba_strand = sc._get_sba_strand_to_use(sc.strands_loaded())
+        sba, seg_starts, names = sc._strand_arrays(sba_strand)
+        strand_char = "+" if sba_strand == "forward" else "-"
+        sba_idx, seg = self._engine.locate(nums)
+        starts64 = seg_starts.astype(np.int64)
+        b = starts64[seg]
+        e = np.where(seg == len(seg_starts) - 1, len(sba) - 1, starts64[np.minimum(seg + 1, len(seg_starts) - 1)] - 2)
+        s64 = sba_idx.astype(np.int64)
+        seq_idx = (s64 - b if sba_strand == "forward" else e - s64) + (1 if one_based else 0)
+        klen = (e - s64 + 1) if kmer_len is None else np.full(len(s64), kmer_len, dtype=np.int64)
+        bad = (s64 > e) | ((s64 + klen - 1) > e)
+        first_bad = int(np.argmax(bad)) if bad.any() else len(s64)
+        names = tuple(names)
+        num_l, y_l, t_l, seg_l, seq_l, k_l = (nums.tolist(), yielded.tolist(), totals.tolist(), seg.tolist(),
+                                              seq_idx.tolist(), klen.tolist())
+        for i in range(first_bad):
+            yield (num_l[i], strand_char, names[seg_l[i]], seq_l[i], k_l[i], y_l[i], t_l[i])
+        if first_bad < len(s64):  # the reference's own checks and messages for that k-mer
+            info = self.generate_get_kmer_info_func(one_based)
+            i = first_bad
+            yield info(num_l[i], self._start_lookup(num_l[i]), sba, kmer_len, y_l[i], t_l[i])
+
+    def _start_lookup(self, kmer_num):
+        """A one-element start view for generate_get_kmer_info_func's checks."""
+
+        class _One:
+            def __len__(_self):
+                return int(self._engine.n)
+
+            def __getitem__(_self, k):
+                return int(self._engine.locate(np.array([k], dtype=np.uint64))[0][0])
+
+        return _One()
 
     def get_kmer_count(self, kmer_len: Union[int, None], kmer_filter_func: Callable = kmer_filter_keep_all,
                        min_group_size: int = 1, max_group_size: Union[int, None] = None) -> int:

@@ -18,6 +18,7 @@
  *                          (kmers.py:869-992)
  *   gk_unique_counts       the (unique k-mer, multiplicity) view of the sorted groups (kmers.py:597-625)
  *   gk_copy_keys           encoded k-mers (no reference counterpart: the reference compares bytes)
+ *   gk_locate              the start / record lookups behind get_kmer_info (kmers.py:1180-1264)
  *   gk_shard_partition,    one GPU's share of Kmers.sort under torch.distributed (no reference
  *   gk_shard_sort          counterpart: the reference is single-process, kmers.py:1644-1648)
  *   gk_fasta_open,         SequenceCollection._get_fasta_stats + _load_forward_sba_from_fasta
@@ -178,6 +179,12 @@ int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint64
 int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
                   const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
                   uint32_t npieces);
+
+/* Location of selected k-mers for Kmers.get_kmers(kmer_info_to_yield="full") (kmers.py:1180-1264):
+ * sba_idx[i] = kmer_sba_start_indices[kmer_nums[i]] and seg[i] = the segment holding it
+ * (bisect_right over the segment starts, sequence_collection.py:76-97), computed on the device
+ * against the resident starts -- the host never needs the whole start array. */
+int gk_locate(gk_ctx *ctx, const uint64_t *kmer_nums, uint64_t m, uint32_t *sba_idx, uint32_t *seg);
 
 /* ---- FASTA ingest (host; no context, no device) ------------------------------------------
  * gk_fasta_open maps `path` and scans it once with n_threads threads (<= 0: up to 16): the

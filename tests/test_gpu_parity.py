@@ -338,3 +338,49 @@ def test_large_single_contig_properties():
     assert int(counts.sum()) == n
     h, t = km.get_kmer_group_counts(31, max_counts_bin=8)
     assert t == n and int((h * np.arange(9))[:8].sum()) <= n
+
+
+# ---------------------------------------------------------------------------------------------
+# get_kmers(kmer_info_to_yield="full"): device gk_locate vs the per-k-mer reference path
+# ---------------------------------------------------------------------------------------------
+def _full_info_reference(km, kmer_len, one_based, **kw):
+    """kmers.py:1180-1264 element by element: the minimum info, then get_kmer_info per k-mer."""
+    info = km.generate_get_kmer_info_func(one_based)
+    starts = km.kmer_sba_start_indices
+    out = []
+    try:
+        for num, y, t in km.get_kmers(kmer_len, kmer_info_to_yield="minimum", **kw):
+            out.append(info(num, starts, km.seq_coll.forward_sba, kmer_len, y, t))
+    except ValueError as e:
+        out.append(("ValueError", str(e)))
+    return out
+
+
+def _full_info_device(km, kmer_len, one_based, **kw):
+    out = []
+    try:
+        for t in km.get_kmers(kmer_len, one_based_seq_index=one_based, kmer_info_to_yield="full", **kw):
+            out.append(t)
+    except ValueError as e:
+        out.append(("ValueError", str(e)))
+    return out
+
+
+@pytest.mark.parametrize("sort", [True, False])
+@pytest.mark.parametrize("kmer_len,one_based,kw", [
+    (8, False, {}), (8, True, {"min_group_size": 2}), (5, False, {"yield_first_n": 2}),
+    (None, False, {}), (12, True, {"max_group_size": 3}),
+])
+def test_full_info_matches_reference_path(sort, kmer_len, one_based, kw):
+    rng = np.random.default_rng(21)
+    seqs = random_genome(rng, [3000, 40, 1200, 9], alphabet=b"ACGT")
+    seqs = [(n, s[: len(s) // 3] + s[: len(s) // 3] + s[len(s) // 3:]) for n, s in seqs]  # planted repeats
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=8, max_kmer_len=None if kmer_len is None else 12)
+    if sort:
+        km.sort()
+    if not sort and kw:
+        pytest.skip("group-size arguments need a sorted Kmers")
+    want = _full_info_reference(km, kmer_len, one_based, **kw)
+    got = _full_info_device(km, kmer_len, one_based, **kw)
+    assert got == want

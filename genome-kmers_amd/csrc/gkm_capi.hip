@@ -305,7 +305,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     uint32_t h[2] = {0, 0};
     GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = false;
+    c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = c->canonical = false;
     c->n = 0;
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;
@@ -347,7 +347,7 @@ extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
     c->have_starts = true;
     c->enumerated = true;
     c->starts_materialized = false;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
     if (n_out) *n_out = n;
     return GK_OK;
 }
@@ -368,7 +368,7 @@ extern "C" int gk_set_start_indices(gk_ctx *c, const uint32_t *src, uint64_t n, 
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
     return GK_OK;
 }
 
@@ -411,9 +411,9 @@ int gkm::ensure_keys(gk_ctx *c) {
 static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     int rc = ensure_elems(c, c->n, ks.words);
     if (rc != GK_OK) return rc;
-    // fixed-length one-word keys from the enumerated starts: stable MSD (gkm_msd.hip)
+    // fixed-length keys (k <= 64) from the enumerated starts: stable MSD in one-word phases (gkm_msd.hip)
     static const bool force_lsd = std::getenv("GKM_SORT_LSD") != nullptr;
-    if (c->enumerated && ks.words == 1 && ks.symbols == ks.min_len && (ks.bits == 2 || ks.bits == 4) && !force_lsd) {
+    if (c->enumerated && ks.symbols == ks.min_len && ks.symbols <= 64 && (ks.bits == 2 || ks.bits == 4) && !force_lsd) {
         rc = msd_sort(c, ks);
         if (rc != GK_OK) return rc;
         c->spec = ks;
@@ -423,7 +423,14 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         return GK_OK;
     }
     bool hist_ready = false;
-    if (c->enumerated) {
+    if (c->enumerated && ks.canonical) {  // k > 64: canonical keys of the (ascending) starts
+        rc = materialize_starts(c);
+        if (rc != GK_OK) return rc;
+        int slot;
+        timer_begin(c, "encode", &slot);
+        GK_TRY_HIP(c, launch_encode_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur]));
+        timer_end(c, slot);
+    } else if (c->enumerated) {
         int slot;
         timer_begin(c, "encode", &slot);
         GK_TRY_HIP(c, launch_encode_positions(c, ks, c->keys[c->cur], c->vals[c->cur], c->hist));
@@ -552,11 +559,16 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
 }
 
 extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
-    (void)flags;
     if (!c) return GK_E_ARG;
+    if (flags & ~GK_SORT_CANONICAL) return fail(c, GK_E_ARG, "unknown gk_sort flags");
+    const bool canonical = (flags & GK_SORT_CANONICAL) != 0;
     if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (max_kmer_len != 0 && max_kmer_len < c->min_k) return fail(c, GK_E_ARG, "max_kmer_len is less than min_kmer_len");
+    if (canonical && max_kmer_len != c->min_k)
+        return fail(c, GK_E_ARG, "canonical k-mers need a fixed length (max_kmer_len == min_kmer_len)");
+    if (canonical && (c->acgt ? 2u : 4u) * max_kmer_len > 64u * kMaxWords)
+        return fail(c, GK_E_UNSUPPORTED, "canonical k-mers are limited to 256-bit keys");
     if (c->internal_dollar)
         return fail(c, GK_E_NO_BASES, "kmers compared were less than min_kmer_len: the sba holds a '$' inside a segment");
     if (!c->enumerated && c->n > 0) {
@@ -576,6 +588,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
         c->sorted = true;
         c->sort_len = max_kmer_len;
         c->keys_valid = false;
+        c->canonical = canonical;
         return GK_OK;
     }
     // direct key?
@@ -587,6 +600,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
         ks.min_len = (int)c->min_k;
         const bool bounded = max_kmer_len != c->min_k;
         ks.lenbits = (bounded && ks.bits == 2) ? bit_width(max_kmer_len) : 0;
+        ks.canonical = canonical ? 1 : 0;
         const uint64_t tb = (uint64_t)ks.bits * max_kmer_len + ks.lenbits;
         if (tb <= 64ull * kMaxWords) {
             ks.total_bits = (int)tb;
@@ -600,6 +614,25 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     c->sorted = true;
     c->enumerated = false;
     c->sort_len = max_kmer_len;
+    c->canonical = canonical;
+    return GK_OK;
+}
+
+extern "C" int gk_copy_strands(gk_ctx *c, uint8_t *dst, uint64_t n) {
+    if (!c) return GK_E_ARG;
+    if (!c->sorted || !c->canonical) return fail(c, GK_E_STATE, "strands need a canonical sort (GK_SORT_CANONICAL)");
+    if (n != c->n) return fail(c, GK_E_ARG, "n differs from the k-mer count");
+    if (n == 0) return GK_OK;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (int rc = materialize_starts(c)) return rc;
+    KeySpec ks{};
+    ks.bits = c->acgt ? 2 : 4;
+    ks.symbols = (int)c->sort_len;
+    uint8_t *d;
+    GK_TRY_HIP(c, scratch(c, "strands", n, &d));
+    GK_TRY_HIP(c, launch_canon_strands(c, ks, c->vals[c->cur], n, d));
+    GK_TRY_HIP(c, hipMemcpyAsync(dst, d, n, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     return GK_OK;
 }
 
@@ -769,14 +802,14 @@ extern "C" int gk_profile_report(gk_ctx *c, char *buf, uint64_t buflen) {
 // ---------------------------------------------------------------------------------------------
 static int shard_spec(gk_ctx *c, uint32_t k, KeySpec *ks) {
     const int bits = c->acgt ? 2 : 4;
-    if (k == 0 || (uint64_t)bits * k > 64) return fail(c, GK_E_ARG, "shard k-mers must fit one 64-bit key");
+    if (k == 0 || k > 64) return fail(c, GK_E_ARG, "shard k-mers must have 1 <= k <= 64");
     *ks = KeySpec{};
     ks->bits = bits;
     ks->symbols = (int)k;
     ks->min_len = (int)k;
     ks->lenbits = 0;
-    ks->words = 1;
     ks->total_bits = bits * (int)k;
+    ks->words = (ks->total_bits + 63) / 64;  // exchanged: the first word; the rest re-encoded from the sba
     return GK_OK;
 }
 
@@ -806,14 +839,14 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     if (rc != GK_OK) return rc;
     for (uint32_t i = 1; i < npieces; ++i)
         if (h_piece_bucket[i] < h_piece_bucket[i - 1]) return fail(c, GK_E_ARG, "pieces must be in bucket order");
-    rc = ensure_elems(c, std::max<uint64_t>(n, 1), 1);
+    rc = ensure_elems(c, std::max<uint64_t>(n, 1), ks.words);
     if (rc != GK_OK) return rc;
     c->n = n;
     c->min_k = k;
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
     if (n > 0) {
         rc = msd_shard_sort(c, ks, d_keys, d_starts, h_piece_off, h_piece_len, h_piece_bucket, npieces);
         if (rc != GK_OK) return rc;

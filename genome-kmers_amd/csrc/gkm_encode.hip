@@ -6,6 +6,7 @@
 //   alphabet    sequence_collection.py:441-458, 694-697  {A,C,G,T,R,Y,S,W,K,M,B,D,H,V,N,$}
 // The encoders turn the k-mer at a start into an integer whose unsigned order equals that byte
 // order: 2-bit codes when the sba is pure ACGT, 4-bit codes ('$' = 0) otherwise.
+#include "gkm_canon.h"
 #include "gkm_internal.h"
 
 namespace gkm {
@@ -37,10 +38,12 @@ static hipError_t init_tables() {
 }
 
 struct KS {  // POD copy of KeySpec for kernels
-    int bits, symbols, lenbits, min_len, words, total_bits, digits;
+    int bits, symbols, lenbits, min_len, words, total_bits, digits, canonical;
 };
 
-static KS pod(const KeySpec &k) { return KS{k.bits, k.symbols, k.lenbits, k.min_len, k.words, k.total_bits, k.digits()}; }
+static KS pod(const KeySpec &k) {
+    return KS{k.bits, k.symbols, k.lenbits, k.min_len, k.words, k.total_bits, k.digits(), k.canonical};
+}
 
 __device__ __forceinline__ uint32_t code2(uint32_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
 
@@ -368,10 +371,42 @@ __global__ __launch_bounds__(256) void encode_gather_kernel(const uint8_t *__res
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t *b = sba + starts[i];
         uint64_t w[W];
-        window_key<W, BITS, BOUNDED>(ks, [&](int k) { return (uint32_t)b[k]; }, s_lut4, w);
+        if (!BOUNDED && (BITS == 2 || BITS == 4) && ks.canonical) {  // fixed length: canonical strand
+            const bool rc = canon_is_rc<(BITS == 2 ? 2 : 4)>(b, ks.symbols, s_lut4);
+#pragma unroll
+            for (int k = 0; k < W; ++k) w[k] = 0;
+            for (int t = 0; t < ks.symbols; ++t)
+                bi_shl_or<W>(w, BITS, canon_sym<(BITS == 2 ? 2 : 4)>(b, ks.symbols, t, rc, s_lut4));
+        } else {
+            window_key<W, BITS, BOUNDED>(ks, [&](int k) { return (uint32_t)b[k]; }, s_lut4, w);
+        }
 #pragma unroll
         for (int k = 0; k < W; ++k) keys[(uint64_t)k * n + i] = w[k];
     }
+}
+
+template <int BITS>
+__global__ __launch_bounds__(256) void canon_strand_kernel(const uint8_t *__restrict__ sba, int k,
+                                                           const uint32_t *__restrict__ starts, uint64_t n,
+                                                           uint8_t *__restrict__ out) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = canon_is_rc<BITS>(sba + starts[i], k, s_lut4) ? 1 : 0;
+}
+
+hipError_t launch_canon_strands(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint8_t *out) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+    if (ks.bits == 2)
+        hipLaunchKernelGGL(canon_strand_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, ks.symbols, starts, n,
+                           out);
+    else
+        hipLaunchKernelGGL(canon_strand_kernel<4>, dim3(grid), dim3(256), 0, c->stream, c->sba, ks.symbols, starts, n,
+                           out);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -470,6 +470,10 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
         return GK_OK;
     }
 
+    // canonical k-mers have no prefixes: groups exist at the sort length only
+    if (is_sorted && c->canonical && (kmer_len < 0 || (uint64_t)kmer_len != c->sort_len))
+        return fail(c, GK_E_UNSUPPORTED, "canonical k-mers are grouped at kmer_len == the sort length only");
+
     // 3. heads
     const uint8_t *heads = c->flags;
     if (is_sorted && kind == GK_FILTER_KEEP_ALL && c->heads_valid && c->keys_valid && !c->keys_are_ranks &&

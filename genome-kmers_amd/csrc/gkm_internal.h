@@ -48,6 +48,7 @@ struct KeySpec {
     int min_len;      // validity: a start needs min_len bases before '$'
     int words;        // W
     int total_bits;
+    int canonical;    // 1: key of min(k-mer, reverse complement) (gkm_canon.h; fixed length only)
     int digits() const { return (total_bits + kRadixBits - 1) / kRadixBits; }
 };
 
@@ -80,6 +81,7 @@ struct gk_ctx {
     bool starts_materialized = true;  // false: enumerated starts not yet written to vals[cur]
     bool sorted = false;
     uint32_t sort_len = 0;     // max_kmer_len of the last sort (0 = None)
+    bool canonical = false;    // the last sort ordered canonical k-mers (GK_SORT_CANONICAL)
     bool keys_valid = false;   // keys[cur] encode the k-mers of vals[cur] (sort order)
     bool keys_stale = false;   // ... once re-encoded from vals[cur]: the MSD sort does not keep them (ensure_keys)
     bool keys_are_ranks = false;
@@ -175,6 +177,8 @@ hipError_t launch_enumerate(gk_ctx *c, uint32_t min_k, uint32_t *out);
 hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n, uint32_t min_k, uint32_t *d_bad);
 hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist);
 hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys);
+// strand of each canonical k-mer: 1 if its reverse complement is the smaller (the key), else 0
+hipError_t launch_canon_strands(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint8_t *out);
 
 // sort
 hipError_t launch_histogram(gk_ctx *c, const uint64_t *keys, uint64_t n, int words, int digits, uint32_t *hist);

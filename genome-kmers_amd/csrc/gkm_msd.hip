@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "gkm_canon.h"
 #include "gkm_internal.h"
 #include "gkm_partition.h"
 
@@ -68,7 +69,7 @@ struct L0Args {
 
 template <int BITS, int TILE>
 struct L0Pack {
-    static constexpr int kGroups = TILE / 32 + 2;             // 32-position groups packed
+    static constexpr int kGroups = TILE / 32 + 3;             // 32-position groups packed (k <= 64)
     static constexpr int kCodeWords = kGroups * BITS / 2 + 1;  // u64 words (+1 for the funnel)
 };
 
@@ -121,13 +122,29 @@ __device__ __forceinline__ uint64_t l0_key(const uint64_t *s_code, uint32_t p, i
     return x >> (64 - B);
 }
 
+// CANON: the first key word of the canonical k-mer (gkm_canon.h) is the smaller of the first word
+// of the k-mer and the first word of its reverse complement -- the reverse complement of the
+// k-mer's last B / BITS symbols.  (If the two are equal the whole-k-mer choice does not change the
+// first word; later words are decided in tie_encode_kernel.)
+template <int BITS, bool CANON>
+__device__ __forceinline__ uint64_t l0_key_of(const uint64_t *s_code, uint32_t p, int B, int k) {
+    const uint64_t f = l0_key<BITS>(s_code, p, B);
+    if (!CANON) return f;
+    const int n = B / BITS;
+    const uint64_t r = revcomp_word<BITS>(l0_key<BITS>(s_code, p + k - n, B), n);
+    return r < f ? r : f;
+}
+
 __device__ __forceinline__ bool l0_valid(const uint32_t *s_dol, uint32_t p, int S) {
     const uint32_t w = p >> 5, s = p & 31;
     const uint64_t x = (((uint64_t)s_dol[w] << 32) | s_dol[w + 1]) << s;
-    return (x >> (64 - S)) == 0;
+    if (S <= 32) return (x >> (64 - S)) == 0;
+    // multi-word keys (33 <= S <= 64): the first 32 positions, then the rest from p + 32
+    const uint64_t y = (((uint64_t)s_dol[w + 1] << 32) | s_dol[w + 2]) << s;
+    return (x >> 32) == 0 && (y >> (96 - S)) == 0;
 }
 
-template <int BITS, int T, int I, int R>
+template <int BITS, int T, int I, int R, bool CANON = false>
 __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_t *__restrict__ tile_hist) {
     constexpr int TILE = T * I;
     constexpr int RADIX = 1 << R;
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     for (int i = 0; i < I; ++i) {
         const uint32_t p = i * T + t;
         if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi)
-            atomicAdd(&s_hist[dg_of(l0_key<BITS>(s_code, p, a.total_bits), d0)], 1u);
+            atomicAdd(&s_hist[dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0)], 1u);
     }
     lds_barrier();
     for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
@@ -211,7 +228,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
 
 // software-pipelined L0 (see msd_pipe_kernel): the previous tile's stores overlap this tile's
 // packing, key extraction and ranking; the next tile's bytes are loaded after the staging
-template <int BITS, int T, int I, int R, bool ND>
+template <int BITS, int T, int I, int R, bool ND, bool CANON = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t ntiles, uint64_t sink, NextDigits nd) {
@@ -266,7 +283,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int i = 0; i < I; ++i) {
             const uint32_t p = p0 + i * 64;
             valid[i] = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi;
-            key[i] = l0_key<BITS>(s_code, p, a.total_bits);
+            key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
             val[i] = (uint32_t)(P0 + p);
         }
 #pragma unroll
@@ -475,7 +492,7 @@ constexpr int kClassT = 1024;
 __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__restrict__ seg_base,
                                                            const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
                                                            int B, int parity, Lists L, uint32_t *__restrict__ ctr,
-                                                           unsigned long long *__restrict__ sums) {
+                                                           unsigned long long *__restrict__ sums, uint32_t min_size) {
     constexpr int NW = kClassT / 64;
     __shared__ uint32_t s_cnt[kLists][NW];
     __shared__ uint32_t s_elems[kLists][NW];
@@ -483,7 +500,7 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kClassT + tid;
     const uint32_t size = i < nsub ? seg_cnt[i] : 0, st = i < nsub ? seg_base[i] : 0;
-    const int li = size >= 1 ? list_of(size, hi, B, true) : -1;
+    const int li = size >= min_size ? list_of(size, hi, B, true) : -1;
     bool f[kLists];
 #pragma unroll
     for (int l = 0; l < kLists; ++l) f[l] = li == l;
@@ -587,7 +604,7 @@ __device__ __forceinline__ void local_load(const uint2 e, const uint64_t *k0, co
     }
 }
 
-template <int T, int I, int R>
+template <int T, int I, int R, bool TIES>
 __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
@@ -637,38 +654,43 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live, s_mask);
 
         // 2. final position and head flag of every element
-        uint32_t out[I];
+        uint32_t out[I], tie_n[I];
         uint8_t hd[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             out[i] = slot[i];
             hd[i] = 0;
+            tie_n[i] = 0;
             if (i >= live) continue;  // wave-uniform
             const uint32_t dg = dg_of(key[i], dd);
             const uint32_t sb = s_start[dg], size = s_start[dg + 1] - sb;
             hd[i] = slot[i] == sb;  // singleton or equal keys: the first is the head
+            if (TIES && valid[i] && size > 1 && last && hd[i]) tie_n[i] = size;
             if (valid[i] && size > 1 && !last) {
                 if (size <= (uint32_t)kSmall) {
                     const uint32_t me = slot[i] - sb;
-                    uint32_t lt = 0, eq = 0;
+                    uint32_t lt = 0, eq = 0, eqall = 0;
                     for (uint32_t j = 0; j < size; ++j) {
                         const uint64_t kj = s_k[sb + j];
                         lt += kj < key[i];
                         eq += kj == key[i] && j < me;
+                        if (TIES) eqall += kj == key[i];
                     }
                     out[i] = sb + lt + eq;
                     hd[i] = eq == 0;
+                    if (TIES && eq == 0 && eqall > 1) tie_n[i] = eqall;
                 } else {
                     hd[i] = 2;  // not final: re-listed, head written by the next round
                 }
             }
         }
-        // re-list the large sub-buckets (rare): one entry each, from its first element
+        // re-list the large sub-buckets (rare): one entry each, from its first element.  TIES:
+        // every group of equal words (more words to compare) goes to the done list, from its head
         bool first[I], any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             first[i] = valid[i] && hd[i] == 2 && slot[i] == s_start[dg_of(key[i], dd)];
-            any |= first[i];
+            any |= first[i] || tie_n[i] > 0;
         }
         if (any) s_any = 1;
         lds_barrier();  // also: every rank-by-count read is done before the staging is overwritten
@@ -677,8 +699,9 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const uint32_t dg = dg_of(key[i], dd);
-                const uint32_t size = first[i] ? s_start[dg + 1] - s_start[dg] : 0;
-                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
+                const uint32_t size = first[i] ? s_start[dg + 1] - s_start[dg] : tie_n[i];
+                route((uint32_t)st + (first[i] ? slot[i] : out[i]), size, first[i] ? nhi : B, B, 0, false, L, ctr,
+                      lane);
             }
         }
 #pragma unroll
@@ -711,7 +734,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 // counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
 // in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
 // -- the ranks are stable.  About 12 VALU per item instead of about 50.
-template <int I>
+template <int I, bool TIES>
 __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
@@ -804,20 +827,22 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
         }
 
         // final position and head flag of every element (reads precede writes: one wave)
-        uint32_t out[I];
+        uint32_t out[I], tie_n[I];
         uint8_t hd[I];
         bool any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             out[i] = slot[i];
             hd[i] = 0;
+            tie_n[i] = 0;
             if (i >= live) continue;
             const uint32_t sb = s_cnt[dig[i]], size = s_cnt[dig[i] + 1] - sb;
             hd[i] = slot[i] == sb;
+            if (TIES && valid[i] && size > 1 && last && hd[i]) tie_n[i] = size;
             if (valid[i] && size > 1 && !last) {
                 if (size <= (uint32_t)kSmall) {
                     const uint32_t me = slot[i] - sb;
-                    uint32_t lt = 0, eq = 0;
+                    uint32_t lt = 0, eq = 0, eqall = 0;
                     // 4 keys per step (their LDS reads in flight together); indices past the
                     // sub-bucket are clamped and not counted
                     for (uint32_t j0 = 0; j0 < size; j0 += 4) {
@@ -829,23 +854,27 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
                             const uint32_t j = j0 + u;
                             lt += j < size && kj[u] < key[i];
                             eq += j < me && kj[u] == key[i];
+                            if (TIES) eqall += j < size && kj[u] == key[i];
                         }
                     }
                     out[i] = sb + lt + eq;
                     hd[i] = eq == 0;
+                    if (TIES && eq == 0 && eqall > 1) tie_n[i] = eqall;
                 } else {
                     hd[i] = 2;
                     any = true;
                 }
             }
         }
+#pragma unroll
+        for (int i = 0; i < I; ++i) any |= tie_n[i] > 0;
         const bool relist = __ballot(any) != 0;
-        if (relist) {  // re-list the large sub-buckets (rare)
+        if (relist) {  // re-list the large sub-buckets (rare); TIES: groups of equal words -> done
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
-                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : 0;
-                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
+                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : tie_n[i];
+                route((uint32_t)st + (first ? slot[i] : out[i]), size, first ? nhi : B, B, 0, false, L, ctr, lane);
             }
         }
 #pragma unroll
@@ -879,6 +908,33 @@ __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restri
     for (uint32_t i = threadIdx.x; i < len; i += 256) {  // (keys are not kept: see kSmall)
         if (copy) v0[st + i] = v1[st + i];
         heads[st + i] = i == 0;
+    }
+}
+
+// Multi-word keys: the next phase's key word of every element of a group of equal earlier words
+// (symbols [sym0, sym0 + nsym) of its k-mer, right-aligned).  One wave per group.
+template <int BITS>
+__global__ __launch_bounds__(256) void tie_encode_kernel(const uint8_t *__restrict__ sba,
+                                                         const uint32_t *__restrict__ g_start,
+                                                         const uint32_t *__restrict__ g_len, uint32_t ngroups,
+                                                         const uint32_t *__restrict__ vals, uint64_t *__restrict__ keys,
+                                                         int sym0, int nsym, int k, int canonical) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4_msd[threadIdx.x];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6); g < ngroups; g += nw) {
+        const uint64_t st = g_start[g];
+        const uint32_t len = g_len[g];
+        if (len < 2) continue;
+        for (uint32_t i = lane; i < len; i += 64) {
+            const uint8_t *b = sba + vals[st + i];
+            const bool rc = canonical && canon_is_rc<BITS>(b, k, s_lut4);
+            uint64_t key = 0;
+            for (int t = sym0; t < sym0 + nsym; ++t) key = (key << BITS) | canon_sym<BITS>(b, k, t, rc, s_lut4);
+            keys[st + i] = key;
+        }
     }
 }
 
@@ -1045,6 +1101,40 @@ struct MsdDriver {
         return GK_OK;
     }
 
+    // L0 kernels: count (per-tile digit histograms) or partition; bits x digit width x next digits
+    // x canonical
+    template <int BITS, int R, bool ND, bool CANON>
+    void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
+                   uint64_t sink, const NextDigits &ndg) {
+        if (count)
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kPI, R, CANON>), dim3(nt0), dim3(kPT), 0, c->stream, a, d0,
+                               tile_hist);
+        else
+            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kPT, kPI, R, ND, CANON>), dim3(pgrid), dim3(kPT), 0, c->stream,
+                               a, d0, tile_hist, kout, vout, nt, sink, ndg);
+    }
+
+    template <bool CANON>
+    void l0_dispatch_c(bool count, int w0, bool nd_, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout,
+                       uint32_t *vout, uint32_t nt, uint64_t sink, const NextDigits &ndg) {
+        if (ks.bits == 2 && w0 == 7) {
+            if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else l0_launch<2, 7, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+        } else if (ks.bits == 2) {
+            if (nd_) l0_launch<2, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else l0_launch<2, kGR, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+        } else {
+            if (nd_) l0_launch<4, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else l0_launch<4, kGR, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+        }
+    }
+
+    void l0_dispatch(bool count, int w0, bool nd_, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout,
+                     uint32_t *vout, uint32_t nt, uint64_t sink, const NextDigits &ndg) {
+        if (ks.canonical) l0_dispatch_c<true>(count, w0, nd_, a, d0, nt0, kout, vout, nt, sink, ndg);
+        else l0_dispatch_c<false>(count, w0, nd_, a, d0, nt0, kout, vout, nt, sink, ndg);
+    }
+
     // L0: encode the k-mers starting in [lo, hi) and partition them by the top kGR key bits into
     // kout / vout (capacity >= n + 1: element n is the scatter's sink).  seg_base / seg_cnt then
     // hold the kGRadix buckets.  *count: k-mers found (checked against cap before the scatter).
@@ -1072,15 +1162,7 @@ struct MsdDriver {
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
         timer_begin(c, "msd_l0_count", &slot);
-        if (ks.bits == 2 && w0 == 7)
-            hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, 7>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
-                               d0, tile_hist);
-        else if (ks.bits == 2)
-            hipLaunchKernelGGL((msd0_count_kernel<2, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
-                               d0, tile_hist);
-        else
-            hipLaunchKernelGGL((msd0_count_kernel<4, kPT, kPI, kGR>), dim3((unsigned)nt0), dim3(kPT), 0, c->stream, a,
-                               d0, tile_hist);
+        l0_dispatch(true, w0, false, a, d0, (unsigned)nt0, nullptr, nullptr, 0, 0, NextDigits{});
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         rc = scan_offsets(w0, nc0, s_misc, s_misc + 1, s_misc + 2, 1);
@@ -1102,31 +1184,19 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
-        const unsigned g = pgrid;
-        const uint32_t nt = (uint32_t)nt0;
-        if (ks.bits == 2 && with_nd && w0 == 7)
-            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, 7, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, nt, *count, ndg);
-        else if (ks.bits == 2 && with_nd)
-            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, nt, *count, ndg);
-        else if (ks.bits == 2)
-            hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kPI, kGR, false>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, nt, *count, ndg);
-        else if (with_nd)
-            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR, true>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, nt, *count, ndg);
-        else
-            hipLaunchKernelGGL((msd0_pipe_kernel<4, kPT, kPI, kGR, false>), dim3(g), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist, kout, vout, nt, *count, ndg);
+        l0_dispatch(false, w0, with_nd, a, d0, (unsigned)nt0, kout, vout, (uint32_t)nt0, *count, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = with_nd;
         return GK_OK;
     }
 
-    // route nsub sub-buckets (seg_base / seg_cnt) of a level; hi = key bits sorted after it
-    int classify(uint64_t nsub, int hi, int parity, int bigsel) {
+    // route nsub sub-buckets (seg_base / seg_cnt, or base / cnt) of a level; hi = key bits sorted
+    // after it; sub-buckets under min_size elements are dropped (final as they stand)
+    int classify(uint64_t nsub, int hi, int parity, int bigsel, const uint32_t *base = nullptr,
+                 const uint32_t *cnt = nullptr, uint32_t min_size = 1) {
+        if (!base) base = seg_base;
+        if (!cnt) cnt = seg_cnt;
         for (int k = 0; k < kLocal; ++k)
             GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], nloc[k] + nsub, nloc[k], &loc[k][0]));
         GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nsub, ndone, &dn_start));
@@ -1136,7 +1206,7 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * kLists, c->stream));
         timer_begin(c, "msd_classify", &slot);
         hipLaunchKernelGGL(classify_kernel, dim3((unsigned)((nsub + kClassT - 1) / kClassT)), dim3(kClassT), 0,
-                           c->stream, seg_base, seg_cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums);
+                           c->stream, base, cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums, min_size);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         int r = read_ctr();
@@ -1265,6 +1335,40 @@ struct MsdDriver {
         return classify(nseg << width(1), kGR + width(1), 0, cur_big);
     }
 
+    // Multi-word keys, phase > 0: the done list of the previous phase holds the groups of equal
+    // earlier words (in buffer 0); sort each group of >= 2 by the key word of symbols
+    // [sym0, sym0 + nsym).  more: further words follow (collect this phase's ties).
+    int next_phase(int sym0, int nsym, bool more) {
+        const uint64_t ng = ndone;
+        if (ng == 0) return GK_OK;
+        uint32_t *g_start, *g_len;
+        GK_TRY_HIP(c, scratch(c, "tie_start", ng, &g_start));
+        GK_TRY_HIP(c, scratch(c, "tie_len", ng, &g_len));
+        GK_TRY_HIP(c, hipMemcpyAsync(g_start, dn_start, 4 * ng, hipMemcpyDeviceToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(g_len, dn_len, 4 * ng, hipMemcpyDeviceToDevice, c->stream));
+        timer_begin(c, "msd_tie_encode", &slot);
+        const unsigned grid = (unsigned)std::min<uint64_t>((ng + 3) / 4, (uint64_t)cus * 16);
+        if (ks.bits == 2)
+            hipLaunchKernelGGL(tie_encode_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, g_start, g_len,
+                               (uint32_t)ng, c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
+        else
+            hipLaunchKernelGGL(tie_encode_kernel<4>, dim3(grid), dim3(256), 0, c->stream, c->sba, g_start, g_len,
+                               (uint32_t)ng, c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        B = ks.bits * nsym;
+        GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
+        ndone = 0;
+        nbig = 0;
+        for (int k = 0; k < kLocal; ++k) nloc[k] = loc_elems[k] = 0;
+        nd_ready = false;
+        int rc = classify(ng, 0, 0, cur_big, g_start, g_len, 2);
+        if (rc != GK_OK) return rc;
+        rc = levels(1, 0, 0);
+        if (rc != GK_OK) return rc;
+        return finish(more);
+    }
+
     // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
     // key bits are sorted
     int levels(int level, int hi, int in) {
@@ -1302,8 +1406,32 @@ struct MsdDriver {
         return GK_OK;
     }
 
-    // local rounds (generation g lists -> re-listed sub-buckets in generation g ^ 1), done copies
-    int finish() {
+    // one local class's kernel over a list of cnt buckets
+    template <bool TIES>
+    void local_launch(int k, uint32_t cnt, const uint2 *lst, uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                      const uint32_t *v1, const Lists &nl) {
+        switch (k) {
+        case 0:
+            hipLaunchKernelGGL((msd_wave_kernel<4, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            break;
+        case 1:
+            hipLaunchKernelGGL((msd_wave_kernel<8, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            break;
+        case 2:
+            hipLaunchKernelGGL((msd_wave_kernel<16, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            break;
+        default:
+            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
+                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+        }
+    }
+
+    // local rounds (generation g lists -> re-listed sub-buckets in generation g ^ 1), done copies.
+    // ties: more key words follow -- groups of equal words are collected in the done list
+    int finish(bool ties = false) {
         const uint64_t max_spill = n / (kSmall + 1) + 1024;
         uint64_t pending = 0;
         for (int k = 0; k < kLocal; ++k) {
@@ -1311,9 +1439,11 @@ struct MsdDriver {
             GK_TRY_HIP(c, grow_keep(c, kLocName[k][1], max_spill, 0, &loc[k][1]));
             pending += nloc[k];
         }
-        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
-        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
-        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
+        // ties: every group of >= 2 equal words may be listed as done
+        const uint64_t dn_spill = ties ? n / 2 + 1024 : max_spill;
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + dn_spill, ndone, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + dn_spill, ndone, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + dn_spill, ndone, &dn_par));
         int g = 0, round = 0;
         while (pending > 0) {
             const int ng = g ^ 1;
@@ -1328,29 +1458,8 @@ struct MsdDriver {
                 uint64_t *k0 = c->keys[0], *k1 = c->keys[1];
                 uint32_t *v0 = c->vals[0], *v1 = c->vals[1];
                 const uint2 *lst = loc[k][g];
-                switch (k) {
-                case 0:
-                    hipLaunchKernelGGL(msd_wave_kernel<4>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
-                                       0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
-                    break;
-                case 1:
-                    hipLaunchKernelGGL(msd_wave_kernel<8>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
-                                       0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
-                    break;
-                case 2:
-                    if (std::getenv("GKM_LOC2_BLOCK"))  // A/B experiment
-                        hipLaunchKernelGGL((msd_local_kernel<kBT, 4, kBR>),
-                                           dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(kBT), 0, c->stream,
-                                           lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
-                    else
-                        hipLaunchKernelGGL(msd_wave_kernel<16>, dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
-                                           dim3(64), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
-                    break;
-                default:
-                    hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
-                                       dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(kBT), 0, c->stream, lst,
-                                       cnt, B, k0, v0, k1, v1, heads, nl, ctr);
-                }
+                if (ties) local_launch<true>(k, cnt, lst, k0, v0, k1, v1, nl);
+                else local_launch<false>(k, cnt, lst, k0, v0, k1, v1, nl);
                 GK_TRY_HIP(c, hipGetLastError());
                 timer_end(c, slot);
             }
@@ -1377,9 +1486,14 @@ struct MsdDriver {
     }
 };
 
-// the enumerated k-mers of the whole sequence (gk_sort's fixed-length one-word path)
+// The enumerated k-mers of the whole sequence (gk_sort's fixed-length path, k <= 64).  Keys of
+// more than 64 bits are sorted in phases of one word (64 / bits symbols): phase 0 sorts every
+// k-mer by its first word, each later phase sorts the groups of equal earlier words by the next.
 int msd_sort(gk_ctx *c, const KeySpec &ks) {
+    const int spw = 64 / ks.bits;
+    const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
+    d.B = ks.bits * std::min(ks.symbols, spw);
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
@@ -1391,7 +1505,9 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     if (rc != GK_OK) return rc;
     rc = d.levels(1, d.width(0), 0);
     if (rc != GK_OK) return rc;
-    rc = d.finish();
+    rc = d.finish(nphase > 1);
+    for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
+        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw), ph + 1 < nphase);
     timer_end(c, d.total_slot);
     return rc;
 }
@@ -1400,6 +1516,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,
                         uint64_t cap, uint64_t *hist, uint64_t *count) {
     MsdDriver d(c, ks);
+    d.B = ks.bits * std::min(ks.symbols, 64 / ks.bits);  // the first key word (see msd_sort)
     d.wsched[0] = kGR;  // the exchange splits by kGR-bit buckets (msd_radix_bits)
     GK_TRY_HIP(c, msd_tables());
     int rc = d.run_l0(lo, hi, kout, vout, cap, count);
@@ -1414,7 +1531,10 @@ int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, 
 // multi-GPU receive side: sort n received k-mers (buckets as pieces) into keys[0] / vals[0]
 int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint32_t *vin, const uint64_t *poff,
                    const uint64_t *plen, const uint32_t *pbucket, uint32_t np) {
+    const int spw = 64 / ks.bits;
+    const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
+    d.B = ks.bits * std::min(ks.symbols, spw);
     d.wsched[0] = kGR;  // pieces are kGR-bit buckets
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
@@ -1423,7 +1543,9 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     if (rc != GK_OK) return rc;
     rc = d.levels(2, kGR + d.width(1), 0);
     if (rc != GK_OK) return rc;
-    rc = d.finish();
+    rc = d.finish(nphase > 1);
+    for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
+        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw), ph + 1 < nphase);
     timer_end(c, d.total_slot);
     return rc;
 }

@@ -50,8 +50,10 @@ EXPORTED = (
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
     "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
-    "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate",
+    "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
 )
+
+SORT_CANONICAL = 1  # GK_SORT_CANONICAL
 
 
 class GkFilter(ctypes.Structure):
@@ -123,6 +125,7 @@ _SIGS = {
     "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
     "gk_fasta_close": ([_P], None),
     "gk_locate": ([_P, _U64P, ctypes.c_uint64, _U32P, _U32P], ctypes.c_int),
+    "gk_copy_strands": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
 }
 
 
@@ -248,8 +251,14 @@ class Engine:
         self._check(self.lib.gk_set_start_indices(self.ctx, _ptr(arr, ctypes.c_uint32), arr.size, min_kmer_len))
         self.n = arr.size
 
-    def sort(self, max_kmer_len: int = None):
-        self._check(self.lib.gk_sort(self.ctx, 0 if max_kmer_len is None else int(max_kmer_len), 0))
+    def sort(self, max_kmer_len: int = None, canonical: bool = False):
+        flags = SORT_CANONICAL if canonical else 0
+        self._check(self.lib.gk_sort(self.ctx, 0 if max_kmer_len is None else int(max_kmer_len), flags))
+
+    def copy_strands(self) -> np.ndarray:
+        out = np.empty(self.n, dtype=np.uint8)
+        self._check(self.lib.gk_copy_strands(self.ctx, _ptr(out, ctypes.c_uint8), out.size))
+        return out
 
     def sync(self):
         self._check(self.lib.gk_sync(self.ctx))

@@ -381,6 +381,7 @@ class Kmers:
         self._is_initialized = False
         self._is_set = False
         self._is_sorted = False
+        self._canonical = False       # sorted by canonical k-mer (sort(canonical=True); no reference counterpart)
         self._engine = None
         self._host_starts = None      # host view of the start indices (or a user-assigned array)
         self._host_valid = True       # _host_starts matches the device order
@@ -470,6 +471,7 @@ class Kmers:
 
     @kmer_sba_start_indices.setter
     def kmer_sba_start_indices(self, value):
+        self._canonical = False
         self._host_starts = value
         self._host_valid = True
         self._device_stale = True
@@ -512,6 +514,11 @@ class Kmers:
                 "sequence_collection.strands_loaded() must be 'forward'"
             )
 
+    def _check_canonical_len(self, kmer_len):
+        if self._is_sorted and getattr(self, "_canonical", False) and kmer_len != self.max_kmer_len:
+            raise ValueError(f"canonical k-mers are grouped at kmer_len == {self.max_kmer_len} only "
+                             f"(kmer_len = {kmer_len})")
+
     def _check_unsorted_group_args(self, min_group_size, max_group_size, yield_first_n=None):
         if not self._is_sorted:
             if min_group_size != 1:
@@ -535,6 +542,7 @@ class Kmers:
         if kmer_len is not None and kmer_len < 1:
             raise ValueError(f"kmer_len ({kmer_len}) must be > 0")
         self._check_unsorted_group_args(min_group_size, max_group_size, yield_first_n)
+        self._check_canonical_len(kmer_len)
         if kmer_info_to_yield not in ("minimum", "full"):
             raise ValueError(f"kmer_info_to_yield ({kmer_info_to_yield}) not recognized")
         _check_group_args(min_group_size, max_group_size, yield_first_n)
@@ -599,6 +607,7 @@ class Kmers:
         if kmer_len is not None and kmer_len < 1:
             raise ValueError(f"kmer_len ({kmer_len}) must be > 0")
         self._check_unsorted_group_args(min_group_size, max_group_size)
+        self._check_canonical_len(kmer_len)
         _, total = self._group_hist(kmer_len, kmer_filter_func, min_group_size, max_group_size, 1000000)
         return total
 
@@ -610,6 +619,7 @@ class Kmers:
         if kmer_len is not None and kmer_len < 1:
             raise ValueError(f"kmer_len ({kmer_len}) must be > 0")
         self._check_unsorted_group_args(min_group_size, max_group_size)
+        self._check_canonical_len(kmer_len)
         if not self._is_sorted:
             raise AssertionError("The kmers must be sorted when calling get_kmer_group_counts")
         return self._group_hist(kmer_len, kmer_filter_func, min_group_size, max_group_size, max_counts_bin)
@@ -808,12 +818,22 @@ class Kmers:
         return bytes(self.seq_coll.forward_sba[start : start + kmer_len]).decode("utf-8")
 
     # ---- sort (kmers.py:1624-1731) -----------------------------------------------------------
-    def sort(self):
-        """Sort the start indices by k-mer on the GPU (in place from the caller's point of view)."""
+    def sort(self, *, canonical: bool = False):
+        """Sort the start indices by k-mer on the GPU (in place from the caller's point of view).
+
+        canonical=True (this build's extension; the reference has no canonical k-mers,
+        kmers.py:689-696): order by min(k-mer, reverse complement) with the reference's IUPAC
+        complement (sequence_collection.py:402-433).  Needs min_kmer_len == max_kmer_len; groups,
+        counts and encoded keys then refer to canonical k-mers (at kmer_len == max_kmer_len), and
+        get_canonical_strands() tells which strand each sorted k-mer's canonical form came from.
+        """
         self._check_forward()
+        if canonical and (self.max_kmer_len is None or self.max_kmer_len != self.min_kmer_len):
+            raise ValueError(f"canonical k-mers need min_kmer_len == max_kmer_len (min_kmer_len = "
+                             f"{self.min_kmer_len}, max_kmer_len = {self.max_kmer_len})")
         self._sync_device()
         try:
-            self._engine.sort(self.max_kmer_len)
+            self._engine.sort(self.max_kmer_len, canonical=canonical)
         except _native.GkError as e:
             if e.code == _native.GK_E_NO_BASES:
                 raise AssertionError(
@@ -823,6 +843,14 @@ class Kmers:
             raise
         self._after_device_reorder()
         self._is_sorted = True
+        self._canonical = canonical
+
+    def get_canonical_strands(self) -> np.ndarray:
+        """uint8 per sorted k-mer after sort(canonical=True): 1 if the canonical form is the k-mer's
+        reverse complement (strictly smaller), 0 if it is the k-mer itself (or a palindrome)."""
+        if not (self._is_sorted and self._canonical):
+            raise AssertionError("get_canonical_strands needs sort(canonical=True)")
+        return self._engine.copy_strands()
 
     def get_is_less_than_func(self, validate_kmers: bool = True, break_ties: bool = False) -> Callable:
         """Scalar is_less_than(a, b) of the reference (kmers.py:1654-1731), host-side, for callers

@@ -89,6 +89,11 @@ typedef struct gk_filter {
 
 /* gk_sort flags */
 #define GK_SORT_DEFAULT 0u
+/* Canonical k-mers (C5; this build's extension -- the reference defines none, kmers.py:689-696):
+ * sort by min(k-mer, reverse complement) under the reference's byte order, with the reference's
+ * IUPAC complement (sequence_collection.py:402-433).  Fixed length only (min_kmer_len ==
+ * max_kmer_len); groups, counts and keys then refer to the canonical k-mers. */
+#define GK_SORT_CANONICAL 1u
 
 /* ---- lifetime ------------------------------------------------------------------------------ */
 int gk_create(gk_ctx **out, int device);
@@ -121,6 +126,9 @@ int gk_copy_start_range(gk_ctx *ctx, uint64_t offset, uint32_t *dst, uint64_t co
 /* encoded keys of the sorted k-mers: words_per_key uint64 words per k-mer, most significant first */
 int gk_key_layout(gk_ctx *ctx, uint32_t *words_per_key, uint32_t *bits_per_symbol, uint32_t *symbols);
 int gk_copy_keys(gk_ctx *ctx, uint64_t *dst, uint64_t n_words);
+/* after a GK_SORT_CANONICAL sort: dst[i] = 1 if the reverse complement of sorted k-mer i is its
+ * canonical form (strictly smaller than the k-mer), else 0 (the k-mer itself, or a palindrome) */
+int gk_copy_strands(gk_ctx *ctx, uint8_t *dst, uint64_t n);
 
 /* ---- groups ---------------------------------------------------------------------------------- */
 /* mask for GK_FILTER_MASK: one byte per position of the current start-index order */

@@ -212,3 +212,67 @@ def encode_keys(sba, starts, bits, symbols, lenbits, words):
     if lenbits:
         lsw[:, 0] |= length
     return lsw[:, ::-1].copy()
+
+
+# ---------------------------------------------------------------------------------------------
+# canonical k-mers (C5) -- this build's extension: the reference defines no canonical k-mer
+# (kmers.py:689-696), so the ORDER below is parity-unpinned by the reference; the complement
+# mapping it uses is the reference's and is pinned by tests/golden/complement.npz.
+# ---------------------------------------------------------------------------------------------
+# SequenceCollection._get_complement_mapping_array (sequence_collection.py:402-433)
+COMPLEMENT_LUT = np.zeros(256, dtype=np.uint8)
+for _a, _b in zip(b"ACGTRYSWKMBDHVN$", b"TGCAYRSWMKVHDBN$"):
+    COMPLEMENT_LUT[_a] = _b
+
+
+def reverse_complement(sba):
+    """reverse_complement_sba(sba, lut) with inplace=False (sequence_collection.py:42-73)."""
+    return COMPLEMENT_LUT[np.asarray(sba, dtype=np.uint8)[::-1]]
+
+
+def canonical_windows(sba, starts, k):
+    """(canonical k-mer bytes (n, k), is_rc (n,)) of the fixed-length k-mers at starts: the
+    smaller of the k-mer and its reverse complement under the reference's byte order
+    (compare_sba_kmers_lexicographically, kmers.py:306-397; equal lengths, no '$' inside)."""
+    sba = np.asarray(sba, dtype=np.uint8)
+    starts = np.asarray(starts, dtype=np.int64)
+    win = sba[starts[:, None] + np.arange(k)[None, :]]
+    rc = COMPLEMENT_LUT[win[:, ::-1]]
+    diff = win != rc
+    first = diff.argmax(axis=1)
+    rows = np.arange(len(starts))
+    is_rc = diff.any(axis=1) & (rc[rows, first] < win[rows, first])
+    return np.where(is_rc[:, None], rc, win), is_rc
+
+
+def canonical_sort(sba, starts, k):
+    """Starts ordered by canonical k-mer, equal canonical k-mers by ascending start (the device's
+    break_ties order)."""
+    starts = np.asarray(starts, dtype=np.uint32)
+    canon, _ = canonical_windows(sba, starts, k)
+    order = np.lexsort([starts] + [canon[:, j] for j in range(k - 1, -1, -1)])
+    return starts[order]
+
+
+def canonical_group_hist(sba, sorted_starts, k, max_counts_bin=1000000):
+    """Group-size histogram + total of equal canonical k-mers over a canonical-sorted array, with
+    get_kmer_group_size_hist's binning (kmers.py:454-520: overflow into the last bin)."""
+    hist = np.zeros(max_counts_bin + 1, dtype=np.int64)
+    if len(sorted_starts) == 0:
+        return hist, 0
+    canon, _ = canonical_windows(sba, sorted_starts, k)
+    heads = np.concatenate([[True], (canon[1:] != canon[:-1]).any(axis=1)])
+    gs = np.flatnonzero(heads)
+    sizes = np.diff(np.append(gs, len(sorted_starts)))
+    np.add.at(hist, np.minimum(sizes, max_counts_bin), 1)
+    return hist, int(sizes.sum())
+
+
+def canonical_keys(sba, starts, k, bits):
+    """Encoded canonical keys (n, words), word 0 most significant (DESIGN.md §2 encoding of the
+    canonical bytes)."""
+    canon, _ = canonical_windows(sba, starts, k)
+    flat = np.concatenate([canon, np.full((len(canon), 1), DOLLAR, dtype=np.uint8)], axis=1).ravel()
+    rows = np.arange(len(canon), dtype=np.int64) * (k + 1)
+    words = (bits * k + 63) // 64
+    return encode_keys(flat, rows, bits, k, 0, words)

@@ -226,6 +226,34 @@ def test_k_sweep_vs_oracle(k):
     oracle_check(random_genome(rng, [40_000, 9_000, 128]), k, k)
 
 
+# Multi-word keys (2 bits x k > 64 or 4 bits x k > 64): the MSD sorts the first key word, then
+# each group of equal earlier words by the next word (gkm_msd.hip next_phase).  Planted repeats
+# make groups that tie on one and on every word.
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTACGTACGTNRY"])
+@pytest.mark.parametrize("k", [17, 33, 40, 63, 64])
+def test_multiword_repeats_vs_oracle(alphabet, k):
+    rng = np.random.default_rng(200 + k + len(alphabet))
+    rep = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), 3000).astype(np.uint8)
+    oracle_check(random_genome(rng, [60_000, 25_000, 300], alphabet=alphabet, repeat=rep, copies=6), k, k)
+
+
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTN"])
+def test_multiword_big_first_word_group(alphabet):
+    # 6000 contigs of one k-mer each that share their first 32 bases: a first-word group above the
+    # local limit (4096) goes through a global level of the second phase; a few exact duplicates
+    rng = np.random.default_rng(31)
+    pre = "A" * 32
+    tails = ["".join(rng.choice(list(alphabet.decode()), 31)) for _ in range(6000)]
+    tails += tails[:50]
+    oracle_check([(f"r{i}", pre + t) for i, t in enumerate(tails)], 63, 63)
+
+
+def test_multiword_homopolymer_all_words_tie():
+    seqs = [("a", "A" * 30_000), ("b", "C" * 64 + "A" * 9000), ("c", "ACGT" * 3000)]
+    oracle_check(seqs, 63, 63)
+    oracle_check(seqs, 40, 40)
+
+
 @pytest.mark.parametrize("min_k,max_k", [(1, 8), (5, 31), (10, 40), (3, 70)])
 def test_bounded_variable_length_vs_oracle(min_k, max_k):
     rng = np.random.default_rng(min_k * 7 + max_k)
@@ -384,3 +412,21 @@ def test_full_info_matches_reference_path(sort, kmer_len, one_based, kw):
     want = _full_info_reference(km, kmer_len, one_based, **kw)
     got = _full_info_device(km, kmer_len, one_based, **kw)
     assert got == want
+
+
+@pytest.mark.parametrize("k,alphabet", [(63, b"ACGT"), (31, b"ACGTN")])
+def test_multiword_runs_the_msd_phases(k, alphabet):
+    """Fixed-length multi-word keys are sorted by the MSD path (no LSD fallback): the profile
+    shows the L0 pass and the tie re-encode of the second phase."""
+    rng = np.random.default_rng(5)
+    rep = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), 2000).astype(np.uint8)
+    sc = SequenceCollection(sequence_list=random_genome(rng, [50_000], alphabet=alphabet, repeat=rep, copies=3))
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    eng = km._get_engine()
+    eng.profile_enable(True)
+    km.sort()
+    rep_ = eng.profile_report()
+    assert "msd_pass_l0" in str(rep_) and "msd_tie_encode" in str(rep_), rep_
+    want = oracle.quicksort(sc.forward_sba, oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k),
+                            k, k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)

@@ -125,3 +125,26 @@ def test_key_order_isomorphic_to_comparator(alphabet, is_acgt, min_k, max_k):
         c, _ = oracle.compare(sba, int(starts[i]), int(starts[j]), max_k)
         d = (as_int[i] > as_int[j]) - (as_int[i] < as_int[j])
         assert c == d, (int(starts[i]), int(starts[j]))
+
+
+def test_complement_mapping_pinned_to_reference():
+    """The canonical extension's complement = the reference's (tests/golden/make_complement.py)."""
+    z = load_case("complement")
+    np.testing.assert_array_equal(oracle.COMPLEMENT_LUT, z["complement_lut"])
+    np.testing.assert_array_equal(oracle.reverse_complement(z["sba"]), z["rc_sba"])
+    np.testing.assert_array_equal(oracle.reverse_complement(z["sba"]), z["both_sba"])
+
+
+def test_canonical_oracle_small_cases():
+    sba = np.frombuffer(b"ACGTTGCAAC$GGCC", dtype=np.uint8)
+    starts = np.array([0, 1, 2, 3, 4, 5, 6, 11], dtype=np.uint32)
+    canon, is_rc = oracle.canonical_windows(sba, starts, 4)
+    assert [bytes(c) for c in canon] == [b"ACGT", b"AACG", b"CAAC", b"GCAA", b"TGCA", b"GCAA", b"CAAC", b"GGCC"]
+    assert is_rc.tolist() == [False, True, True, True, False, False, False, False]
+    srt = oracle.canonical_sort(sba, starts, 4)
+    assert srt.tolist() == [1, 0, 2, 6, 3, 5, 11, 4]
+    hist, total = oracle.canonical_group_hist(sba, srt, 4, 5)
+    assert hist.tolist() == [0, 4, 2, 0, 0, 0] and total == 8
+    # canonical keys are the forward keys of the canonical bytes
+    keys = oracle.canonical_keys(sba, srt, 4, 2)
+    assert np.all(keys[1:, 0] >= keys[:-1, 0])

@@ -35,9 +35,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--genome-len", type=int, default=3_100_000_000)
-    ap.add_argument("--k", type=int, default=31)
-    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3",
+                    help="c3: the headline (3.1 Gb single contig, k=31); c4: GRCh38-shaped surrogate (24 "
+                         "contigs, ~5%% N, diverged repeats), k=31; c5: the same genome, k=63, canonical")
+    ap.add_argument("--genome-len", type=int, default=None, help="c3 genome length (default 3.1e9)")
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=16_000_000, help="k-mers in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
@@ -59,18 +62,68 @@ def make_genome(L: int, seed: int) -> np.ndarray:
     return out
 
 
+# GRCh38 primary assembly chromosome lengths, chr1..chr22, chrX, chrY (total 3,088,269,832 bp)
+GRCH38_LENGTHS = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636,
+                  138394717, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,
+                  83257441, 80373285, 58617616, 64444167, 46709983, 50818468, 156040895, 57227415]
+
+
+def make_grch38_surrogate(seed: int, lengths=GRCH38_LENGTHS):
+    """C4/C5 input without a FASTA: GRCh38's 24 contig lengths joined by '$',
+    uniform random ACGT, ~5 % N (runs at both contig ends and the centre), and repeat families with
+    realistic divergence so that k-mer groups of every size exist:
+      Alu-like  300 bp x 400,000 copies, 12 % substitutions;  L1-like 6 kb x 15,000 copies, 8 %;
+      segmental duplications 20 kb x 300 exact copies;  (CA)n microsatellites 40 bp x 50,000."""
+    rng = np.random.default_rng(seed)
+    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
+    L = sum(lengths) + len(lengths) - 1
+    sba = np.empty(L, dtype=np.uint8)
+    chunk = 1 << 28
+    for at in range(0, L, chunk):
+        m = min(chunk, L - at)
+        sba[at:at + m] = lut[rng.integers(0, 4, m, dtype=np.uint8)]
+
+    def plant(unit, copies, div):
+        at = rng.integers(0, L - len(unit), copies)
+        for a in range(0, copies, 20_000):
+            b = min(copies, a + 20_000)
+            rows = np.broadcast_to(unit, (b - a, len(unit))).copy()
+            mut = rng.random(rows.shape) < div
+            rows[mut] = lut[rng.integers(0, 4, int(mut.sum()), dtype=np.uint8)]
+            sba[at[a:b, None] + np.arange(len(unit))[None, :]] = rows
+
+    plant(lut[rng.integers(0, 4, 300)], 400_000, 0.12)
+    plant(lut[rng.integers(0, 4, 6000)], 15_000, 0.08)
+    for _ in range(300):
+        src, dst = rng.integers(0, L - 20_000, 2)
+        sba[dst:dst + 20_000] = sba[src:src + 20_000]
+    plant(np.frombuffer(b"CA" * 20, dtype=np.uint8), 50_000, 0.0)
+    starts = np.concatenate([[0], np.cumsum(np.asarray(lengths[:-1], dtype=np.int64) + 1)])
+    for s0, n in zip(starts, lengths):
+        e, c = int(n * 0.015), int(n * 0.02)
+        sba[s0:s0 + e] = ord("N")
+        sba[s0 + n - e:s0 + n] = ord("N")
+        sba[s0 + n // 2 - c // 2:s0 + n // 2 + c // 2] = ord("N")
+    sba[starts[1:] - 1] = ord("$")
+    return sba, starts.astype(np.uint32)
+
+
 def cpu_baseline(sba: np.ndarray, k: int, sample: int) -> dict:
     """Reference algorithm (Kmers.sort: numba quicksort + byte comparator with validation,
     kmers.py:1624-1731) restated in C (oracle/gk_oracle.c), 1 thread, on the first `sample` k-mers."""
     from oracle import oracle
 
-    sub = np.ascontiguousarray(sba[: sample + k - 1])
+    # a contig-free window of the genome (no '$' / N run inside), so every start is a k-mer
+    at = len(sba) // 3
+    sub = np.ascontiguousarray(sba[at: at + sample + k - 1])
+    if np.any(sub == 36):
+        at, sub = 0, np.ascontiguousarray(sba[: sample + k - 1])
     starts = np.arange(sample, dtype=np.uint32)
     t0 = time.perf_counter()
     oracle.quicksort(sub, starts, k, k)
     dt = time.perf_counter() - t0
     return {"value": sample / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample:,} {k}-mers of the same genome (single contig), numba-quicksort "
+            "sample": f"{sample:,} consecutive {k}-mers of the same genome, numba-quicksort "
                       f"restatement with validate_kmers, gcc -O3, 1 thread; {dt:.1f} s"}
 
 
@@ -104,9 +157,22 @@ def main():
 
     from genome_kmers import _native
 
-    k = args.k
-    L = args.genome_len
-    sba = make_genome(L, args.seed)
+    cfg = args.config
+    k = args.k or (63 if cfg == "c5" else 31)
+    canonical = cfg == "c5"
+    seed = args.seed if args.seed is not None else (42 if cfg == "c3" else 2)
+    if cfg == "c3":
+        L = args.genome_len or 3_100_000_000
+        sba, seg = make_genome(L, seed), np.zeros(1, dtype=np.uint32)
+        workload = f"C3: {L:,}-base synthetic single-contig genome, k={k} (min=max={k})"
+        data = f"synthetic: uniform random ACGT, numpy PCG64 seed {seed}"
+    else:
+        sba, seg = make_grch38_surrogate(seed)
+        L = len(sba)
+        workload = (f"{cfg.upper()}: GRCh38-shaped surrogate (24 contigs, {L:,} sba bytes), k={k}"
+                    + (", canonical" if canonical else ""))
+        data = (f"synthetic GRCh38 surrogate: contig lengths of GRCh38, random ACGT + ~5% N + diverged repeat "
+                f"families, numpy PCG64 seed {seed} (no FASTA on the box)")
 
     def barrier():
         if dist is not None:
@@ -116,19 +182,19 @@ def main():
     if world == 1 and not args.sharded:
         eng = _native.Engine(local)
         t0 = time.perf_counter()
-        eng.set_sequence(sba, np.zeros(1, dtype=np.uint32))
+        eng.set_sequence(sba, seg)
         eng.sync()
         h2d_ms = (time.perf_counter() - t0) * 1e3
-        n_units = L - k + 1
+        n_units = eng.enumerate(k)
 
         def step():
             eng.enumerate(k)
-            eng.sort(k)
+            eng.sort(k, canonical=canonical)
             return eng.unique_count_only()
     else:
         from genome_kmers import distributed
 
-        job = distributed.ShardedKmerSort(sba, np.zeros(1, dtype=np.uint32), k, rank, world, device=local)
+        job = distributed.ShardedKmerSort(sba, seg, k, rank, world, device=local, canonical=canonical)
         eng = job.engine
         h2d_ms = job.h2d_ms
         n_units = job.total_kmers
@@ -136,15 +202,21 @@ def main():
         def step():
             return job.run()
 
+    def log(msg):
+        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    log(f"{cfg}: {n_units:,} k-mers, sba on the device; warmup")
     n_unique = None
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         n_unique = step()
+        log(f"warmup step {i} done")
     barrier()
     eng.profile_enable(True)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         n_unique = step()
+        log(f"step {i} queued")
     eng.sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -215,8 +287,10 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u64",
-            "data": f"synthetic: uniform random ACGT, numpy PCG64 seed {args.seed}",
-            "config": {"workload": f"C3: {L:,}-base synthetic single-contig genome, k={k} (min=max={k})",
+            **({} if cfg == "c3" else {"metric": f"sorted {k}-mers/sec end-to-end on the GRCh38 surrogate"
+                                                 + (" (canonical)" if canonical else "")}),
+            "data": data,
+            "config": {"workload": workload,
                        "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
                        "parallelism": (f"position-range shards x{world} + 1 RCCL all-to-all" if dist is not None
                                        else "1 GPU"),

@@ -247,6 +247,8 @@ extern "C" void gk_destroy(gk_ctx *c) {
                     c->dhist, c->mask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
         if (b) hipFree(b);
+    for (auto &e : c->scratch)
+        if (e.second.first) hipFree(e.second.first);
     for (auto &t : c->timers) {
         hipEventDestroy(t.start);
         hipEventDestroy(t.stop);
@@ -400,20 +402,25 @@ static int presort_by_start(gk_ctx *c) {
 
 int gkm::ensure_keys(gk_ctx *c) {
     if (!c->keys_valid || !c->keys_stale) return GK_OK;
+    // the MSD sort runs on one key word; all words are allocated on first use
+    if (int rc = ensure_elems(c, c->n, c->spec.words)) return rc;
     int slot;
     timer_begin(c, "reencode_keys", &slot);
     GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
     timer_end(c, slot);
+    c->keys_valid = true;
     c->keys_stale = false;
     return GK_OK;
 }
 
 static int sort_direct(gk_ctx *c, const KeySpec &ks) {
-    int rc = ensure_elems(c, c->n, ks.words);
-    if (rc != GK_OK) return rc;
     // fixed-length keys (k <= 64) from the enumerated starts: stable MSD in one-word phases (gkm_msd.hip)
     static const bool force_lsd = std::getenv("GKM_SORT_LSD") != nullptr;
-    if (c->enumerated && ks.symbols == ks.min_len && ks.symbols <= 64 && (ks.bits == 2 || ks.bits == 4) && !force_lsd) {
+    const bool msd =
+        c->enumerated && ks.symbols == ks.min_len && ks.symbols <= 64 && (ks.bits == 2 || ks.bits == 4) && !force_lsd;
+    int rc = ensure_elems(c, c->n, msd ? 1 : ks.words);
+    if (rc != GK_OK) return rc;
+    if (msd) {
         rc = msd_sort(c, ks);
         if (rc != GK_OK) return rc;
         c->spec = ks;
@@ -800,7 +807,8 @@ extern "C" int gk_profile_report(gk_ctx *c, char *buf, uint64_t buflen) {
 // ---------------------------------------------------------------------------------------------
 // multi-GPU shards
 // ---------------------------------------------------------------------------------------------
-static int shard_spec(gk_ctx *c, uint32_t k, KeySpec *ks) {
+static int shard_spec(gk_ctx *c, uint32_t k, uint32_t flags, KeySpec *ks) {
+    if (flags & ~GK_SORT_CANONICAL) return fail(c, GK_E_ARG, "unknown shard flags");
     const int bits = c->acgt ? 2 : 4;
     if (k == 0 || k > 64) return fail(c, GK_E_ARG, "shard k-mers must have 1 <= k <= 64");
     *ks = KeySpec{};
@@ -810,12 +818,13 @@ static int shard_spec(gk_ctx *c, uint32_t k, KeySpec *ks) {
     ks->lenbits = 0;
     ks->total_bits = bits * (int)k;
     ks->words = (ks->total_bits + 63) / 64;  // exchanged: the first word; the rest re-encoded from the sba
+    ks->canonical = (flags & GK_SORT_CANONICAL) ? 1 : 0;
     return GK_OK;
 }
 
 extern "C" int gk_shard_bucket_bits(void) { return gkm::msd_radix_bits(); }
 
-extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint64_t *d_keys,
+extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *d_keys,
                                   uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out) {
     if (!c || !d_keys || !d_starts || !h_hist || !n_out) return GK_E_ARG;
     GK_TRY_HIP(c, hipSetDevice(c->device));
@@ -823,23 +832,23 @@ extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     if (hi > c->sba_len) hi = c->sba_len;
     if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
     KeySpec ks;
-    int rc = shard_spec(c, k, &ks);
+    int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
     return msd_shard_partition(c, ks, lo, std::max(hi, lo), d_keys, d_starts, cap, h_hist, n_out);
 }
 
 extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
-                             const uint64_t *h_piece_off, const uint64_t *h_piece_len,
+                             uint32_t flags, const uint64_t *h_piece_off, const uint64_t *h_piece_len,
                              const uint32_t *h_piece_bucket, uint32_t npieces) {
     if (!c || (n && (!d_keys || !d_starts || !h_piece_off || !h_piece_len || !h_piece_bucket))) return GK_E_ARG;
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (n > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
     KeySpec ks;
-    int rc = shard_spec(c, k, &ks);
+    int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
     for (uint32_t i = 1; i < npieces; ++i)
         if (h_piece_bucket[i] < h_piece_bucket[i - 1]) return fail(c, GK_E_ARG, "pieces must be in bucket order");
-    rc = ensure_elems(c, std::max<uint64_t>(n, 1), ks.words);
+    rc = ensure_elems(c, std::max<uint64_t>(n, 1), 1);
     if (rc != GK_OK) return rc;
     c->n = n;
     c->min_k = k;
@@ -859,5 +868,6 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     c->keys_are_ranks = false;
     c->sorted = true;
     c->sort_len = k;
+    c->canonical = ks.canonical != 0;
     return GK_OK;
 }

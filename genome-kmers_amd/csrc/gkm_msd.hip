@@ -17,6 +17,7 @@
 // exhausted is final as it stands.  Every global partition offset is known before its scatter
 // starts (count pass + column scan of per-tile digit histograms): no look-back chain.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "gkm_canon.h"
@@ -34,7 +35,8 @@ constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 k
 constexpr int kBlockMax = kBT * kBI;    // 4096
 // local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
 // 4 or 16 keys (msd_local_kernel)
-constexpr int kLocal = 4;
+constexpr int kLocal = 5;                // 4 = tiny (<= kTiny elements: one thread per bucket)
+constexpr int kTiny = 8;
 constexpr int kSmall = 24;
 // The local rounds write back the keys of a bucket only when some of its elements are re-listed
 // (rare): the sort's product is the start order (+ group heads), and keys are re-encoded from the
@@ -449,12 +451,15 @@ struct Lists {
 };
 
 // local class of a bucket of <= kBlockMax elements
-__host__ __device__ constexpr uint32_t local_cap(int cls) { return cls == 0 ? 256 : cls == 1 ? 512 : cls == 2 ? 1024 : 4096; }
+__host__ __device__ constexpr uint32_t local_cap(int cls) {
+    return cls == 0 ? 256 : cls == 1 ? 512 : cls == 2 ? 1024 : cls == 3 ? 4096 : kTiny;
+}
 
 // list of a live sub-bucket of `size` elements (kCtr* index)
 __device__ __forceinline__ int list_of(uint32_t size, int hi, int B, bool allow_big) {
     if (hi >= B) return kCtrDone;
     if (size > (uint32_t)kBlockMax && allow_big) return kCtrBig;
+    if (size <= (uint32_t)kTiny) return kCtrLoc + 4;
     return kCtrLoc + (size <= local_cap(0) ? 0 : size <= local_cap(1) ? 1 : size <= local_cap(2) ? 2 : 3);
 }
 
@@ -587,6 +592,25 @@ __global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restr
 // Output always goes to buffer 0; the bucket is read fully before any write, so in place is safe.
 // Loads and stores are branch-free with static counts (clamped to the bucket), so the next
 // bucket's loads -- issued once the current one is final in LDS -- overlap its stores.
+// Common-prefix skip: x_or = OR over a bucket's keys of (key ^ first key).  The bits of the key
+// below the hi sorted ones that are equal in every element need no partition pass: the bucket's
+// next digit starts at its highest differing bit.  All keys equal: one last digit (one sub-bucket,
+// final).  Repeats make such buckets common (a 30-copy repeat k-mer would otherwise take one round
+// per 8 bits).
+__device__ __forceinline__ int skip_hi(uint64_t x_or, int B, int hi) {
+    const int rem = B - hi;
+    if (rem <= 0) return hi;
+    x_or &= rem >= 64 ? ~0ull : ((1ull << rem) - 1);
+    if (x_or == 0) return max(hi, B - 8);
+    return B - 1 - (63 - __clzll(x_or));
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x |= __shfl_xor(x, off);
+    return x;
+}
+
 template <int T, int I>
 __device__ __forceinline__ void local_load(const uint2 e, const uint64_t *k0, const uint32_t *v0, const uint64_t *k1,
                                            const uint32_t *v1, uint64_t (&key)[I], uint32_t (&val)[I]) {
@@ -604,11 +628,11 @@ __device__ __forceinline__ void local_load(const uint2 e, const uint64_t *k0, co
     }
 }
 
-template <int T, int I, int R, bool TIES>
+template <int T, int I, int R>
 __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr) {
+                                                      uint32_t *__restrict__ ctr, int skip) {
     using SM = PartSmem<T, I, R>;
     constexpr int TILE = SM::kTile;
     constexpr int RADIX = SM::kRadix;
@@ -617,6 +641,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     __shared__ uint32_t s_start[RADIX + 1];
     __shared__ uint8_t s_hd[TILE + 1];
     __shared__ uint32_t s_any;
+    __shared__ uint64_t s_kf, s_or;                  // common-prefix skip: first key, OR of differences
     __shared__ uint64_t s_mask[SM::kWaves * RADIX];  // ranking masks (zero between uses)
     uint64_t *s_k = reinterpret_cast<uint64_t *>(s_raw);
     uint32_t *s_v = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
@@ -634,7 +659,22 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         const uint2 ce = e;
         const uint64_t st = ce.x;
         const uint32_t len = ce.y >> 8;
-        const int hi = (ce.y >> 1) & 127;
+        int hi = (ce.y >> 1) & 127;
+        if (skip) {
+            if (tid == 0) {
+                s_kf = key[0];
+                s_or = 0;
+            }
+            lds_barrier();
+            uint64_t x = 0;
+#pragma unroll
+            for (int i = 0; i < I; ++i)
+                if ((uint32_t)(wave * (I * 64) + i * 64 + lane) < len) x |= key[i] ^ s_kf;
+            x = wave_or64(x);
+            if (lane == 0 && x) atomicOr((unsigned long long *)&s_or, (unsigned long long)x);
+            lds_barrier();
+            hi = skip_hi(s_or, B, hi);
+        }
         const Dig dd = dig_at(B, hi, R);
         const int nhi = hi + R;      // key bits sorted within a sub-bucket
         const bool last = nhi >= B;  // sub-bucket keys are equal
@@ -654,43 +694,38 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live, s_mask);
 
         // 2. final position and head flag of every element
-        uint32_t out[I], tie_n[I];
+        uint32_t out[I];
         uint8_t hd[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             out[i] = slot[i];
             hd[i] = 0;
-            tie_n[i] = 0;
             if (i >= live) continue;  // wave-uniform
             const uint32_t dg = dg_of(key[i], dd);
             const uint32_t sb = s_start[dg], size = s_start[dg + 1] - sb;
             hd[i] = slot[i] == sb;  // singleton or equal keys: the first is the head
-            if (TIES && valid[i] && size > 1 && last && hd[i]) tie_n[i] = size;
             if (valid[i] && size > 1 && !last) {
                 if (size <= (uint32_t)kSmall) {
                     const uint32_t me = slot[i] - sb;
-                    uint32_t lt = 0, eq = 0, eqall = 0;
+                    uint32_t lt = 0, eq = 0;
                     for (uint32_t j = 0; j < size; ++j) {
                         const uint64_t kj = s_k[sb + j];
                         lt += kj < key[i];
                         eq += kj == key[i] && j < me;
-                        if (TIES) eqall += kj == key[i];
                     }
                     out[i] = sb + lt + eq;
                     hd[i] = eq == 0;
-                    if (TIES && eq == 0 && eqall > 1) tie_n[i] = eqall;
                 } else {
                     hd[i] = 2;  // not final: re-listed, head written by the next round
                 }
             }
         }
-        // re-list the large sub-buckets (rare): one entry each, from its first element.  TIES:
-        // every group of equal words (more words to compare) goes to the done list, from its head
+        // re-list the large sub-buckets (rare): one entry each, from its first element
         bool first[I], any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             first[i] = valid[i] && hd[i] == 2 && slot[i] == s_start[dg_of(key[i], dd)];
-            any |= first[i] || tie_n[i] > 0;
+            any |= first[i];
         }
         if (any) s_any = 1;
         lds_barrier();  // also: every rank-by-count read is done before the staging is overwritten
@@ -699,9 +734,8 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const uint32_t dg = dg_of(key[i], dd);
-                const uint32_t size = first[i] ? s_start[dg + 1] - s_start[dg] : tie_n[i];
-                route((uint32_t)st + (first[i] ? slot[i] : out[i]), size, first[i] ? nhi : B, B, 0, false, L, ctr,
-                      lane);
+                const uint32_t size = first[i] ? s_start[dg + 1] - s_start[dg] : 0;
+                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
             }
         }
 #pragma unroll
@@ -734,11 +768,11 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 // counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
 // in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
 // -- the ranks are stable.  About 12 VALU per item instead of about 50.
-template <int I, bool TIES>
+template <int I>
 __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr) {
+                                                      uint32_t *__restrict__ ctr, int skip) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
     __shared__ uint32_t s_v[CAP + 1];
@@ -760,7 +794,15 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
         const uint2 ce = e;
         const uint64_t st = ce.x;
         const uint32_t len = ce.y >> 8;
-        const int hi = (ce.y >> 1) & 127;
+        int hi = (ce.y >> 1) & 127;
+        if (skip) {
+            const uint64_t kf = __shfl(key[0], 0);
+            uint64_t x = 0;
+#pragma unroll
+            for (int i = 0; i < I; ++i)
+                if ((uint32_t)(i * 64 + lane) < len) x |= key[i] ^ kf;
+            hi = skip_hi(wave_or64(x), B, hi);
+        }
         const Dig dd = dig_at(B, hi, 8);
         const int nhi = hi + 8;
         const bool last = nhi >= B;
@@ -827,22 +869,20 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
         }
 
         // final position and head flag of every element (reads precede writes: one wave)
-        uint32_t out[I], tie_n[I];
+        uint32_t out[I];
         uint8_t hd[I];
         bool any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             out[i] = slot[i];
             hd[i] = 0;
-            tie_n[i] = 0;
             if (i >= live) continue;
             const uint32_t sb = s_cnt[dig[i]], size = s_cnt[dig[i] + 1] - sb;
             hd[i] = slot[i] == sb;
-            if (TIES && valid[i] && size > 1 && last && hd[i]) tie_n[i] = size;
             if (valid[i] && size > 1 && !last) {
                 if (size <= (uint32_t)kSmall) {
                     const uint32_t me = slot[i] - sb;
-                    uint32_t lt = 0, eq = 0, eqall = 0;
+                    uint32_t lt = 0, eq = 0;
                     // 4 keys per step (their LDS reads in flight together); indices past the
                     // sub-bucket are clamped and not counted
                     for (uint32_t j0 = 0; j0 < size; j0 += 4) {
@@ -854,27 +894,23 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
                             const uint32_t j = j0 + u;
                             lt += j < size && kj[u] < key[i];
                             eq += j < me && kj[u] == key[i];
-                            if (TIES) eqall += j < size && kj[u] == key[i];
                         }
                     }
                     out[i] = sb + lt + eq;
                     hd[i] = eq == 0;
-                    if (TIES && eq == 0 && eqall > 1) tie_n[i] = eqall;
                 } else {
                     hd[i] = 2;
                     any = true;
                 }
             }
         }
-#pragma unroll
-        for (int i = 0; i < I; ++i) any |= tie_n[i] > 0;
         const bool relist = __ballot(any) != 0;
-        if (relist) {  // re-list the large sub-buckets (rare); TIES: groups of equal words -> done
+        if (relist) {  // re-list the large sub-buckets (rare)
 #pragma unroll
             for (int i = 0; i < I; ++i) {
                 const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
-                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : tie_n[i];
-                route((uint32_t)st + (first ? slot[i] : out[i]), size, first ? nhi : B, B, 0, false, L, ctr, lane);
+                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : 0;
+                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
             }
         }
 #pragma unroll
@@ -892,6 +928,88 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
             v0[st + p] = s_v[p];
             heads[st + p] = s_hd[p] & 1;
         }
+    }
+}
+
+// Buckets of <= kTiny elements (mostly from the tie groups of multi-word keys): one thread per
+// bucket, stable rank-by-count over the full word (ties: load order = start order), write-back of
+// starts and head flags to buffer 0.
+__global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__ list, uint32_t count,
+                                                       const uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                       const uint32_t *v1, uint8_t *__restrict__ heads) {
+    const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+    const bool live = idx < count;
+    const uint2 e = live ? list[idx] : make_uint2(0, 1u << 8);
+    const uint64_t st = e.x;
+    const uint32_t len = e.y >> 8;
+    const uint64_t *sk = (e.y & 1) ? k1 : k0;
+    const uint32_t *sv = (e.y & 1) ? v1 : v0;
+    uint64_t key[kTiny];
+    uint32_t val[kTiny];
+#pragma unroll
+    for (int j = 0; j < kTiny; ++j) {
+        const uint64_t at = st + min((uint32_t)j, len - 1);
+        key[j] = live ? sk[at] : 0;
+        val[j] = live ? sv[at] : 0;
+    }
+    uint32_t out[kTiny];
+    bool hd[kTiny];
+#pragma unroll
+    for (int j = 0; j < kTiny; ++j) {
+        uint32_t lt = 0, eq = 0;
+#pragma unroll
+        for (int i = 0; i < kTiny; ++i) {
+            lt += (uint32_t)i < len && key[i] < key[j];
+            eq += i < j && key[i] == key[j];
+        }
+        out[j] = lt + eq;
+        hd[j] = eq == 0;
+    }
+    if (!live) return;
+#pragma unroll
+    for (int j = 0; j < kTiny; ++j) {
+        if ((uint32_t)j >= len) break;
+        v0[st + out[j]] = val[j];
+        heads[st + out[j]] = hd[j] ? 1 : 0;
+    }
+}
+
+// Multi-word keys: the groups of >= 2 equal earlier words, from the head flags of the order so far:
+// f_first[i] = first element of such a group, f_last[i] = its last element.
+__global__ __launch_bounds__(256) void tie_run_flags_kernel(const uint8_t *__restrict__ heads, uint64_t n,
+                                                            uint8_t *__restrict__ f_first, uint8_t *__restrict__ f_last) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const bool h = heads[i] != 0, hn = i + 1 >= n || heads[i + 1] != 0;
+        f_first[i] = h && !hn;
+        f_last[i] = !h && hn;
+    }
+}
+
+__global__ __launch_bounds__(256) void tie_run_lengths_kernel(const uint32_t *__restrict__ first,
+                                                              uint32_t *__restrict__ last_to_len, uint64_t ng) {
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 256)
+        last_to_len[g] = last_to_len[g] - first[g] + 1;
+}
+
+// Flat variant of tie_encode_kernel for many groups: every element in a group of >= 2 (a head
+// flag of 0 at it or at its successor) gets the next key word.
+template <int BITS>
+__global__ __launch_bounds__(256) void tie_encode_flat_kernel(const uint8_t *__restrict__ sba,
+                                                              const uint8_t *__restrict__ heads, uint64_t n,
+                                                              const uint32_t *__restrict__ vals,
+                                                              uint64_t *__restrict__ keys, int sym0, int nsym, int k,
+                                                              int canonical) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4_msd[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const bool tie = heads[i] == 0 || (i + 1 < n && heads[i + 1] == 0);
+        if (!tie) continue;
+        const uint8_t *b = sba + vals[i];
+        const bool rc = canonical && canon_is_rc<BITS>(b, k, s_lut4);
+        uint64_t key = 0;
+        for (int t = sym0; t < sym0 + nsym; ++t) key = (key << BITS) | canon_sym<BITS>(b, k, t, rc, s_lut4);
+        keys[i] = key;
     }
 }
 
@@ -944,6 +1062,7 @@ __global__ __launch_bounds__(256) void tie_encode_kernel(const uint8_t *__restri
 static int grid_n(uint64_t n) { return (int)std::max<uint64_t>((n + 255) / 256, 1); }
 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
+hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);
 
 // grow a device array to hold `need` entries, keeping the first `keep` entries
 template <typename T>
@@ -977,11 +1096,12 @@ static unsigned cu_count(gk_ctx *c) {
 }
 
 static const char *kLocName[kLocal][2] = {{"loc0a", "loc0b"}, {"loc1a", "loc1b"}, {"loc2a", "loc2b"},
-                                          {"loc3a", "loc3b"}};
+                                          {"loc3a", "loc3b"}, {"loc4a", "loc4b"}};
 static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_r"},
                                            {"msd_local_wave8", "msd_local_wave8_r"},
                                            {"msd_local_wave16", "msd_local_wave16_r"},
-                                           {"msd_local_block16", "msd_local_block16_r"}};
+                                           {"msd_local_block16", "msd_local_block16_r"},
+                                           {"msd_local_tiny", "msd_local_tiny_r"}};
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
 
@@ -1010,6 +1130,7 @@ struct MsdDriver {
     uint64_t nloc[kLocal] = {0}, loc_elems[kLocal] = {0}, ndone = 0, big_elems = 0;
     uint32_t nbig = 0;
     int cur_big = 0;
+    int phase = 0;  // key word being sorted (multi-word keys)
 
     MsdDriver(gk_ctx *c_, const KeySpec &ks_) : c(c_), ks(ks_), B(ks_.total_bits) {
         cus = cu_count(c);
@@ -1038,7 +1159,7 @@ struct MsdDriver {
 
     Lists lists(int g, int bigsel) {
         return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par,
-                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g]}};
+                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g], loc[4][g]}};
     }
 
     int init(uint64_t n_) {
@@ -1335,20 +1456,49 @@ struct MsdDriver {
         return classify(nseg << width(1), kGR + width(1), 0, cur_big);
     }
 
-    // Multi-word keys, phase > 0: the done list of the previous phase holds the groups of equal
-    // earlier words (in buffer 0); sort each group of >= 2 by the key word of symbols
-    // [sym0, sym0 + nsym).  more: further words follow (collect this phase's ties).
-    int next_phase(int sym0, int nsym, bool more) {
-        const uint64_t ng = ndone;
-        if (ng == 0) return GK_OK;
+    // Multi-word keys, phase > 0: the head flags of the order so far (buffer 0) mark the groups of
+    // equal earlier words; sort each group of >= 2 by the key word of symbols [sym0, sym0 + nsym).
+    int next_phase(int sym0, int nsym) {
+        uint8_t *f_first, *f_last;
         uint32_t *g_start, *g_len;
-        GK_TRY_HIP(c, scratch(c, "tie_start", ng, &g_start));
-        GK_TRY_HIP(c, scratch(c, "tie_len", ng, &g_len));
-        GK_TRY_HIP(c, hipMemcpyAsync(g_start, dn_start, 4 * ng, hipMemcpyDeviceToDevice, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(g_len, dn_len, 4 * ng, hipMemcpyDeviceToDevice, c->stream));
+        GK_TRY_HIP(c, scratch(c, "tie_f_first", n + 64, &f_first));
+        GK_TRY_HIP(c, scratch(c, "tie_f_last", n + 64, &f_last));
+        timer_begin(c, "msd_tie_groups", &slot);
+        const unsigned fgrid = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 32);
+        hipLaunchKernelGGL(tie_run_flags_kernel, dim3(fgrid), dim3(256), 0, c->stream, heads, n, f_first, f_last);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t ng = 0, ng2 = 0;
+        GK_TRY_HIP(c, scratch(c, "tie_start", n / 2 + 64, &g_start));
+        GK_TRY_HIP(c, scratch(c, "tie_len", n / 2 + 64, &g_len));
+        GK_TRY_HIP(c, select_flags(c, f_first, n, g_start, &ng));
+        GK_TRY_HIP(c, select_flags(c, f_last, n, g_len, &ng2));
+        if (ng != ng2) return fail(c, GK_E_HIP, "msd: tie group bounds do not pair up");
+        if (ng > 0)
+            hipLaunchKernelGGL(tie_run_lengths_kernel, dim3((unsigned)std::min<uint64_t>((ng + 255) / 256, 8192)),
+                               dim3(256), 0, c->stream, g_start, g_len, ng);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        if (ng == 0) return GK_OK;
         timer_begin(c, "msd_tie_encode", &slot);
         const unsigned grid = (unsigned)std::min<uint64_t>((ng + 3) / 4, (uint64_t)cus * 16);
-        if (ks.bits == 2)
+        bool flat = ng > 4096;
+        if (!flat) {  // few groups: flat too if they are large (one wave per group would be serial)
+            std::vector<uint32_t> lens(ng);
+            GK_TRY_HIP(c, hipMemcpyAsync(lens.data(), g_len, 4 * ng, hipMemcpyDeviceToHost, c->stream));
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+            uint64_t tot = 0;
+            for (uint32_t v : lens) tot += v;
+            flat = tot > (1u << 20);
+        }
+        if (flat) {  // many groups: one pass over the head flags, one thread per element
+            const unsigned fg = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 32);
+            if (ks.bits == 2)
+                hipLaunchKernelGGL(tie_encode_flat_kernel<2>, dim3(fg), dim3(256), 0, c->stream, c->sba, heads, n,
+                                   c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
+            else
+                hipLaunchKernelGGL(tie_encode_flat_kernel<4>, dim3(fg), dim3(256), 0, c->stream, c->sba, heads, n,
+                                   c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
+        } else if (ks.bits == 2)
             hipLaunchKernelGGL(tie_encode_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, g_start, g_len,
                                (uint32_t)ng, c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
         else
@@ -1357,6 +1507,7 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         B = ks.bits * nsym;
+        ++phase;
         GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
         ndone = 0;
         nbig = 0;
@@ -1366,7 +1517,7 @@ struct MsdDriver {
         if (rc != GK_OK) return rc;
         rc = levels(1, 0, 0);
         if (rc != GK_OK) return rc;
-        return finish(more);
+        return finish();
     }
 
     // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
@@ -1407,31 +1558,36 @@ struct MsdDriver {
     }
 
     // one local class's kernel over a list of cnt buckets
-    template <bool TIES>
     void local_launch(int k, uint32_t cnt, const uint2 *lst, uint64_t *k0, uint32_t *v0, const uint64_t *k1,
-                      const uint32_t *v1, const Lists &nl) {
+                      const uint32_t *v1, const Lists &nl, int round) {
+        // common-prefix skip: re-listed buckets, later phases (repeats) and the block class; not
+        // the first wave round of phase 0, where random keys differ right below the sorted bits
+        const int skip = (round > 0 || phase > 0 || k == 3) ? 1 : 0;
         switch (k) {
         case 0:
-            hipLaunchKernelGGL((msd_wave_kernel<4, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            hipLaunchKernelGGL((msd_wave_kernel<4>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
             break;
         case 1:
-            hipLaunchKernelGGL((msd_wave_kernel<8, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            hipLaunchKernelGGL((msd_wave_kernel<8>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
             break;
         case 2:
-            hipLaunchKernelGGL((msd_wave_kernel<16, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            hipLaunchKernelGGL((msd_wave_kernel<16>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(64),
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
+            break;
+        case 3:
+            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
+                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
             break;
         default:
-            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR, TIES>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
-                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr);
+            hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
+                               v1, heads);
         }
     }
 
     // local rounds (generation g lists -> re-listed sub-buckets in generation g ^ 1), done copies.
-    // ties: more key words follow -- groups of equal words are collected in the done list
-    int finish(bool ties = false) {
+    int finish() {
         const uint64_t max_spill = n / (kSmall + 1) + 1024;
         uint64_t pending = 0;
         for (int k = 0; k < kLocal; ++k) {
@@ -1439,11 +1595,9 @@ struct MsdDriver {
             GK_TRY_HIP(c, grow_keep(c, kLocName[k][1], max_spill, 0, &loc[k][1]));
             pending += nloc[k];
         }
-        // ties: every group of >= 2 equal words may be listed as done
-        const uint64_t dn_spill = ties ? n / 2 + 1024 : max_spill;
-        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + dn_spill, ndone, &dn_start));
-        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + dn_spill, ndone, &dn_len));
-        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + dn_spill, ndone, &dn_par));
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + max_spill, ndone, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + max_spill, ndone, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + max_spill, ndone, &dn_par));
         int g = 0, round = 0;
         while (pending > 0) {
             const int ng = g ^ 1;
@@ -1458,10 +1612,26 @@ struct MsdDriver {
                 uint64_t *k0 = c->keys[0], *k1 = c->keys[1];
                 uint32_t *v0 = c->vals[0], *v1 = c->vals[1];
                 const uint2 *lst = loc[k][g];
-                if (ties) local_launch<true>(k, cnt, lst, k0, v0, k1, v1, nl);
-                else local_launch<false>(k, cnt, lst, k0, v0, k1, v1, nl);
+                static const bool trace = std::getenv("GKM_MSD_TRACE") != nullptr;
+                hipEvent_t t0 = nullptr, t1 = nullptr;
+                if (trace) {
+                    hipEventCreate(&t0);
+                    hipEventCreate(&t1);
+                    hipEventRecord(t0, c->stream);
+                }
+                local_launch(k, cnt, lst, k0, v0, k1, v1, nl, round);
                 GK_TRY_HIP(c, hipGetLastError());
                 timer_end(c, slot);
+                if (trace) {  // diagnostics: one line per local launch
+                    hipEventRecord(t1, c->stream);
+                    hipEventSynchronize(t1);
+                    float ms = 0;
+                    hipEventElapsedTime(&ms, t0, t1);
+                    std::fprintf(stderr, "[msd] phase %d round %d class %d buckets %u: %.3f ms\n", phase, round, k,
+                                 cnt, ms);
+                    hipEventDestroy(t0);
+                    hipEventDestroy(t1);
+                }
             }
             int rc = read_ctr();
             if (rc != GK_OK) return rc;
@@ -1505,9 +1675,9 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     if (rc != GK_OK) return rc;
     rc = d.levels(1, d.width(0), 0);
     if (rc != GK_OK) return rc;
-    rc = d.finish(nphase > 1);
+    rc = d.finish();
     for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
-        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw), ph + 1 < nphase);
+        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));
     timer_end(c, d.total_slot);
     return rc;
 }
@@ -1543,9 +1713,9 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     if (rc != GK_OK) return rc;
     rc = d.levels(2, kGR + d.width(1), 0);
     if (rc != GK_OK) return rc;
-    rc = d.finish(nphase > 1);
+    rc = d.finish();
     for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
-        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw), ph + 1 < nphase);
+        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));
     timer_end(c, d.total_slot);
     return rc;
 }

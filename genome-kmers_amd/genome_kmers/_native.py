@@ -117,16 +117,34 @@ _SIGS = {
     "gk_profile_report": ([_P, ctypes.c_char_p, ctypes.c_uint64], ctypes.c_int),
     "gk_stream": ([_P, ctypes.POINTER(_P)], ctypes.c_int),
     "gk_shard_bucket_bits": ([], ctypes.c_int),
-    "gk_shard_partition": ([_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _P, _P, ctypes.c_uint64, _U64P,
-                            _U64P], ctypes.c_int),
-    "gk_shard_sort": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, _U64P, _U64P, _U32P, ctypes.c_uint32],
-                      ctypes.c_int),
+    "gk_shard_partition": ([_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
+                            ctypes.c_uint64, _U64P, _U64P], ctypes.c_int),
+    "gk_shard_sort": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _U64P, _U64P, _U32P,
+                       ctypes.c_uint32], ctypes.c_int),
     "gk_fasta_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P), _U64P, _U64P, _U64P], ctypes.c_int),
     "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
     "gk_fasta_close": ([_P], None),
     "gk_locate": ([_P, _U64P, ctypes.c_uint64, _U32P, _U32P], ctypes.c_int),
     "gk_copy_strands": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
 }
+
+
+def _share_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (soname
+    libamdhip64.so.7, loaded by torch as "libamdhip64.so"); libgkm needs libamdhip64.so.7.  If
+    libgkm loaded /opt/rocm's copy first, torch would later load a second runtime and fail to see
+    the GPU ("No HIP GPUs are available").  Loading torch's copy first (global, without importing
+    torch) makes both bind the same runtime, whichever is imported first."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for root in spec.submodule_search_locations:
+        hip = Path(root) / "lib" / "libamdhip64.so"
+        if hip.exists():
+            ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+            return
 
 
 def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -139,6 +157,7 @@ def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
             f"libgkm.so not found at {path}; build it with `make -C genome-kmers_amd/csrc` "
             "(genome_kmers has no CPU fallback)"
         )
+    _share_hip_runtime()
     lib = ctypes.CDLL(str(path))
     for name, (args, res) in _SIGS.items():
         fn = getattr(lib, name)
@@ -350,24 +369,26 @@ class Engine:
     def shard_bucket_bits(self) -> int:
         return int(self.lib.gk_shard_bucket_bits())
 
-    def shard_partition(self, lo: int, hi: int, k: int, keys, starts):
+    def shard_partition(self, lo: int, hi: int, k: int, keys, starts, canonical: bool = False):
         """Encode + partition the k-mers starting in [lo, hi) into the device tensors ``keys``
         (int64) / ``starts`` (int32); returns (bucket sizes as a numpy uint64 array, count)."""
         hist = np.zeros(1 << self.shard_bucket_bits(), dtype=np.uint64)
         n = ctypes.c_uint64(0)
         cap = min(keys.numel(), starts.numel())
-        self._check(self.lib.gk_shard_partition(self.ctx, lo, hi, k, keys.data_ptr(), starts.data_ptr(), cap,
+        self._check(self.lib.gk_shard_partition(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
+                                                keys.data_ptr(), starts.data_ptr(), cap,
                                                 _ptr(hist, ctypes.c_uint64), ctypes.byref(n)))
         return hist, n.value
 
     def shard_sort(self, keys, starts, n: int, k: int, piece_off: np.ndarray, piece_len: np.ndarray,
-                   piece_bucket: np.ndarray):
+                   piece_bucket: np.ndarray, canonical: bool = False):
         """Sort n received (key, start) pairs held in device tensors, given as bucket pieces."""
         off = np.ascontiguousarray(piece_off, dtype=np.uint64)
         ln = np.ascontiguousarray(piece_len, dtype=np.uint64)
         bk = np.ascontiguousarray(piece_bucket, dtype=np.uint32)
         self._check(self.lib.gk_shard_sort(self.ctx, keys.data_ptr() if n else None, starts.data_ptr() if n else None,
-                                           n, k, _ptr(off, ctypes.c_uint64), _ptr(ln, ctypes.c_uint64),
+                                           n, k, SORT_CANONICAL if canonical else 0, _ptr(off, ctypes.c_uint64),
+                                           _ptr(ln, ctypes.c_uint64),
                                            _ptr(bk, ctypes.c_uint32), len(bk)))
         self.n = n
 

@@ -84,12 +84,13 @@ class ShardedKmerSort:
     """
 
     def __init__(self, sba: np.ndarray, seg_starts: np.ndarray, k: int, rank: int, world: int, device: int = 0,
-                 engine=None, torch_device=None, group=None, chunk: int = None):
+                 engine=None, torch_device=None, group=None, chunk: int = None, canonical: bool = False):
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist, self.group = torch, dist, group
         self.rank, self.world, self.k = rank, world, k
+        self.canonical = canonical  # canonical k-mers (Kmers.sort(canonical=True)); same flag on every rank
         self.dev = torch_device if torch_device is not None else torch.device("cuda", device)
         if engine is None:
             from genome_kmers import _native
@@ -153,7 +154,8 @@ class ShardedKmerSort:
     def run(self) -> int:
         """One sort; returns this rank's number of distinct k-mers."""
         torch, dist = self.torch, self.dist
-        hist, n = self.engine.shard_partition(self.lo, self.hi, self.k, self.send_k, self.send_v)
+        hist, n = self.engine.shard_partition(self.lo, self.hi, self.k, self.send_k, self.send_v,
+                                              canonical=self.canonical)
         h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to(self.dev)
         gathered = [torch.empty_like(h) for _ in range(self.world)]
         dist.all_gather(gathered, h, group=self.group)
@@ -171,6 +173,6 @@ class ShardedKmerSort:
         off, ln, bk = receive_pieces(H, b0, b1, recv_counts)
         if self.recv_k.is_cuda:  # the engine works on its own stream: the exchange must be done
             torch.cuda.current_stream(self.dev).synchronize()
-        self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk)
+        self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk, canonical=self.canonical)
         self.local_kmers = R
         return self.engine.unique_count_only()

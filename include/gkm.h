@@ -168,14 +168,16 @@ int gk_stream(gk_ctx *ctx, void **stream);
 /* number of top key bits the shard buckets are cut on (buckets = 1 << bits) */
 int gk_shard_bucket_bits(void);
 /*
- * Send side: encode the fixed-length k-mers (length k, no '$') that start in sequence positions
- * [lo, hi) (lo a multiple of 32) and partition them stably by their top gk_shard_bucket_bits()
- * key bits into the caller's DEVICE buffers d_keys / d_starts (capacity cap >= count + 1), in
- * ascending bucket order.  h_hist[1 << bits] receives the bucket sizes, *n_out the count.
+ * Send side: encode the fixed-length k-mers (length k <= 64, no '$') that start in sequence
+ * positions [lo, hi) (lo a multiple of 32) and partition them stably by their top
+ * gk_shard_bucket_bits() key bits into the caller's DEVICE buffers d_keys / d_starts (capacity
+ * cap >= count + 1), in ascending bucket order.  d_keys holds each k-mer's FIRST key word (the
+ * first 64 / bits symbols); later words are re-encoded from the sba by the receiver.  flags:
+ * 0 or GK_SORT_CANONICAL (the same on every rank and in gk_shard_sort).  h_hist[1 << bits] receives the bucket sizes, *n_out the count.
  * Returns after the device work is complete (the buffers can go straight to another stream).
  */
-int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint64_t *d_keys, uint32_t *d_starts,
-                       uint64_t cap, uint64_t *h_hist, uint64_t *n_out);
+int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *d_keys,
+                       uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out);
 /*
  * Receive side: sort n received (key, start) pairs in DEVICE buffers, given as npieces pieces
  * (offset, length, bucket) listed in ascending bucket order; the pieces of one bucket are listed
@@ -185,7 +187,7 @@ int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint64
  * been synchronised by the caller).
  */
 int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
-                  const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
+                  uint32_t flags, const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
                   uint32_t npieces);
 
 /* Location of selected k-mers for Kmers.get_kmers(kmer_info_to_yield="full") (kmers.py:1180-1264):

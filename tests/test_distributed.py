@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from genome_kmers import distributed as D
+from oracle import oracle
 
 K = 11
 
@@ -65,7 +66,8 @@ class NumpyShardEngine:
     def shard_bucket_bits(self):
         return self.bits
 
-    def shard_partition(self, lo, hi, k, keys_t, starts_t):
+    def shard_partition(self, lo, hi, k, keys_t, starts_t, canonical=False):
+        assert not canonical
         s = _valid_starts(self.sba, self.seg, k, lo, hi)
         key = _keys(self.sba, s, k)
         top = (key >> np.uint64(2 * k - self.bits)).astype(np.int64)
@@ -75,7 +77,7 @@ class NumpyShardEngine:
         starts_t[:n] = __import__("torch").from_numpy(s[order].astype(np.int32))
         return np.bincount(top, minlength=1 << self.bits).astype(np.uint64), n
 
-    def shard_sort(self, keys_t, starts_t, n, k, off, ln, bk):
+    def shard_sort(self, keys_t, starts_t, n, k, off, ln, bk, canonical=False):
         assert np.all(np.diff(bk.astype(np.int64)) >= 0), "pieces must come in bucket order"
         key = keys_t[:n].numpy().view(np.uint64)
         st = starts_t[:n].numpy().astype(np.int64)
@@ -184,15 +186,20 @@ def test_gloo_world2_matches_oracle(contigs, chunk):
 
 # ---- device shard entry points, two ranks in one process ---------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,contigs", [(2, 1), (3, 4)])
-def test_gpu_shards_concatenate_to_single_sort(world, contigs):
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
+    (2, 1, 31, False, False), (3, 4, 31, False, False), (2, 3, 63, False, False), (3, 2, 31, True, False),
+    (2, 2, 63, True, True), (2, 1, 40, False, True)])
+def test_gpu_shards_concatenate_to_single_sort(world, contigs, k, canonical, iupac):
     import torch
 
     from genome_kmers import _native
 
     sba, seg = _random_sba(200_000 + 17, 3 + world, contigs)
     sba[150_100:151_000] = sba[1000:1900]  # repeats across ranks (inside a contig)
-    k = 31
+    sba[160_000:160_900] = oracle.reverse_complement(sba[1000:1900])  # reverse-complement repeat
+    if iupac:
+        sba[5000:5100] = ord("N")
+        sba[90_000:90_050:7] = ord("R")
     engines = [_native.Engine(0) for _ in range(world)]
     bounds = D.position_ranges(len(sba), world)
     dev = torch.device("cuda", 0)
@@ -202,7 +209,7 @@ def test_gpu_shards_concatenate_to_single_sort(world, contigs):
         cap = bounds[r + 1] - bounds[r] + 64
         sk = torch.empty(cap, dtype=torch.int64, device=dev)
         sv = torch.empty(cap, dtype=torch.int32, device=dev)
-        hist, n = e.shard_partition(bounds[r], bounds[r + 1], k, sk, sv)
+        hist, n = e.shard_partition(bounds[r], bounds[r + 1], k, sk, sv, canonical=canonical)
         sends.append((sk, sv, n))
         hists.append(np.asarray(hist, dtype=np.int64))
     H = np.stack(hists)
@@ -221,12 +228,12 @@ def test_gpu_shards_concatenate_to_single_sort(world, contigs):
         rv = torch.cat(parts_v + [torch.empty(64, dtype=torch.int32, device=dev)])
         off, ln, bk = D.receive_pieces(H, bb[r], bb[r + 1], recv_counts)
         torch.cuda.current_stream(dev).synchronize()
-        e.shard_sort(rk, rv, R, k, off, ln, bk)
+        e.shard_sort(rk, rv, R, k, off, ln, bk, canonical=canonical)
         got.append(e.copy_starts())
         uniq += e.unique_count_only()
     ref = _native.Engine(0)
     ref.set_sequence(sba, seg)
     ref.enumerate(k)
-    ref.sort(k)
+    ref.sort(k, canonical=canonical)
     np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
     assert uniq == ref.unique_count_only()

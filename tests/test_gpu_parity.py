@@ -430,3 +430,12 @@ def test_multiword_runs_the_msd_phases(k, alphabet):
     want = oracle.quicksort(sc.forward_sba, oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k),
                             k, k, break_ties=True)
     np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+
+
+def test_multiword_many_tiny_tie_groups_flat_encode():
+    """4-bit keys at k=31 over a low-entropy alphabet: the first word (16 symbols) ties often, so
+    the second phase sees >4096 small groups (flat re-encode, one-thread tiny buckets)."""
+    rng = np.random.default_rng(77)
+    seqs = random_genome(rng, [1_500_000, 500_000], alphabet=b"ACACACACACN")
+    seqs.append(("n", "N" * 3000 + "ACGT" * 100))  # one large all-N group
+    oracle_check(seqs, 31, 31)

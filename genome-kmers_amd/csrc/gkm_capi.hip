@@ -421,7 +421,14 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     int rc = ensure_elems(c, c->n, msd ? 1 : ks.words);
     if (rc != GK_OK) return rc;
     if (msd) {
-        rc = msd_sort(c, ks);
+        // a mixed sba (N runs, IUPAC letters): ACGT-only k-mers on 2-bit keys, the rest apart
+        static const bool no_split = std::getenv("GKM_NO_SPLIT") != nullptr;
+        bool split = false;
+        if (!c->acgt && !no_split) {
+            rc = split_sort(c, ks, &split);
+            if (rc != GK_OK) return rc;
+        }
+        if (!split) rc = msd_sort(c, ks);
         if (rc != GK_OK) return rc;
         c->spec = ks;
         c->keys_valid = true;

@@ -49,6 +49,7 @@ struct KeySpec {
     int words;        // W
     int total_bits;
     int canonical;    // 1: key of min(k-mer, reverse complement) (gkm_canon.h; fixed length only)
+    int acgt_only;    // MSD of a mixed sba's ACGT-only k-mers (2-bit keys; the rest sorted apart, gkm_split.hip)
     int digits() const { return (total_bits + kRadixBits - 1) / kRadixBits; }
 };
 
@@ -156,8 +157,11 @@ inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) 
 }
 // re-encode keys[cur] from vals[cur] when the sort left them stale (gk_ctx::keys_stale)
 int ensure_keys(gk_ctx *c);
-// MSD sort of one-word keys from the enumerated positions (gkm_msd.hip)
+// MSD sort of fixed-length keys from the enumerated positions (gkm_msd.hip)
 int msd_sort(gk_ctx *c, const KeySpec &ks);
+// fixed-length sort of a mixed-alphabet sba: ACGT-only k-mers by the 2-bit MSD, the others by
+// 4-bit keys, merged (gkm_split.hip); *used = false when the split does not pay (caller falls back)
+int split_sort(gk_ctx *c, const KeySpec &ks, bool *used);
 // multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the
 // top msd_radix_bits() key bits; receive-side sort of buckets given as pieces
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,

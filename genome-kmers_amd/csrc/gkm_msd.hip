@@ -67,6 +67,7 @@ struct L0Args {
     const uint8_t *sba;
     uint64_t lo, hi;  // k-mer starts in [lo, hi) (lo a multiple of 32: 16-B aligned tiles)
     int symbols, total_bits;
+    int acgt_only;    // 2-bit keys of a mixed sba: k-mers holding a non-ACGT byte are not started
 };
 
 template <int BITS, int TILE>
@@ -85,9 +86,10 @@ __device__ __forceinline__ void l0_load(const uint8_t *__restrict__ src, uint4 &
     rb = s4[1];
 }
 
+// s_dol bit = the position ends k-mers: '$' (or, acgt_only, any byte outside ACGT)
 template <int BITS, int TILE>
 __device__ __forceinline__ void l0_pack(const uint4 &ra, const uint4 &rb, uint64_t *s_code, uint32_t *s_dol,
-                                        const uint8_t *lut4) {
+                                        const uint8_t *lut4, int acgt_only = 0) {
     using P = L0Pack<BITS, TILE>;
     const int g = threadIdx.x;
     if (g < P::kGroups) {
@@ -97,7 +99,8 @@ __device__ __forceinline__ void l0_pack(const uint4 &ra, const uint4 &rb, uint64
 #pragma unroll
         for (int q = 0; q < 32; ++q) {
             const uint32_t ch = (wv[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-            dm = (dm << 1) | (ch == GK_DOLLAR ? 1u : 0u);
+            const bool stop = acgt_only ? !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T') : ch == GK_DOLLAR;
+            dm = (dm << 1) | (stop ? 1u : 0u);
             if (BITS == 2) {
                 c0 = (c0 << 2) | (((ch >> 1) ^ (ch >> 2)) & 3u);
             } else {
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     const uint64_t P0 = a.lo + (uint64_t)blockIdx.x * TILE;
     uint4 ra, rb;
     l0_load<BITS, TILE>(a.sba + P0, ra, rb);
-    l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+    l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < I; ++i) {
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
         lds_barrier();  // the previous tile's runs have been read out of LDS
         for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
         if (tid < RADIX) s_toff[tid] = toff;
-        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
         lds_barrier();
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         uint64_t key[I];
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int u = 0; u < (RADIX + 63) / 64; ++u)
             if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
         if (tid < RADIX) s_toff[cur][tid] = toff;
-        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4);
+        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
         for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
@@ -1279,7 +1282,7 @@ struct MsdDriver {
             GK_TRY_HIP(c, hipMemcpyAsync(s_misc, misc, 12, hipMemcpyHostToDevice, c->stream));
             GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         }
-        const L0Args a{c->sba, lo, hi, ks.symbols, B};
+        const L0Args a{c->sba, lo, hi, ks.symbols, B, ks.acgt_only};
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
         timer_begin(c, "msd_l0_count", &slot);

@@ -108,3 +108,20 @@ def test_canonical_argument_errors():
     with pytest.raises(AssertionError, match="needs sort"):
         km.get_canonical_strands()
     assert km.get_kmer_count(3) == 7
+
+
+@pytest.mark.parametrize("k", [15, 31, 63])
+def test_canonical_split_n_runs_vs_oracle(k):
+    """Canonical k-mers over a GRCh38-like sba (N runs): the ACGT/other split keeps each k-mer's
+    class under reverse complement, so it serves canonical sorts too."""
+    rng = np.random.default_rng(600 + k)
+    seqs = genome_with_rc_repeats(rng, [50_000, 20_000], b"ACGT")
+    out = []
+    for name, s in seqs:
+        b = bytearray(s.encode())
+        for a in rng.integers(0, len(b) - 300, 4):
+            b[a:a + 200] = b"N" * 200
+        b[int(rng.integers(0, len(b)))] = ord("R")
+        out.append((name, b.decode()))
+    km, _ = check_canonical(out, k)
+    assert not km._engine.is_acgt()

@@ -439,3 +439,47 @@ def test_multiword_many_tiny_tie_groups_flat_encode():
     seqs = random_genome(rng, [1_500_000, 500_000], alphabet=b"ACACACACACN")
     seqs.append(("n", "N" * 3000 + "ACGT" * 100))  # one large all-N group
     oracle_check(seqs, 31, 31)
+
+
+def n_run_genome(rng, lengths, runs=6, run_len=(40, 400), sparse=30):
+    """Random ACGT records with N runs (GRCh38-like) and a few scattered IUPAC letters, planted
+    repeats inside and across records."""
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 900).astype(np.uint8)
+    seqs = []
+    for i, L in enumerate(lengths):
+        s = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), L).astype(np.uint8)
+        for _ in range(3):
+            at = int(rng.integers(0, max(1, L - len(rep))))
+            s[at:at + len(rep)] = rep[: L - at]
+        for _ in range(runs):
+            a = int(rng.integers(0, L))
+            s[a:a + int(rng.integers(*run_len))] = ord("N")
+        at = rng.integers(0, L, sparse)
+        s[at] = np.frombuffer(b"RYKMSWBDHVN", dtype=np.uint8)[rng.integers(0, 11, sparse)]
+        s[:50] = ord("N")  # contig starts / ends in N, as GRCh38's do
+        s[-50:] = ord("N")
+        seqs.append((f"c{i}", s.tobytes().decode()))
+    return seqs
+
+
+@pytest.mark.parametrize("k", [5, 21, 31, 32, 33, 63, 64])
+def test_split_acgt_and_n_kmers_vs_oracle(k):
+    """Mixed sba with few non-ACGT k-mers: ACGT-only k-mers on the 2-bit MSD, the rest on 4-bit keys,
+    merged (gkm_split.hip) -- the profile shows the merge ran."""
+    rng = np.random.default_rng(500 + k)
+    seqs = n_run_genome(rng, [120_000, 40_000, 3_000])
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    eng = km._get_engine()
+    eng.profile_enable(True)
+    km.sort()
+    assert "split_merge" in str(eng.profile_report())
+    unsorted = oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k)
+    want = oracle.quicksort(sc.forward_sba, unsorted, k, k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    h, t = km.get_kmer_group_counts(k, max_counts_bin=64)
+    oh, ot = oracle.group_scan(sc.forward_sba, want, k, max_counts_bin=64)
+    np.testing.assert_array_equal(h, oh)
+    assert t == ot
+    spec = oracle.key_spec(False, k, k)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))

@@ -243,7 +243,7 @@ def main():
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out
         if name.startswith("msd_local"):
-            return 25 * u  # (key, start) in and out + 1 head flag
+            return 17 * u  # (key, start) in; start + 1 head flag out (keys re-encoded on demand)
         if name == "msd_count":
             return 8 * u
         return 0

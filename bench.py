@@ -4,10 +4,14 @@ One step = the hot path over the whole genome with the sequence byte array alrea
 enumerate -> encode (2-bit keys) -> stable LSD radix sort -> unique k-mers + multiplicities.
 Timed with a barrier + device synchronisation on both sides, max over ranks.
 
-N = 1: the genome on one MI355X.  N > 1 (torch.distributed, one rank per GPU): the same genome is
-split into N contiguous position ranges (a (k-1)-base halo each); every rank encodes its range,
-the ranks exchange k-mers by top key bits in ONE all-to-all over RCCL, and each rank sorts and
-counts its key range -- total work fixed, "scaling": "strong".
+N = 1: the genome on one MI355X.  N > 1 (torch.distributed, one rank per GPU), total work fixed,
+"scaling": "strong".  Every rank holds the whole sequence byte array (1 B per k-mer) and owns one
+contiguous range of top key digits (genome_kmers.distributed):
+  --exchange range (default): the digit ranges come from a 2 KiB all-reduce of per-rank digit
+      histograms; each rank re-derives its own k-mers from the whole sequence and sorts them --
+      no k-mer crosses xGMI;
+  --exchange a2a: each rank encodes its position share and the k-mers go to their owners in ONE
+      all-to-all over RCCL (12 B per k-mer), then each rank sorts what it received.
 
 Also reported: the dominant kernel's roofline (HIP events on the engine's stream) and the CPU
 baseline -- the reference algorithm (numba-quicksort restatement, oracle/) on a bounded sample.
@@ -44,7 +48,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=16_000_000, help="k-mers in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
-                    help="use the multi-GPU (all-to-all) path even at N = 1 (exercises it on one GPU)")
+                    help="use the multi-GPU path even at N = 1 (exercises it on one GPU)")
+    ap.add_argument("--exchange", choices=("range", "a2a"), default="range",
+                    help="multi-GPU scheme: key ranges re-derived from the resident sequence (no k-mer "
+                         "exchange) or one all-to-all of the encoded k-mers")
     ap.add_argument("--traffic", type=str, default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc (if present)")
     return ap.parse_args()
@@ -194,7 +201,8 @@ def main():
     else:
         from genome_kmers import distributed
 
-        job = distributed.ShardedKmerSort(sba, seg, k, rank, world, device=local, canonical=canonical)
+        cls = distributed.KeyRangeKmerSort if args.exchange == "range" else distributed.ShardedKmerSort
+        job = cls(sba, seg, k, rank, world, device=local, canonical=canonical)
         eng = job.engine
         h2d_ms = job.h2d_ms
         n_units = job.total_kmers
@@ -234,7 +242,7 @@ def main():
     value = n_units * args.steps / dt
 
     # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4
-    seq_bytes = L if dist is None else job.hi - job.lo
+    seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
 
     def stage_bytes(name, v):
         u = v.get("units", 0)
@@ -292,8 +300,10 @@ def main():
             "data": data,
             "config": {"workload": workload,
                        "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
-                       "parallelism": (f"position-range shards x{world} + 1 RCCL all-to-all" if dist is not None
-                                       else "1 GPU"),
+                       "parallelism": ("1 GPU" if dist is None else
+                                       f"key-range shards x{world}: whole sba per rank, 2 KiB RCCL all-reduce, "
+                                       "no k-mer exchange" if args.exchange == "range" else
+                                       f"position-range shards x{world} + 1 RCCL all-to-all of the k-mers"),
                        "h2d_sba_ms": round(h2d_ms, 2), "stages_ms_per_step": stages},
             "roofline": roofline,
             "cpu_baseline": cpu,

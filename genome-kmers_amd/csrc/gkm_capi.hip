@@ -160,7 +160,7 @@ using namespace gkm;
 // ---------------------------------------------------------------------------------------------
 // buffers
 // ---------------------------------------------------------------------------------------------
-static int ensure_elems(gk_ctx *c, uint64_t n, int words) {
+int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
     // vals[0] / vals[1] hold data that must survive when only keys grow; grow both together
     if (n > c->elem_cap) {
         uint32_t *nv[2] = {nullptr, nullptr};
@@ -842,6 +842,49 @@ extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
     return msd_shard_partition(c, ks, lo, std::max(hi, lo), d_keys, d_starts, cap, h_hist, n_out);
+}
+
+extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
+                                  uint32_t *bits) {
+    if (!c || !h_hist || !bits) return GK_E_ARG;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
+    if (hi > c->sba_len) hi = c->sba_len;
+    if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
+    KeySpec ks;
+    int rc = shard_spec(c, k, flags, &ks);
+    if (rc != GK_OK) return rc;
+    for (int i = 0; i < 256; ++i) h_hist[i] = 0;
+    int b = 0;
+    rc = msd_l0_histogram(c, ks, lo, std::max(hi, lo), h_hist, &b);
+    *bits = (uint32_t)b;
+    return rc;
+}
+
+extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                                   uint64_t *n_kept) {
+    if (!c || !n_kept) return GK_E_ARG;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
+    if (digit_lo > digit_hi || digit_hi > 256u) return fail(c, GK_E_ARG, "digit range outside [0, 256]");
+    KeySpec ks;
+    int rc = shard_spec(c, k, flags, &ks);
+    if (rc != GK_OK) return rc;
+    c->min_k = k;
+    c->have_starts = true;
+    c->enumerated = false;
+    c->starts_materialized = true;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
+    rc = msd_sort_range(c, ks, digit_lo, digit_hi, n_kept);
+    if (rc != GK_OK) return rc;
+    c->spec = ks;
+    c->keys_valid = true;
+    c->keys_stale = c->n > 0;  // the MSD sort keeps the start order, not the keys
+    c->keys_are_ranks = false;
+    c->sorted = true;
+    c->sort_len = k;
+    c->canonical = ks.canonical != 0;
+    return GK_OK;
 }
 
 extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,

@@ -169,6 +169,13 @@ int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, 
 int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint32_t *vin, const uint64_t *poff,
                    const uint64_t *plen, const uint32_t *pbucket, uint32_t np);
 int msd_radix_bits();
+// key-range shards (gkm_msd.hip): the L0 digit histogram (*bits = digit width) of the k-mers
+// starting in [lo, hi); the sort of the k-mers of the whole sba whose L0 digit is in
+// [digit_lo, digit_hi) into keys[0] / vals[0] (c->n = *n_kept)
+int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *hist, int *bits);
+int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t digit_hi, uint64_t *n_kept);
+// key / start buffers for n elements and `words` key words (gkm_capi.hip)
+int ensure_elems(gk_ctx *c, uint64_t n, int words);
 void timer_begin(gk_ctx *c, const char *name, int *slot);
 void timer_end(gk_ctx *c, int slot);
 void timer_units(gk_ctx *c, int slot, uint64_t units);

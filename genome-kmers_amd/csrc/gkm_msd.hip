@@ -68,7 +68,11 @@ struct L0Args {
     uint64_t lo, hi;  // k-mer starts in [lo, hi) (lo a multiple of 32: 16-B aligned tiles)
     int symbols, total_bits;
     int acgt_only;    // 2-bit keys of a mixed sba: k-mers holding a non-ACGT byte are not started
+    // key-range shard: only k-mers whose L0 digit d has d - own_lo < own_span are kept (all: 0, ~0)
+    uint32_t own_lo = 0, own_span = 0xFFFFFFFFu;
 };
+
+__device__ __forceinline__ bool l0_owned(uint32_t d, const L0Args &a) { return d - a.own_lo < a.own_span; }
 
 template <int BITS, int TILE>
 struct L0Pack {
@@ -76,47 +80,76 @@ struct L0Pack {
     static constexpr int kCodeWords = kGroups * BITS / 2 + 1;  // u64 words (+1 for the funnel)
 };
 
-// thread g < kGroups holds the 32 bytes of group g (two 16-B loads)
-template <int BITS, int TILE>
-__device__ __forceinline__ void l0_load(const uint8_t *__restrict__ src, uint4 &ra, uint4 &rb) {
-    // threads past kGroups re-load the last group: no branch, so load counts stay static
-    const uint32_t g = min((uint32_t)threadIdx.x, (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src + 32 * g);
-    ra = s4[0];
-    rb = s4[1];
+// The tile's bytes (kGroups * 32, incl. the halo) in 8-byte units, spread over all T threads:
+// thread t holds units t, t + T, ... (kPer registers; index clamped so the loads stay branch-free)
+template <int BITS, int TILE, int T>
+struct L0Units {
+    static constexpr int kUnits = L0Pack<BITS, TILE>::kGroups * 4;
+    static constexpr int kPer = (kUnits + T - 1) / T;
+};
+
+template <int BITS, int TILE, int T>
+__device__ __forceinline__ void l0_load(const uint8_t *__restrict__ src, uint64_t (&r)[L0Units<BITS, TILE, T>::kPer]) {
+    using U = L0Units<BITS, TILE, T>;
+    const uint64_t *s8 = reinterpret_cast<const uint64_t *>(src);
+#pragma unroll
+    for (int j = 0; j < U::kPer; ++j) r[j] = s8[min((uint32_t)(threadIdx.x + j * T), (uint32_t)U::kUnits - 1)];
 }
 
-// s_dol bit = the position ends k-mers: '$' (or, acgt_only, any byte outside ACGT)
-template <int BITS, int TILE>
-__device__ __forceinline__ void l0_pack(const uint4 &ra, const uint4 &rb, uint64_t *s_code, uint32_t *s_dol,
-                                        const uint8_t *lut4, int acgt_only = 0) {
+// SWAR over 8 bytes (byte 0 = the first position): bit 7 of each byte set iff the byte is zero
+__device__ __forceinline__ uint64_t zero_bytes(uint64_t y) {
+    constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full;
+    return ~(((y & k7F) + k7F) | y | k7F);
+}
+
+// the 8 flag bits (bit 7 of each byte) as one byte, position 0 in the most significant bit
+__device__ __forceinline__ uint32_t gather_flags8(uint64_t z) {
+    uint64_t t = __builtin_bswap64(z) >> 7;
+    t = (t | (t >> 7)) & 0x0003000300030003ull;
+    t = (t | (t >> 14)) & 0x0000000F0000000Full;
+    return (uint32_t)((t | (t >> 28)) & 0xFFu);
+}
+
+// 2-bit codes (A0 C1 G2 T3) of 8 bytes as 16 bits, position 0 in the most significant pair
+__device__ __forceinline__ uint32_t pack2_8(uint64_t x) {
+    uint64_t t = __builtin_bswap64(((x >> 1) ^ (x >> 2)) & 0x0303030303030303ull);
+    t = (t | (t >> 6)) & 0x000F000F000F000Full;
+    t = (t | (t >> 12)) & 0x000000FF000000FFull;
+    return (uint32_t)((t | (t >> 24)) & 0xFFFFu);
+}
+
+// s_dol bit = the position ends k-mers: '$' (or, acgt_only, any byte outside ACGT).  Every thread
+// packs its 8-byte units: 2-bit codes into 16-bit (4-bit: 32-bit) pieces of the MSB-first code
+// words, stop flags into bytes of the 32-position mask words.
+template <int BITS, int TILE, int T>
+__device__ __forceinline__ void l0_pack(const uint64_t (&r)[L0Units<BITS, TILE, T>::kPer], uint64_t *s_code,
+                                        uint32_t *s_dol, const uint8_t *lut4, int acgt_only = 0) {
+    using U = L0Units<BITS, TILE, T>;
     using P = L0Pack<BITS, TILE>;
-    const int g = threadIdx.x;
-    if (g < P::kGroups) {
-        const uint32_t wv[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-        uint64_t c0 = 0, c1 = 0;
-        uint32_t dm = 0;
+    constexpr uint64_t kOnes = 0x0101010101010101ull;
 #pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            const uint32_t ch = (wv[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-            const bool stop = acgt_only ? !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T') : ch == GK_DOLLAR;
-            dm = (dm << 1) | (stop ? 1u : 0u);
+    for (int j = 0; j < U::kPer; ++j) {
+        const uint32_t u = threadIdx.x + j * T;
+        if (u < (uint32_t)U::kUnits) {
+            const uint64_t x = r[j];
+            uint64_t z;
+            if (acgt_only)
+                z = ~(zero_bytes(x ^ (kOnes * 'A')) | zero_bytes(x ^ (kOnes * 'C')) | zero_bytes(x ^ (kOnes * 'G')) |
+                      zero_bytes(x ^ (kOnes * 'T'))) & (kOnes << 7);
+            else
+                z = zero_bytes(x ^ (kOnes * GK_DOLLAR));
+            reinterpret_cast<uint8_t *>(s_dol)[(u & ~3u) + 3 - (u & 3u)] = (uint8_t)gather_flags8(z);
             if (BITS == 2) {
-                c0 = (c0 << 2) | (((ch >> 1) ^ (ch >> 2)) & 3u);
+                reinterpret_cast<uint16_t *>(s_code)[(u & ~3u) + 3 - (u & 3u)] = (uint16_t)pack2_8(x);
             } else {
-                const uint64_t v = lut4[ch];
-                if (q < 16) c0 = (c0 << 4) | v; else c1 = (c1 << 4) | v;
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) v = (v << 4) | lut4[(x >> (8 * b)) & 0xFFu];
+                reinterpret_cast<uint32_t *>(s_code)[(u & ~1u) + 1 - (u & 1u)] = v;
             }
         }
-        if (BITS == 2) {
-            s_code[g] = c0;
-        } else {
-            s_code[2 * g] = c0;
-            s_code[2 * g + 1] = c1;
-        }
-        s_dol[g] = dm;
     }
-    if (g == 0) s_code[P::kCodeWords - 1] = 0;
+    if (threadIdx.x == 0) s_code[P::kCodeWords - 1] = 0;
 }
 
 template <int BITS>
@@ -163,15 +196,15 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
     lds_barrier();
     const uint64_t P0 = a.lo + (uint64_t)blockIdx.x * TILE;
-    uint4 ra, rb;
-    l0_load<BITS, TILE>(a.sba + P0, ra, rb);
-    l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
+    uint64_t rr[L0Units<BITS, TILE, T>::kPer];
+    l0_load<BITS, TILE, T>(a.sba + P0, rr);
+    l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         const uint32_t p = i * T + t;
-        if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi)
-            atomicAdd(&s_hist[dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0)], 1u);
+        const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
+        if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
     }
     lds_barrier();
     for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
@@ -196,11 +229,12 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    lds_barrier();  // the LUT, read by every thread's pack
     const TileWalk walk(ntiles);
-    uint4 ra, rb;
+    uint64_t rr[L0Units<BITS, TILE, T>::kPer];
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
-        l0_load<BITS, TILE>(a.sba + a.lo + (uint64_t)t * TILE, ra, rb);
+        l0_load<BITS, TILE, T>(a.sba + a.lo + (uint64_t)t * TILE, rr);
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
     };
     if (walk.first < walk.end) load(walk.first);
@@ -209,7 +243,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
         lds_barrier();  // the previous tile's runs have been read out of LDS
         for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
         if (tid < RADIX) s_toff[tid] = toff;
-        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
+        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
         lds_barrier();
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         uint64_t key[I];
@@ -256,12 +290,13 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_stage + SM::kValOff);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    lds_barrier();  // the LUT, read by every thread's pack
     const TileWalk walk(ntiles);
-    uint4 ra, rb;
+    uint64_t rr[L0Units<BITS, TILE, T>::kPer];
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];
-        l0_load<BITS, TILE>(a.sba + a.lo + (uint64_t)t * TILE, ra, rb);
+        l0_load<BITS, TILE, T>(a.sba + a.lo + (uint64_t)t * TILE, rr);
     };
     uint32_t pcnt = 0;
     int cur = 0;
@@ -273,7 +308,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int u = 0; u < (RADIX + 63) / 64; ++u)
             if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
         if (tid < RADIX) s_toff[cur][tid] = toff;
-        l0_pack<BITS, TILE>(ra, rb, s_code, s_dol, s_lut4, a.acgt_only);
+        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
         for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
@@ -343,6 +378,146 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
         for (int g = 0; g < I; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Key-range shard select (gk_shard_sort_range)
+// ---------------------------------------------------------------------------------------------
+// A rank scans the WHOLE sequence and keeps the k-mers whose L0 digit lies in its range -- about
+// 1/N of them -- writing them contiguously in position order.  Two light streaming passes over
+// 4096-position tiles (small LDS and registers, so several workgroups per CU overlap their loads):
+//   STORE = false  kept k-mers per tile -> tile_cnt[t]          (then an exclusive scan)
+//   STORE = true   each wave compacts its kept k-mers with one ballot per row; the kept lanes of
+//                  a row store to consecutive addresses from tile_off[t]
+// Stable: tiles, waves, rows and lanes follow positions.  The kept k-mers then go through the
+// ordinary MSD levels as one bucket (the store pass writes their L0 digit bytes, so the first
+// level counts 1 byte per k-mer).
+constexpr int kST = 512, kSI = 8, kSTile = kST * kSI;  // 4096 positions per tile, 512 per wave
+constexpr int kSW = kST / 64;                          // waves per tile
+
+template <int BITS, bool CANON, bool STORE>
+__global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint32_t ntiles,
+                                                          uint32_t *__restrict__ wave_cnt,
+                                                          const uint32_t *__restrict__ wave_off,
+                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                          uint8_t *__restrict__ nd_out) {
+    using P = L0Pack<BITS, kSTile>;
+    constexpr int kStage = STORE ? kSTile : 1;  // per-wave staging of the kept (key, start): 512 each
+    __shared__ uint64_t s_code[P::kCodeWords];
+    __shared__ uint32_t s_dol[P::kGroups];
+    __shared__ uint8_t s_lut4[256];
+    __shared__ uint64_t s_skey[kStage];
+    __shared__ uint32_t s_sval[kStage];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t wslot = (uint64_t)t * kSW + wave;
+        const uint64_t P0 = a.lo + (uint64_t)t * kSTile;
+        uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
+        l0_load<BITS, kSTile, kST>(a.sba + P0, rr);
+        __syncthreads();  // the LUT; the previous tile's codes have been read
+        l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only);
+        __syncthreads();
+        if constexpr (BITS == 2 && !CANON) {
+            // 8 consecutive positions per thread: one 128-bit code window and one 64-position
+            // stop window serve all 8 keys (no per-position LDS reads)
+            const uint32_t q0 = tid * 8;
+            const uint32_t w0 = q0 >> 5, s0 = (q0 & 31) * 2;  // s0 in {0, 16, 32, 48}
+            const uint64_t A0 = s_code[w0], A1 = s_code[w0 + 1], A2 = s_code[w0 + 2];
+            const uint64_t T = s0 ? (A0 << s0) | (A1 >> (64 - s0)) : A0;   // symbols q0 ..
+            const uint64_t T2 = s0 ? (A1 << s0) | (A2 >> (64 - s0)) : A1;  // symbols q0 + 32 ..
+            const uint32_t ds = q0 & 31;                                     // in {0, 8, 16, 24}
+            const uint64_t D0 = ((uint64_t)s_dol[w0] << 32) | s_dol[w0 + 1];
+            const uint64_t D = ds ? (D0 << ds) | (s_dol[w0 + 2] >> (32 - ds)) : D0;  // stops q0 .. q0 + 63
+            const int64_t left = (int64_t)a.hi - (int64_t)(P0 + q0);
+            // the L0 digit is the top 7 bits of the key when the key has >= 8 bits: bits
+            // [25 - 2i, 32 - 2i) of the window's high half for position q0 + i
+            const uint32_t Th = (uint32_t)(T >> 32);
+            const bool top7 = d0.mask == 0x7Fu && (int)d0.shift == a.total_bits - 7 && a.symbols <= 56;
+            uint32_t keepm = 0;
+            if (top7 && __ballot(D != 0 || left < 8) == 0) {
+                // no stop in any window of the wave and no sequence end: ownership alone decides
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    keepm |= (l0_owned((Th >> (25 - 2 * i)) & 0x7Fu, a) ? 1u : 0u) << i;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint64_t Ti = i ? (T << (2 * i)) | (T2 >> (64 - 2 * i)) : T;
+                    const uint64_t k = a.total_bits >= 64 ? Ti : Ti >> (64 - a.total_bits);
+                    const uint64_t Di = D << i;
+                    const bool valid = a.symbols <= 56 ? (Di == 0 || (int)__clzll((long long)Di) >= a.symbols)
+                                                       : l0_valid(s_dol, q0 + i, a.symbols);
+                    const bool keep = valid && i < left && l0_owned(dg_of(k, d0), a);
+                    keepm |= (keep ? 1u : 0u) << i;
+                }
+            }
+            const uint32_t cnt = (uint32_t)__popc(keepm);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            if (!STORE) {
+                if (lane == 63) wave_cnt[wslot] = incl;
+                continue;
+            }
+            // stage the wave's kept k-mers in position order (keys only for them), then store them
+            // as one coalesced run
+            uint64_t *sk = s_skey + wave * 512;
+            uint32_t *sv = s_sval + wave * 512;
+            uint32_t j = incl - cnt;
+            for (uint32_t m = keepm; m; m &= m - 1) {
+                const int i = __ffs(m) - 1;
+                const uint64_t Ti = i ? (T << (2 * i)) | (T2 >> (64 - 2 * i)) : T;
+                sk[j] = a.total_bits >= 64 ? Ti : Ti >> (64 - a.total_bits);
+                sv[j] = (uint32_t)(P0 + q0 + i);
+                ++j;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            const uint64_t o = wave_off[wslot];
+            for (uint32_t e = lane; e < total; e += 64) {
+                const uint64_t k = sk[e];
+                kout[o + e] = k;
+                vout[o + e] = sv[e];
+                nd_out[o + e] = (uint8_t)dg_of(k, d0);
+            }
+        } else {
+            // one ballot per row of 64 positions
+            const uint32_t wbase = wave * (kSI * 64);
+            uint64_t key[kSI];
+            uint32_t at[kSI];
+            uint32_t keepm = 0, kept = 0;
+#pragma unroll
+            for (int i = 0; i < kSI; ++i) {
+                const uint32_t p = wbase + i * 64 + lane;
+                key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
+                const bool keep = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(dg_of(key[i], d0), a);
+                const uint64_t m = __ballot(keep);
+                at[i] = kept + lanes_below(m);
+                kept += (uint32_t)__popcll(m);
+                keepm |= (keep ? 1u : 0u) << i;
+            }
+            if (!STORE) {
+                if (lane == 0) wave_cnt[wslot] = kept;
+                continue;
+            }
+            const uint64_t base = wave_off[wslot];
+#pragma unroll
+            for (int i = 0; i < kSI; ++i) {
+                if ((keepm >> i) & 1u) {
+                    const uint64_t o = base + at[i];
+                    kout[o] = key[i];
+                    vout[o] = (uint32_t)(P0 + wbase + i * 64 + lane);
+                    nd_out[o] = (uint8_t)dg_of(key[i], d0);
+                }
+            }
+        }
     }
 }
 
@@ -1263,9 +1438,22 @@ struct MsdDriver {
     // kout / vout (capacity >= n + 1: element n is the scatter's sink).  seg_base / seg_cnt then
     // hold the kGRadix buckets.  *count: k-mers found (checked against cap before the scatter).
     int run_l0(uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout, uint64_t cap, uint64_t *count) {
+        int rc = l0_count(lo, hi, 0, 0xFFFFFFFFu, count);
+        if (rc != GK_OK) return rc;
+        return l0_partition(kout, vout, cap, *count);
+    }
+
+    // key-range shards: the L0 digit range [own_lo, own_lo + own_span) is kept (width(0) bits)
+    L0Args l0a{};
+    uint64_t l0_tiles = 0;
+
+    // L0 count pass: per-tile digit histograms of the kept k-mers starting in [lo, hi), their
+    // column scan (seg_base / seg_cnt), *count = k-mers kept
+    int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count) {
         const uint64_t span = hi > lo ? hi - lo : 0;
         const uint64_t nt0 = std::max<uint64_t>((span + kPTile - 1) / kPTile, 1);
         const uint64_t nc0 = (nt0 + kChunkTiles - 1) / kChunkTiles;
+        l0_tiles = nt0;
         int rc = tables(nt0, nc0, 1);
         if (rc != GK_OK) return rc;
         uint32_t *s_misc;
@@ -1282,7 +1470,10 @@ struct MsdDriver {
             GK_TRY_HIP(c, hipMemcpyAsync(s_misc, misc, 12, hipMemcpyHostToDevice, c->stream));
             GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         }
-        const L0Args a{c->sba, lo, hi, ks.symbols, B, ks.acgt_only};
+        L0Args a{c->sba, lo, hi, ks.symbols, B, ks.acgt_only};
+        a.own_lo = own_lo;
+        a.own_span = own_span;
+        l0a = a;
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
         timer_begin(c, "msd_l0_count", &slot);
@@ -1297,9 +1488,16 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemcpyAsync(&last[1], seg_cnt + (1 << w0) - 1, 4, hipMemcpyDeviceToHost, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         *count = (uint64_t)last[0] + last[1];
-        if (*count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
+        return GK_OK;
+    }
+
+    // L0 partition pass after l0_count (same tiles, same range)
+    int l0_partition(uint64_t *kout, uint32_t *vout, uint64_t cap, uint64_t count) {
+        if (count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
+        const int w0 = width(0);
+        const Dig d0 = dig_at(B, 0, w0);
         timer_begin(c, "msd_pass_l0", &slot);
-        timer_units(c, slot, *count);
+        timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
         const bool with_nd = kout == c->keys[0];
@@ -1308,7 +1506,7 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
-        l0_dispatch(false, w0, with_nd, a, d0, (unsigned)nt0, kout, vout, (uint32_t)nt0, *count, ndg);
+        l0_dispatch(false, w0, with_nd, l0a, d0, (unsigned)l0_tiles, kout, vout, (uint32_t)l0_tiles, count, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = with_nd;
@@ -1724,5 +1922,101 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
 }
 
 int msd_radix_bits() { return kGR; }
+
+// L0 digit width of the key-range shards: 7 bits for 2-bit keys (as msd_sort), 8 otherwise
+static int range_width(const KeySpec &ks) { return ks.bits == 2 ? 7 : kGR; }
+
+int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *hist, int *bits) {
+    MsdDriver d(c, ks);
+    d.B = ks.bits * std::min(ks.symbols, 64 / ks.bits);  // the first key word (see msd_sort)
+    d.wsched[0] = range_width(ks);
+    GK_TRY_HIP(c, msd_tables());
+    uint64_t cnt = 0;
+    int rc = d.l0_count(lo, hi, 0, 0xFFFFFFFFu, &cnt);
+    if (rc != GK_OK) return rc;
+    const int R = d.width(0);
+    std::vector<uint32_t> hc(1u << R);
+    GK_TRY_HIP(c, hipMemcpyAsync(hc.data(), d.seg_cnt, 4u << R, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < (1 << R); ++i) hist[i] = hc[i];
+    *bits = R;
+    return GK_OK;
+}
+
+int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t digit_hi, uint64_t *n_kept) {
+    const int spw = 64 / ks.bits;
+    const int nphase = (ks.symbols + spw - 1) / spw;
+    MsdDriver d(c, ks);
+    d.B = ks.bits * std::min(ks.symbols, spw);
+    d.wsched[0] = range_width(ks);
+    timer_begin(c, "msd_total", &d.total_slot);
+    GK_TRY_HIP(c, msd_tables());
+    const uint64_t L = c->sba_len;
+    const uint32_t ntiles = (uint32_t)std::max<uint64_t>((L + kSTile - 1) / kSTile, 1);
+    const uint64_t nw = (uint64_t)ntiles * kSW;
+    L0Args a{c->sba, 0, L, ks.symbols, d.B, ks.acgt_only};
+    a.own_lo = digit_lo;
+    a.own_span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
+    const Dig d0 = dig_at(d.B, 0, d.width(0));
+    uint32_t *wave_cnt, *wave_off;
+    GK_TRY_HIP(c, scratch(c, "sel_wave_cnt", nw + 1, &wave_cnt));
+    GK_TRY_HIP(c, scratch(c, "sel_wave_off", nw + 1, &wave_off));
+    c->n = 0;  // nothing in the buffers survives: ensure_elems copies none
+    c->cur = 0;
+    const unsigned sgrid = std::min<unsigned>(ntiles, d.cus * 6);
+    auto launch = [&](bool store) {
+        uint64_t *ko = store ? c->keys[0] : nullptr;
+        uint32_t *vo = store ? c->vals[0] : nullptr;
+        uint8_t *no = store ? d.nd : nullptr;
+#define GK_SEL(B_, C_, S_)                                                                                   \
+    hipLaunchKernelGGL((msd0_select_kernel<B_, C_, S_>), dim3(sgrid), dim3(kST), 0, c->stream, a, d0, ntiles,    \
+                       wave_cnt, wave_off, ko, vo, no)
+        if (ks.bits == 2 && ks.canonical) { if (store) GK_SEL(2, true, true); else GK_SEL(2, true, false); }
+        else if (ks.bits == 2) { if (store) GK_SEL(2, false, true); else GK_SEL(2, false, false); }
+        else if (ks.canonical) { if (store) GK_SEL(4, true, true); else GK_SEL(4, true, false); }
+        else { if (store) GK_SEL(4, false, true); else GK_SEL(4, false, false); }
+#undef GK_SEL
+    };
+    int slot;
+    timer_begin(c, "msd_select_count", &slot);
+    timer_units(c, slot, L);
+    launch(false);
+    GK_TRY_HIP(c, hipGetLastError());
+    uint64_t found = 0;
+    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, wave_cnt, nw, wave_off, &found));
+    timer_end(c, slot);
+    if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
+    int rc = ensure_elems(c, std::max<uint64_t>(found, 1), 1);
+    if (rc != GK_OK) return rc;
+    GK_TRY_HIP(c, scratch(c, "msd_nd", found + 64, &d.nd));
+    timer_begin(c, "msd_select", &slot);
+    timer_units(c, slot, found);
+    launch(true);
+    GK_TRY_HIP(c, hipGetLastError());
+    timer_end(c, slot);
+    *n_kept = found;
+    c->n = found;
+    if (found == 0) {
+        timer_end(c, d.total_slot);
+        return GK_OK;
+    }
+    uint8_t *nd_keep = d.nd;
+    rc = d.init(found);
+    if (rc != GK_OK) return rc;
+    d.nd = nd_keep;
+    d.nd_ready = true;  // the select wrote the L0 digit bytes
+    // the kept k-mers as one bucket [0, found) with no key bits sorted
+    uint32_t *one;
+    GK_TRY_HIP(c, scratch(c, "sel_bucket", 2, &one));
+    const uint32_t hb[2] = {0, (uint32_t)found};
+    GK_TRY_HIP(c, hipMemcpyAsync(one, hb, 8, hipMemcpyHostToDevice, c->stream));
+    rc = d.classify(1, 0, 0, 0, one, one + 1);
+    if (rc == GK_OK) rc = d.levels(0, 0, 0);
+    if (rc == GK_OK) rc = d.finish();
+    for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
+        rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));
+    timer_end(c, d.total_slot);
+    return rc;
+}
 
 }  // namespace gkm

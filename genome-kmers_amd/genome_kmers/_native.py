@@ -51,6 +51,7 @@ EXPORTED = (
     "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
+    "gk_shard_histogram", "gk_shard_sort_range",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
@@ -121,6 +122,10 @@ _SIGS = {
                             ctypes.c_uint64, _U64P, _U64P], ctypes.c_int),
     "gk_shard_sort": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _U64P, _U64P, _U32P,
                        ctypes.c_uint32], ctypes.c_int),
+    "gk_shard_histogram": ([_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _U64P, _U32P],
+                           ctypes.c_int),
+    "gk_shard_sort_range": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U64P],
+                            ctypes.c_int),
     "gk_fasta_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P), _U64P, _U64P, _U64P], ctypes.c_int),
     "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
     "gk_fasta_close": ([_P], None),
@@ -391,6 +396,23 @@ class Engine:
                                            _ptr(ln, ctypes.c_uint64),
                                            _ptr(bk, ctypes.c_uint32), len(bk)))
         self.n = n
+
+    def shard_histogram(self, lo: int, hi: int, k: int, canonical: bool = False):
+        """Top-digit histogram of the k-mers starting in [lo, hi): (numpy uint64[1 << bits], bits)."""
+        hist = np.zeros(256, dtype=np.uint64)
+        bits = ctypes.c_uint32(0)
+        self._check(self.lib.gk_shard_histogram(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
+                                                _ptr(hist, ctypes.c_uint64), ctypes.byref(bits)))
+        return hist[:1 << bits.value].copy(), bits.value
+
+    def shard_sort_range(self, k: int, digit_lo: int, digit_hi: int, canonical: bool = False) -> int:
+        """Sort the k-mers of the whole sequence whose top digit is in [digit_lo, digit_hi); returns
+        their number (the context then holds them as after sort(k))."""
+        n = ctypes.c_uint64(0)
+        self._check(self.lib.gk_shard_sort_range(self.ctx, k, SORT_CANONICAL if canonical else 0, digit_lo, digit_hi,
+                                                 ctypes.byref(n)))
+        self.n = n.value
+        return n.value
 
     def unique_count_only(self) -> int:
         g = ctypes.c_uint64(0)

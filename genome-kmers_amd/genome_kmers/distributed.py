@@ -176,3 +176,58 @@ class ShardedKmerSort:
         self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk, canonical=self.canonical)
         self.local_kmers = R
         return self.engine.unique_count_only()
+
+
+class KeyRangeKmerSort:
+    """One rank of the N-GPU sort with NO data exchange (the default multi-GPU path).
+
+    Every rank already holds the whole sequence byte array -- 1 byte per k-mer, against the
+    ~12 bytes per k-mer the all-to-all of ``ShardedKmerSort`` moves over xGMI.  So instead of
+    moving k-mers to their owner, each rank re-derives its own from the sequence:
+
+    1. ``shard_histogram``: top-digit histogram of the k-mers starting in the rank's position share;
+    2. ``all_reduce`` (sum) of the histograms -- 2 KiB, the only collective -- and the same split of
+       the digits into N contiguous ranges of about n/N k-mers on every rank (``split_buckets``);
+    3. ``shard_sort_range``: the rank scans the whole sequence, keeps the k-mers of its digit range
+       (compacted per wave before ranking, so the kept share sets the cost) and sorts them.
+
+    Rank r's sorted k-mers are the r-th slice of the single-GPU order (``Kmers.sort``,
+    kmers.py:1624-1652, with break_ties=True, kmers.py:1710-1711): digit ranges ascend with the
+    rank, and within a range the sort is the single-GPU sort restricted to it.
+    """
+
+    def __init__(self, sba: np.ndarray, seg_starts: np.ndarray, k: int, rank: int, world: int, device: int = 0,
+                 engine=None, torch_device=None, group=None, canonical: bool = False):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank, self.world, self.k = rank, world, k
+        self.canonical = canonical
+        self.dev = torch_device if torch_device is not None else torch.device("cuda", device)
+        if engine is None:
+            from genome_kmers import _native
+
+            engine = _native.Engine(device)
+        self.engine = engine
+        t0 = time.perf_counter()
+        self.engine.set_sequence(sba, seg_starts)
+        self.engine.sync()
+        self.h2d_ms = (time.perf_counter() - t0) * 1e3
+        bounds = position_ranges(len(sba), world)
+        self.lo, self.hi = bounds[rank], bounds[rank + 1]
+        self.total_kmers = count_kmers(len(sba), seg_starts, k)
+        self.local_kmers = 0
+        self.digit_bounds = None
+
+    def run(self) -> int:
+        """One sort; returns this rank's number of distinct k-mers."""
+        torch, dist = self.torch, self.dist
+        hist, bits = self.engine.shard_histogram(self.lo, self.hi, self.k, canonical=self.canonical)
+        h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to(self.dev)
+        dist.all_reduce(h, group=self.group)
+        bounds = split_buckets(h.cpu().numpy(), self.world)
+        self.digit_bounds = bounds
+        self.local_kmers = self.engine.shard_sort_range(self.k, bounds[self.rank], bounds[self.rank + 1],
+                                                        canonical=self.canonical)
+        return self.engine.unique_count_only()

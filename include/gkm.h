@@ -190,6 +190,24 @@ int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts,
                   uint32_t flags, const uint64_t *h_piece_off, const uint64_t *h_piece_len, const uint32_t *h_piece_bucket,
                   uint32_t npieces);
 
+/*
+ * Key-range shards: multi-GPU with NO data exchange.  Every rank holds the whole sba (as in the
+ * all-to-all scheme above); rank r keeps the k-mers whose top key digit lies in its digit range and
+ * sorts them, so the ranks' outputs concatenated in rank order are the single-GPU gk_sort order
+ * (kmers.py:1624-1652 with break_ties=True, kmers.py:1710-1711).  Replaces the same reference call
+ * as gk_sort; the reference has no multi-process path.
+ * gk_shard_histogram: histogram of the top *bits key bits (h_hist[256], entries >= 1 << *bits are
+ * 0) of the fixed-length k-mers starting in [lo, hi) (lo a multiple of 32) -- each rank counts its
+ * position share, the caller sums the histograms over ranks (a 2 KiB all-reduce) and cuts the
+ * digits into contiguous ranges of about n / N k-mers.
+ * gk_shard_sort_range: sort every k-mer of the sba whose top digit d has digit_lo <= d < digit_hi;
+ * *n_kept receives their number and the context then holds them as after gk_sort(k).
+ */
+int gk_shard_histogram(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
+                       uint32_t *bits);
+int gk_shard_sort_range(gk_ctx *ctx, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                        uint64_t *n_kept);
+
 /* Location of selected k-mers for Kmers.get_kmers(kmer_info_to_yield="full") (kmers.py:1180-1264):
  * sba_idx[i] = kmer_sba_start_indices[kmer_nums[i]] and seg[i] = the segment holding it
  * (bisect_right over the segment starts, sequence_collection.py:76-97), computed on the device

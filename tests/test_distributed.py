@@ -87,6 +87,29 @@ class NumpyShardEngine:
         order = np.argsort(key, kind="stable")  # the device sort is stable in piece order
         self.keys, self.starts = key[order], st[order]
 
+    # key-range contract (gk_shard_histogram / gk_shard_sort_range): 7-bit top digits of 2-bit keys
+    range_bits = 7
+
+    def _top(self, key, k):
+        return (key >> np.uint64(max(0, 2 * k - self.range_bits))).astype(np.int64)
+
+    def shard_histogram(self, lo, hi, k, canonical=False):
+        assert not canonical
+        s = _valid_starts(self.sba, self.seg, k, lo, hi)
+        return np.bincount(self._top(_keys(self.sba, s, k), k), minlength=1 << self.range_bits).astype(np.uint64), \
+            self.range_bits
+
+    def shard_sort_range(self, k, dlo, dhi, canonical=False):
+        assert not canonical
+        s = _valid_starts(self.sba, self.seg, k, 0, len(self.sba))
+        key = _keys(self.sba, s, k)
+        top = self._top(key, k)
+        keep = (top >= dlo) & (top < dhi)
+        key, s = key[keep], s[keep]
+        order = np.argsort(key, kind="stable")  # the device sort is stable in start order
+        self.keys, self.starts = key[order], s[order]
+        return len(s)
+
     def unique_count_only(self):
         return int(len(np.unique(self.keys)))
 
@@ -139,7 +162,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, sba, seg, k, q, chunk):
+def _worker(rank, world, port, sba, seg, k, q, chunk, scheme="a2a"):
     import torch
     import torch.distributed as dist
 
@@ -147,16 +170,21 @@ def _worker(rank, world, port, sba, seg, k, q, chunk):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        job = D.ShardedKmerSort(sba, seg, k, rank, world, engine=NumpyShardEngine(), torch_device=torch.device("cpu"),
-                                chunk=chunk)
+        if scheme == "range":
+            job = D.KeyRangeKmerSort(sba, seg, k, rank, world, engine=NumpyShardEngine(),
+                                     torch_device=torch.device("cpu"))
+        else:
+            job = D.ShardedKmerSort(sba, seg, k, rank, world, engine=NumpyShardEngine(),
+                                    torch_device=torch.device("cpu"), chunk=chunk)
         n_unique = job.run()
         q.put((rank, job.engine.starts.tolist(), n_unique, job.total_kmers, job.local_kmers))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("contigs,chunk", [(1, None), (3, None), (1, 5000)])
-def test_gloo_world2_matches_oracle(contigs, chunk):
+@pytest.mark.parametrize("scheme,contigs,chunk", [("a2a", 1, None), ("a2a", 3, None), ("a2a", 1, 5000),
+                                                  ("range", 1, None), ("range", 3, None)])
+def test_gloo_world2_matches_oracle(scheme, contigs, chunk):
     import torch.multiprocessing as mp
 
     from oracle import oracle
@@ -168,7 +196,7 @@ def test_gloo_world2_matches_oracle(contigs, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sba, seg, K, q, chunk)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sba, seg, K, q, chunk, scheme)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in procs)
@@ -231,6 +259,46 @@ def test_gpu_shards_concatenate_to_single_sort(world, contigs, k, canonical, iup
         e.shard_sort(rk, rv, R, k, off, ln, bk, canonical=canonical)
         got.append(e.copy_starts())
         uniq += e.unique_count_only()
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(k)
+    ref.sort(k, canonical=canonical)
+    np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
+    assert uniq == ref.unique_count_only()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
+    (2, 1, 31, False, False), (3, 4, 31, False, False), (8, 1, 31, False, False), (2, 3, 63, False, False),
+    (3, 2, 31, True, False), (2, 2, 63, True, True), (2, 1, 40, False, True), (4, 2, 21, False, False)])
+def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac):
+    """gk_shard_histogram / gk_shard_sort_range for every rank of a world in one process: the
+    ranks' sorted starts, concatenated in rank order, equal gk_sort on the whole input."""
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(200_000 + 17, 3 + world, contigs)
+    sba[150_100:151_000] = sba[1000:1900]  # repeats in different position shares
+    sba[160_000:160_900] = oracle.reverse_complement(sba[1000:1900])
+    if iupac:
+        sba[5000:5100] = ord("N")
+        sba[90_000:90_050:7] = ord("R")
+    bounds = D.position_ranges(len(sba), world)
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    hist = None
+    for r in range(world):
+        h, bits = e.shard_histogram(bounds[r], bounds[r + 1], k, canonical=canonical)
+        hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
+    assert bits == (7 if not iupac else 8)
+    total = D.count_kmers(len(sba), seg, k)
+    assert int(hist.sum()) == total
+    db = D.split_buckets(hist, world)
+    got, uniq, kept = [], 0, 0
+    for r in range(world):
+        kept += e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
+        got.append(e.copy_starts())
+        uniq += e.unique_count_only()
+    assert kept == total
     ref = _native.Engine(0)
     ref.set_sequence(sba, seg)
     ref.enumerate(k)

@@ -1,0 +1,96 @@
+"""Per-rank cost of the key-range multi-GPU scheme, measured on ONE GPU.
+
+The key-range scheme (genome_kmers.distributed.KeyRangeKmerSort) has no inter-GPU data path: rank
+r's work is gk_shard_histogram over its position share plus gk_shard_sort_range over its digit
+range.  Running every rank's share one after another on a single MI355X therefore measures each
+rank's device time exactly; only the 2 KiB all-reduce is missing.  Prints one JSON line per N.
+
+Usage: python tools/range_emulate.py [--genome-len L] [--worlds 1,2,4,8] [--reps 2]
+"""
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "genome-kmers_amd"))
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--genome-len", type=int, default=3_100_000_000)
+    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--worlds", type=str, default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+
+    import bench
+    from genome_kmers import _native
+    from genome_kmers import distributed as D
+
+    sba, seg = bench.make_genome(args.genome_len, 42), np.zeros(1, dtype=np.uint32)
+    k = args.k
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    e.sync()
+    total = D.count_kmers(len(sba), seg, k)
+    # single-GPU reference step for the same engine
+    e.enumerate(k)
+    e.sort(k)
+    e.unique_count_only()
+    e.sync()
+    t0 = time.perf_counter()
+    e.enumerate(k)
+    e.sort(k)
+    u1 = e.unique_count_only()
+    e.sync()
+    single_ms = (time.perf_counter() - t0) * 1e3
+    print(json.dumps({"single_gpu_ms": round(single_ms, 2), "kmers": total, "unique": u1}), flush=True)
+    for world in [int(x) for x in args.worlds.split(",")]:
+        pb = D.position_ranges(len(sba), world)
+        per_rank = []
+        uniq = 0
+        kept = 0
+        stages = None
+        # the all-reduced histogram (every rank's share), outside the per-rank timings
+        full = np.zeros(256, dtype=np.int64)
+        for s in range(world):
+            h, bits = e.shard_histogram(pb[s], pb[s + 1], k)
+            full[:len(h)] += h.astype(np.int64)
+        db = D.split_buckets(full[:1 << bits], world)
+        for r in range(world):
+            best = None
+            for rep in range(args.reps + 1):  # the first one warms up
+                e.sync()
+                e.profile_enable(rep == args.reps)
+                t0 = time.perf_counter()
+                e.shard_histogram(pb[r], pb[r + 1], k)  # the rank's own share (its part of the all-reduce)
+                n = e.shard_sort_range(k, db[r], db[r + 1])
+                u = e.unique_count_only()
+                e.sync()
+                dt = time.perf_counter() - t0
+                if rep == args.reps:
+                    rep_stages = e.profile_report()
+                e.profile_enable(False)
+                if rep > 0 and (best is None or dt < best):
+                    best = dt
+            if not per_rank or best * 1e3 > max(per_rank):
+                stages = {name: round(v["total_ms"], 3) for name, v in rep_stages.items()}
+            per_rank.append(round(best * 1e3, 2))
+            uniq += u
+            kept += n
+        assert kept == total, (kept, total)
+        worst = max(per_rank)
+        print(json.dumps({"world": world, "per_rank_ms": per_rank, "max_rank_ms": worst,
+                          "kmers_per_s": round(total / (worst * 1e-3), 1),
+                          "speedup_vs_single": round(single_ms / worst, 2), "unique": uniq,
+                          "slowest_rank_stages_ms": stages}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -305,3 +305,46 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     ref.sort(k, canonical=canonical)
     np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
     assert uniq == ref.unique_count_only()
+
+
+def _gpu_range_worker(rank, world, port, sba, seg, k, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        job = D.KeyRangeKmerSort(sba, seg, k, rank, world, device=0, torch_device=torch.device("cpu"))
+        u = job.run()
+        q.put((rank, job.engine.copy_starts().tolist(), u, job.local_kmers))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_key_range_two_processes():
+    """Two ranks as separate processes (gloo for the 2 KiB all-reduce), each with its own libgkm
+    engine on GPU 0: the rank-ordered concatenation equals the single-GPU sort."""
+    import torch.multiprocessing as mp
+
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(300_000 + 5, 11, 3)
+    sba[200_000:201_000] = sba[2000:3000]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_range_worker, args=(r, 2, port, sba, seg, 31, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(31)
+    ref.sort(31)
+    np.testing.assert_array_equal(np.concatenate([np.asarray(r[1], dtype=np.uint32) for r in res]), ref.copy_starts())
+    assert sum(r[2] for r in res) == ref.unique_count_only()

@@ -138,9 +138,16 @@ __global__ __launch_bounds__(256) void b_group_pos_kernel(const uint8_t *__restr
     }
 }
 
-// number of entries of the ascending array v[0..n) that are < x (lower) or <= x (upper)
-__device__ __forceinline__ uint64_t bound(const uint32_t *v, uint64_t n, uint64_t x, bool upper) {
-    uint64_t lo = 0, hi = n;
+// A element i goes to i + (B elements of the groups with pos <= i); it starts a group if its A
+// predecessor does not share its k-mer or a B group lands right before it.  One workgroup per
+// 4096 A elements: the group positions are sorted and there are few of them (thousands against
+// billions of A elements), so almost every workgroup sees none inside its range and moves its
+// elements by one constant shift -- a streaming copy; the rest search only the few positions
+// inside their range.
+constexpr int kMT = 256, kMI = 16, kMTile = kMT * kMI;
+
+// number of entries of the ascending v[lo, hi) that are < x (lower) or <= x (upper), plus lo
+__device__ __forceinline__ uint64_t bound_in(const uint32_t *v, uint64_t lo, uint64_t hi, uint64_t x, bool upper) {
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
         if (upper ? (uint64_t)v[mid] <= x : (uint64_t)v[mid] < x) lo = mid + 1;
@@ -149,30 +156,55 @@ __device__ __forceinline__ uint64_t bound(const uint32_t *v, uint64_t n, uint64_
     return lo;
 }
 
-// A element i goes to i + (B elements of the groups with pos <= i); it starts a group if its A
-// predecessor does not share its k-mer or a B group lands right before it
-__global__ __launch_bounds__(256) void merge_a_kernel(const uint32_t *__restrict__ a_starts,
+__global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict__ a_starts,
                                                       const uint8_t *__restrict__ a_heads, uint64_t nA,
                                                       const uint32_t *__restrict__ pos,
                                                       const uint32_t *__restrict__ g_first, uint64_t G, uint64_t nB,
                                                       uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nA; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t ub = bound(pos, G, i, true);
-        const uint64_t lb = ub > 0 && pos[ub - 1] == i ? bound(pos, G, i, false) : ub;
+    __shared__ uint64_t s_g[3];  // ub(i0), lb(i0), groups with pos < i1
+    const uint64_t i0 = (uint64_t)blockIdx.x * kMTile;
+    const uint64_t i1 = min(i0 + kMTile, nA);
+    if (threadIdx.x == 0) {
+        s_g[0] = bound_in(pos, 0, G, i0, true);
+        s_g[1] = bound_in(pos, 0, s_g[0], i0, false);
+        s_g[2] = bound_in(pos, s_g[0], G, i1, false);
+    }
+    __syncthreads();
+    const uint64_t g0 = s_g[0], lb0 = s_g[1], g1 = s_g[2];
+    if (g1 == g0) {  // no B group lands inside (i0, i1): one shift for the whole range
+        const uint64_t shift = g0 < G ? g_first[g0] : nB;
+        for (uint64_t i = i0 + threadIdx.x; i < i1; i += kMT) {
+            out[i + shift] = a_starts[i];
+            out_heads[i + shift] = (a_heads[i] || (i == i0 && g0 > lb0)) ? 1 : 0;
+        }
+        return;
+    }
+    for (uint64_t i = i0 + threadIdx.x; i < i1; i += kMT) {
+        const uint64_t ub = bound_in(pos, g0, g1, i, true);
+        const uint64_t lb = i == i0 ? lb0 : bound_in(pos, g0, ub, i, false);
         const uint64_t shift = ub < G ? g_first[ub] : nB;
         out[i + shift] = a_starts[i];
         out_heads[i + shift] = (a_heads[i] || ub > lb) ? 1 : 0;
     }
 }
 
-// B element j of group g goes to j + pos[g]
-__global__ __launch_bounds__(256) void merge_b_kernel(const uint32_t *__restrict__ b_starts,
+// B element j of group g goes to j + pos[g]; per 4096 B elements, the groups they span
+__global__ __launch_bounds__(kMT) void merge_b_kernel(const uint32_t *__restrict__ b_starts,
                                                       const uint8_t *__restrict__ b_heads, uint64_t nB,
                                                       const uint32_t *__restrict__ pos,
                                                       const uint32_t *__restrict__ g_first, uint64_t G,
                                                       uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads) {
-    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < nB; j += (uint64_t)gridDim.x * 256) {
-        const uint64_t g = bound(g_first, G, j, true) - 1;
+    __shared__ uint64_t s_g[2];  // group of j0, groups starting at or before j1 - 1
+    const uint64_t j0 = (uint64_t)blockIdx.x * kMTile;
+    const uint64_t j1 = min(j0 + kMTile, nB);
+    if (threadIdx.x == 0) {
+        s_g[0] = bound_in(g_first, 0, G, j0, true) - 1;
+        s_g[1] = bound_in(g_first, s_g[0], G, j1 - 1, true);
+    }
+    __syncthreads();
+    const uint64_t ga = s_g[0], gb = s_g[1];
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += kMT) {
+        const uint64_t g = gb == ga + 1 ? ga : bound_in(g_first, ga, gb, j, true) - 1;
         out[j + pos[g]] = b_starts[j];
         out_heads[j + pos[g]] = b_heads[j];
     }
@@ -279,10 +311,10 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     GK_TRY_HIP(c, hipGetLastError());
     uint8_t *hd;
     GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
-    hipLaunchKernelGGL(merge_a_kernel, dim3(grid_of_n(nA)), dim3(256), 0, c->stream, c->vals[0], c->heads, nA, pos,
-                       g_first, G, nB, c->vals[1], hd);
-    hipLaunchKernelGGL(merge_b_kernel, dim3(grid_of_n(nB)), dim3(256), 0, c->stream, b_st[bres], b_heads, nB, pos,
-                       g_first, G, c->vals[1], hd);
+    hipLaunchKernelGGL(merge_a_kernel, dim3((unsigned)((nA + kMTile - 1) / kMTile)), dim3(kMT), 0, c->stream,
+                       c->vals[0], c->heads, nA, pos, g_first, G, nB, c->vals[1], hd);
+    hipLaunchKernelGGL(merge_b_kernel, dim3((unsigned)((nB + kMTile - 1) / kMTile)), dim3(kMT), 0, c->stream,
+                       b_st[bres], b_heads, nB, pos, g_first, G, c->vals[1], hd);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     c->cur = 1;

@@ -318,6 +318,9 @@ def _gpu_range_worker(rank, world, port, sba, seg, k, q):
         job = D.KeyRangeKmerSort(sba, seg, k, rank, world, device=0, torch_device=torch.device("cpu"))
         u = job.run()
         q.put((rank, job.engine.copy_starts().tolist(), u, job.local_kmers))
+    except Exception as exc:  # report instead of leaving the parent waiting
+        q.put((rank, repr(exc), None, None))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -331,7 +334,7 @@ def test_gpu_key_range_two_processes():
     from genome_kmers import _native
 
     sba, seg = _random_sba(300_000 + 5, 11, 3)
-    sba[200_000:201_000] = sba[2000:3000]
+    sba[250_000:251_000] = sba[2000:3000]  # a repeat across contigs (inside the third one)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -341,7 +344,8 @@ def test_gpu_key_range_two_processes():
     res = sorted(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+    assert all(r[2] is not None for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
     ref = _native.Engine(0)
     ref.set_sequence(sba, seg)
     ref.enumerate(31)

@@ -182,6 +182,58 @@ __device__ __forceinline__ bool l0_valid(const uint32_t *s_dol, uint32_t p, int 
     return (x >> 32) == 0 && (y >> (96 - S)) == 0;
 }
 
+// Eight consecutive positions q0 .. q0 + 7 (q0 % 8 == 0) of a packed 2-bit tile from one 128-bit
+// code window and one 64-position stop window: keep mask (valid, before a.hi, owned) and the keys
+// (only if `keys`) or the L0 digits.  When no lane of the wave sees a stop or the sequence end and
+// the L0 digit is the top 7 bits of a key of >= 8 bits, the digits come straight from the window's
+// high half (bits [25 - 2i, 32 - 2i)) -- a shift, a mask and a compare per position.
+struct Win8 {
+    uint64_t T, T2;  // symbols q0 .., q0 + 32 ..
+    uint64_t D;      // stops q0 .. q0 + 63, MSB first
+};
+
+__device__ __forceinline__ Win8 win8_load(const uint64_t *s_code, const uint32_t *s_dol, uint32_t q0) {
+    const uint32_t w0 = q0 >> 5, s0 = (q0 & 31) * 2;  // s0 in {0, 16, 32, 48}
+    const uint64_t A0 = s_code[w0], A1 = s_code[w0 + 1], A2 = s_code[w0 + 2];
+    Win8 w;
+    w.T = s0 ? (A0 << s0) | (A1 >> (64 - s0)) : A0;
+    w.T2 = s0 ? (A1 << s0) | (A2 >> (64 - s0)) : A1;
+    const uint32_t ds = q0 & 31;  // in {0, 8, 16, 24}
+    const uint64_t D0 = ((uint64_t)s_dol[w0] << 32) | s_dol[w0 + 1];
+    w.D = ds ? (D0 << ds) | (s_dol[w0 + 2] >> (32 - ds)) : D0;
+    return w;
+}
+
+__device__ __forceinline__ uint64_t win8_key(const Win8 &w, int i, int B) {
+    const uint64_t Ti = i ? (w.T << (2 * i)) | (w.T2 >> (64 - 2 * i)) : w.T;
+    return B >= 64 ? Ti : Ti >> (64 - B);
+}
+
+// wave-uniform call (a ballot inside)
+__device__ __forceinline__ uint32_t win8_keep(const Win8 &w, const L0Args &a, Dig d0, int64_t left,
+                                              const uint32_t *s_dol, uint32_t q0, uint32_t (&dig)[8]) {
+    const uint32_t Th = (uint32_t)(w.T >> 32);
+    const bool top7 = d0.mask == 0x7Fu && (int)d0.shift == a.total_bits - 7 && a.symbols <= 56;
+    uint32_t keepm = 0;
+    if (top7 && __ballot(w.D != 0 || left < 8) == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            dig[i] = (Th >> (25 - 2 * i)) & 0x7Fu;
+            keepm |= (l0_owned(dig[i], a) ? 1u : 0u) << i;
+        }
+        return keepm;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        dig[i] = dg_of(win8_key(w, i, a.total_bits), d0);
+        const uint64_t Di = w.D << i;
+        const bool valid = a.symbols <= 56 ? (Di == 0 || (int)__clzll((long long)Di) >= a.symbols)
+                                           : l0_valid(s_dol, q0 + i, a.symbols);
+        keepm |= ((valid && i < left && l0_owned(dig[i], a)) ? 1u : 0u) << i;
+    }
+    return keepm;
+}
+
 template <int BITS, int T, int I, int R, bool CANON = false>
 __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_t *__restrict__ tile_hist) {
     constexpr int TILE = T * I;
@@ -200,11 +252,24 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     l0_load<BITS, TILE, T>(a.sba + P0, rr);
     l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
     lds_barrier();
+    if constexpr (BITS == 2 && !CANON) {  // 8 consecutive positions per thread (Win8)
+        static_assert(TILE % 8 == 0 && (TILE / 8) % 64 == 0, "whole waves per round");
+        for (uint32_t g = t; g < TILE / 8; g += T) {
+            const uint32_t q0 = g * 8;
+            const Win8 w = win8_load(s_code, s_dol, q0);
+            uint32_t dig[8];
+            const uint32_t keepm = win8_keep(w, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const uint32_t p = i * T + t;
-        const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
-        if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+            for (int i = 0; i < 8; ++i)
+                if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i]], 1u);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = i * T + t;
+            const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
+            if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+        }
     }
     lds_barrier();
     for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
@@ -314,6 +379,12 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         lds_barrier();  // packed codes visible
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
+        // a tile without stops that ends before a.hi: every position starts a k-mer (wave-uniform)
+        uint32_t anystop = 0;
+#pragma unroll
+        for (int j = 0; j < (P::kGroups + 63) / 64; ++j)
+            anystop |= s_dol[min((uint32_t)(j * 64 + lane), (uint32_t)P::kGroups - 1)];
+        const bool clean = __ballot(anystop != 0) == 0 && P0 + TILE <= a.hi;
         uint64_t key[I];
         uint32_t val[I], dig[I], rank[I];
         bool valid[I];
@@ -322,7 +393,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = p0 + i * 64;
-            valid[i] = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi;
+            valid[i] = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
             key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
             val[i] = (uint32_t)(P0 + p);
         }
@@ -420,39 +491,11 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
         l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only);
         __syncthreads();
         if constexpr (BITS == 2 && !CANON) {
-            // 8 consecutive positions per thread: one 128-bit code window and one 64-position
-            // stop window serve all 8 keys (no per-position LDS reads)
+            // 8 consecutive positions per thread (Win8)
             const uint32_t q0 = tid * 8;
-            const uint32_t w0 = q0 >> 5, s0 = (q0 & 31) * 2;  // s0 in {0, 16, 32, 48}
-            const uint64_t A0 = s_code[w0], A1 = s_code[w0 + 1], A2 = s_code[w0 + 2];
-            const uint64_t T = s0 ? (A0 << s0) | (A1 >> (64 - s0)) : A0;   // symbols q0 ..
-            const uint64_t T2 = s0 ? (A1 << s0) | (A2 >> (64 - s0)) : A1;  // symbols q0 + 32 ..
-            const uint32_t ds = q0 & 31;                                     // in {0, 8, 16, 24}
-            const uint64_t D0 = ((uint64_t)s_dol[w0] << 32) | s_dol[w0 + 1];
-            const uint64_t D = ds ? (D0 << ds) | (s_dol[w0 + 2] >> (32 - ds)) : D0;  // stops q0 .. q0 + 63
-            const int64_t left = (int64_t)a.hi - (int64_t)(P0 + q0);
-            // the L0 digit is the top 7 bits of the key when the key has >= 8 bits: bits
-            // [25 - 2i, 32 - 2i) of the window's high half for position q0 + i
-            const uint32_t Th = (uint32_t)(T >> 32);
-            const bool top7 = d0.mask == 0x7Fu && (int)d0.shift == a.total_bits - 7 && a.symbols <= 56;
-            uint32_t keepm = 0;
-            if (top7 && __ballot(D != 0 || left < 8) == 0) {
-                // no stop in any window of the wave and no sequence end: ownership alone decides
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    keepm |= (l0_owned((Th >> (25 - 2 * i)) & 0x7Fu, a) ? 1u : 0u) << i;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint64_t Ti = i ? (T << (2 * i)) | (T2 >> (64 - 2 * i)) : T;
-                    const uint64_t k = a.total_bits >= 64 ? Ti : Ti >> (64 - a.total_bits);
-                    const uint64_t Di = D << i;
-                    const bool valid = a.symbols <= 56 ? (Di == 0 || (int)__clzll((long long)Di) >= a.symbols)
-                                                       : l0_valid(s_dol, q0 + i, a.symbols);
-                    const bool keep = valid && i < left && l0_owned(dg_of(k, d0), a);
-                    keepm |= (keep ? 1u : 0u) << i;
-                }
-            }
+            const Win8 win = win8_load(s_code, s_dol, q0);
+            uint32_t dig[8];
+            const uint32_t keepm = win8_keep(win, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
             const uint32_t cnt = (uint32_t)__popc(keepm);
             uint32_t incl = cnt;
 #pragma unroll
@@ -471,8 +514,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             uint32_t j = incl - cnt;
             for (uint32_t m = keepm; m; m &= m - 1) {
                 const int i = __ffs(m) - 1;
-                const uint64_t Ti = i ? (T << (2 * i)) | (T2 >> (64 - 2 * i)) : T;
-                sk[j] = a.total_bits >= 64 ? Ti : Ti >> (64 - a.total_bits);
+                sk[j] = win8_key(win, i, a.total_bits);
                 sv[j] = (uint32_t)(P0 + q0 + i);
                 ++j;
             }

@@ -995,10 +995,8 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
                                                       uint32_t *__restrict__ ctr, int skip) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
-    __shared__ uint32_t s_v[CAP + 1];
     __shared__ uint64_t s_mask[256];
     __shared__ uint32_t s_cnt[257];  // digit counts, then exclusive starts (s_cnt[256] = total)
-    __shared__ uint8_t s_hd[CAP + 1];
     const int lane = threadIdx.x;
     const uint64_t me_bit = 1ull << lane;
     uint32_t idx = blockIdx.x;
@@ -1133,20 +1131,28 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
                 route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
             }
         }
+        // write-back straight from registers: the bucket spans a few cache lines, so the
+        // scattered stores of a wave combine in L2 (no LDS staging); the next bucket's loads are
+        // issued first so they fly during the stores
+        uint64_t wk[I];
+        uint32_t wv[I], wo[I];
+        uint8_t wh[I];
+        bool wl[I];
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            if (i >= live) continue;
-            s_k[out[i]] = key[i];
-            s_v[out[i]] = val[i];
-            s_hd[out[i]] = hd[i];  // 0 / 1: final (not) a group head; 2: re-listed
+            wl[i] = i < live && valid[i];
+            wk[i] = key[i];
+            wv[i] = val[i];
+            wo[i] = out[i];
+            wh[i] = hd[i] & 1;  // 0 / 1: final (not) a group head; a re-listed one is redone later
         }
-        local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket's loads fly now
+        local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            const uint32_t p = min((uint32_t)(i * 64 + lane), len - 1);
-            if (relist) k0[st + p] = s_k[p];  // keys only for a bucket with re-listed elements
-            v0[st + p] = s_v[p];
-            heads[st + p] = s_hd[p] & 1;
+            if (!wl[i]) continue;
+            if (relist) k0[st + wo[i]] = wk[i];  // keys only for a bucket with re-listed elements
+            v0[st + wo[i]] = wv[i];
+            heads[st + wo[i]] = wh[i];
         }
     }
 }

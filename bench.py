@@ -244,9 +244,15 @@ def main():
     # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4
     seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
 
+    range_mode = dist is not None and args.exchange == "range"
+
     def stage_bytes(name, v):
         u = v.get("units", 0)
-        if name == "msd_pass_l0":
+        if name == "msd_select_count":
+            return u  # key-range shards: the whole sequence, 1 B per position
+        if name == "msd_select":
+            return L * v["count"] + 13 * u  # the whole sequence in; kept (key, start, digit) out
+        if name == "msd_pass_l0" and not range_mode:
             return seq_bytes * v["count"] + 12 * u  # sequence bytes in, (key, start) out
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out

@@ -1,25 +1,26 @@
 """Multi-GPU k-mer sort: one process per GPU under torch.distributed.
 
 The reference sorts in one process (``Kmers.sort``, kmers.py:1624-1652); this module is one rank's
-share of the same result on N GPUs.  Every rank holds the whole sequence byte array in HBM and
-owns the k-mers that START in its position range [lo_r, lo_r+1): ranges are cut at multiples of
-32 bases, and a k-mer near hi reads up to k-1 bases past it (the halo), so no k-mer is lost or
-duplicated.  One run:
+share of the same result on N GPUs.  Every rank holds the whole sequence byte array in HBM and owns
+one contiguous range of top key digits, so the ranks' sorted starts, concatenated in rank order,
+are ``Kmers.sort``'s order with ``break_ties=True`` (kmers.py:1710-1711) -- the single-GPU order --
+and unique counts stay local (equal keys share a digit).  Two drivers:
 
-1. ``shard_partition``: the rank encodes its k-mers and partitions them stably by the top
-   ``bits`` (8) key bits -- the MSD sort's first level -- into a torch-owned send buffer;
+``KeyRangeKmerSort`` (default): no k-mer moves between GPUs.  Histograms of the rank's position
+share are all-reduced (1 KiB), the digits are cut into ranges of about n/N k-mers, and each rank
+selects its k-mers from the whole resident sequence and sorts them.
+
+``ShardedKmerSort`` (all-to-all):
+1. ``shard_partition``: the rank encodes the k-mers that START in its position range
+   [lo_r, lo_r+1) (cut at multiples of 32; a k-mer near hi reads a (k-1)-base halo) and
+   partitions them stably by the top ``bits`` (8) key bits into a torch-owned send buffer;
 2. ``all_gather`` of the 256-bucket histograms: every rank derives the same split of the buckets
    into N contiguous ranges of about n/N k-mers each (``split_buckets``);
 3. the exchange: every rank sends each other rank the buckets it owns, keys and starts, as one
    group of point-to-point messages (ncclSend / ncclRecv over xGMI under RCCL);
 4. ``shard_sort``: the received buckets are sorted by the MSD levels below the top bits.  A bucket
    arrives as one piece per source rank; pieces are listed in source-rank order, and ranks own
-   ascending positions, so equal keys stay in ascending start order;
-5. unique counts are local: the bucket ranges end on bucket boundaries, so equal keys never
-   straddle two ranks.
-
-The concatenation of the ranks' sorted starts, in rank order, is ``Kmers.sort``'s order with
-``break_ties=True`` (kmers.py:1710-1711) -- the single-GPU order.
+   ascending positions, so equal keys stay in ascending start order.
 """
 
 from __future__ import annotations

@@ -308,6 +308,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->pk_fresh = false;
     c->n = 0;
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;

@@ -73,6 +73,8 @@ struct gk_ctx {
     uint64_t nseg = 0, seg_cap = 0;
     uint64_t max_seg_len = 0;
     int acgt = 1;
+    bool pk_fresh = false;  // the packed sequence (scratch "pk_code" / "pk_dol") is current for
+                            // the next gk_shard_sort_range (set by gk_shard_histogram)
 
     // k-mers
     uint64_t n = 0;

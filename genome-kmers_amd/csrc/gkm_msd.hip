@@ -38,6 +38,10 @@ constexpr int kBlockMax = kBT * kBI;    // 4096
 constexpr int kLocal = 5;                // 4 = tiny (<= kTiny elements: one thread per bucket)
 constexpr int kTiny = 8;
 constexpr int kSmall = 24;
+// later local rounds (buckets re-listed because a sub-bucket outgrew kSmall: repeat families) and
+// later phases finish sub-buckets of up to kSmallLate by rank-by-count instead of re-listing them
+// for another round -- a round costs a bucket load, ranking and write-back per bucket
+constexpr int kSmallLate = 96;
 // The local rounds write back the keys of a bucket only when some of its elements are re-listed
 // (rare): the sort's product is the start order (+ group heads), and keys are re-encoded from the
 // sorted starts when an API call needs them (gk_ctx::keys_stale).
@@ -70,6 +74,9 @@ struct L0Args {
     int acgt_only;    // 2-bit keys of a mixed sba: k-mers holding a non-ACGT byte are not started
     // key-range shard: only k-mers whose L0 digit d has d - own_lo < own_span are kept (all: 0, ~0)
     uint32_t own_lo = 0, own_span = 0xFFFFFFFFu;
+    // 2-bit packed copy of an ACGT sba (pack2_kernel, 32 positions per word; null: pack bytes)
+    const uint64_t *pk_code = nullptr;
+    const uint32_t *pk_dol = nullptr;
 };
 
 __device__ __forceinline__ bool l0_owned(uint32_t d, const L0Args &a) { return d - a.own_lo < a.own_span; }
@@ -89,9 +96,16 @@ struct L0Units {
 };
 
 template <int BITS, int TILE, int T>
-__device__ __forceinline__ void l0_load(const uint8_t *__restrict__ src, uint64_t (&r)[L0Units<BITS, TILE, T>::kPer]) {
+__device__ __forceinline__ void l0_load(const L0Args &a, uint64_t P0, uint64_t (&r)[L0Units<BITS, TILE, T>::kPer]) {
     using U = L0Units<BITS, TILE, T>;
-    const uint64_t *s8 = reinterpret_cast<const uint64_t *>(src);
+    static_assert(U::kPer >= 2, "the packed path keeps a code word and a stop word");
+    if (BITS == 2 && a.pk_code) {  // pre-packed: thread g < kGroups holds group g's words
+        const uint64_t g = (P0 >> 5) + min((uint32_t)threadIdx.x, (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
+        r[0] = a.pk_code[g];
+        r[1] = a.pk_dol[g];
+        return;
+    }
+    const uint64_t *s8 = reinterpret_cast<const uint64_t *>(a.sba + P0);
 #pragma unroll
     for (int j = 0; j < U::kPer; ++j) r[j] = s8[min((uint32_t)(threadIdx.x + j * T), (uint32_t)U::kUnits - 1)];
 }
@@ -123,10 +137,18 @@ __device__ __forceinline__ uint32_t pack2_8(uint64_t x) {
 // words, stop flags into bytes of the 32-position mask words.
 template <int BITS, int TILE, int T>
 __device__ __forceinline__ void l0_pack(const uint64_t (&r)[L0Units<BITS, TILE, T>::kPer], uint64_t *s_code,
-                                        uint32_t *s_dol, const uint8_t *lut4, int acgt_only = 0) {
+                                        uint32_t *s_dol, const uint8_t *lut4, int acgt_only, bool packed) {
     using U = L0Units<BITS, TILE, T>;
     using P = L0Pack<BITS, TILE>;
     constexpr uint64_t kOnes = 0x0101010101010101ull;
+    if (BITS == 2 && packed) {
+        if (threadIdx.x < (uint32_t)P::kGroups) {
+            s_code[threadIdx.x] = r[0];
+            s_dol[threadIdx.x] = (uint32_t)r[1];
+        }
+        if (threadIdx.x == 0) s_code[P::kCodeWords - 1] = 0;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < U::kPer; ++j) {
         const uint32_t u = threadIdx.x + j * T;
@@ -235,7 +257,8 @@ __device__ __forceinline__ uint32_t win8_keep(const Win8 &w, const L0Args &a, Di
 }
 
 template <int BITS, int T, int I, int R, bool CANON = false>
-__global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_t *__restrict__ tile_hist) {
+__global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_t *__restrict__ tile_hist,
+                                                       uint32_t ntiles) {
     constexpr int TILE = T * I;
     constexpr int RADIX = 1 << R;
     using P = L0Pack<BITS, TILE>;
@@ -245,34 +268,38 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     __shared__ uint8_t s_lut4[256];
     const int t = threadIdx.x;
     if (t < 256) s_lut4[t] = c_code4_msd[t];
-    for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
-    lds_barrier();
-    const uint64_t P0 = a.lo + (uint64_t)blockIdx.x * TILE;
+    // persistent: the next tile's bytes are loaded while this one is counted
     uint64_t rr[L0Units<BITS, TILE, T>::kPer];
-    l0_load<BITS, TILE, T>(a.sba + P0, rr);
-    l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
-    lds_barrier();
-    if constexpr (BITS == 2 && !CANON) {  // 8 consecutive positions per thread (Win8)
-        static_assert(TILE % 8 == 0 && (TILE / 8) % 64 == 0, "whole waves per round");
-        for (uint32_t g = t; g < TILE / 8; g += T) {
-            const uint32_t q0 = g * 8;
-            const Win8 w = win8_load(s_code, s_dol, q0);
-            uint32_t dig[8];
-            const uint32_t keepm = win8_keep(w, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
+    if (blockIdx.x < ntiles) l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)blockIdx.x * TILE, rr);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t P0 = a.lo + (uint64_t)tile * TILE;
+        for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
+        lds_barrier();  // the LUT; the previous tile's histogram and codes have been read
+        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
+        lds_barrier();
+        if (tile + gridDim.x < ntiles) l0_load<BITS, TILE, T>(a, P0 + (uint64_t)gridDim.x * TILE, rr);
+        if constexpr (BITS == 2 && !CANON) {  // 8 consecutive positions per thread (Win8)
+            static_assert(TILE % 8 == 0 && (TILE / 8) % 64 == 0, "whole waves per round");
+            for (uint32_t g = t; g < TILE / 8; g += T) {
+                const uint32_t q0 = g * 8;
+                const Win8 w = win8_load(s_code, s_dol, q0);
+                uint32_t dig[8];
+                const uint32_t keepm = win8_keep(w, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i]], 1u);
-        }
-    } else {
+                for (int i = 0; i < 8; ++i)
+                    if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i]], 1u);
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < I; ++i) {
-            const uint32_t p = i * T + t;
-            const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
-            if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+            for (int i = 0; i < I; ++i) {
+                const uint32_t p = i * T + t;
+                const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
+                if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+            }
         }
+        lds_barrier();
+        for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)tile * RADIX + i] = s_hist[i];
     }
-    lds_barrier();
-    for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
 }
 
 // persistent (see msd_scatter_kernel): the next tile's bytes are loaded while runs are stored
@@ -299,7 +326,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
     uint64_t rr[L0Units<BITS, TILE, T>::kPer];
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
-        l0_load<BITS, TILE, T>(a.sba + a.lo + (uint64_t)t * TILE, rr);
+        l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)t * TILE, rr);
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
     };
     if (walk.first < walk.end) load(walk.first);
@@ -308,7 +335,7 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
         lds_barrier();  // the previous tile's runs have been read out of LDS
         for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
         if (tid < RADIX) s_toff[tid] = toff;
-        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
+        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         lds_barrier();
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         uint64_t key[I];
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     uint32_t toff = 0;
     auto load = [&](uint32_t t) {
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];
-        l0_load<BITS, TILE, T>(a.sba + a.lo + (uint64_t)t * TILE, rr);
+        l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)t * TILE, rr);
     };
     uint32_t pcnt = 0;
     int cur = 0;
@@ -373,7 +400,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int u = 0; u < (RADIX + 63) / 64; ++u)
             if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
         if (tid < RADIX) s_toff[cur][tid] = toff;
-        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only);
+        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
         for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
@@ -482,14 +509,16 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
     __shared__ uint32_t s_sval[kStage];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
+    if (blockIdx.x < ntiles) l0_load<BITS, kSTile, kST>(a, a.lo + (uint64_t)blockIdx.x * kSTile, rr);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t wslot = (uint64_t)t * kSW + wave;
         const uint64_t P0 = a.lo + (uint64_t)t * kSTile;
-        uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
-        l0_load<BITS, kSTile, kST>(a.sba + P0, rr);
         __syncthreads();  // the LUT; the previous tile's codes have been read
-        l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only);
+        l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         __syncthreads();
+        // the next tile's bytes fly while this one is processed
+        if (t + gridDim.x < ntiles) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)gridDim.x * kSTile, rr);
         if constexpr (BITS == 2 && !CANON) {
             // 8 consecutive positions per thread (Win8)
             const uint32_t q0 = tid * 8;
@@ -560,6 +589,32 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 }
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2-bit packed copy of an ACGT sba: one u64 of codes (A0 C1 G2 T3, MSB first) and one u32 stop
+// mask ('$') per 32 positions -- the layout the L0 kernels build in LDS.  Packed once per sort and
+// read by every full-sequence pass (L0 count and partition; histogram, select count and store of
+// the key-range shards) instead of each pass re-packing the bytes: 0.28 B per position.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack2_kernel(const uint8_t *__restrict__ sba, uint64_t nwords,
+                                                    uint64_t *__restrict__ code, uint32_t *__restrict__ dol) {
+    constexpr uint64_t kOnes = 0x0101010101010101ull;
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < nwords; g += (uint64_t)gridDim.x * 256) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(sba + 32 * g);
+        const uint4 ra = s4[0], rb = s4[1];
+        const uint64_t x[4] = {((uint64_t)ra.y << 32) | ra.x, ((uint64_t)ra.w << 32) | ra.z,
+                               ((uint64_t)rb.y << 32) | rb.x, ((uint64_t)rb.w << 32) | rb.z};
+        uint64_t cw = 0;
+        uint32_t dw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cw = (cw << 16) | pack2_8(x[j]);
+            dw = (dw << 8) | gather_flags8(zero_bytes(x[j] ^ (kOnes * GK_DOLLAR)));
+        }
+        code[g] = cw;
+        dol[g] = dw;
     }
 }
 
@@ -852,7 +907,7 @@ template <int T, int I, int R>
 __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small) {
     using SM = PartSmem<T, I, R>;
     constexpr int TILE = SM::kTile;
     constexpr int RADIX = SM::kRadix;
@@ -925,7 +980,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
             const uint32_t sb = s_start[dg], size = s_start[dg + 1] - sb;
             hd[i] = slot[i] == sb;  // singleton or equal keys: the first is the head
             if (valid[i] && size > 1 && !last) {
-                if (size <= (uint32_t)kSmall) {
+                if (size <= small) {
                     const uint32_t me = slot[i] - sb;
                     uint32_t lt = 0, eq = 0;
                     for (uint32_t j = 0; j < size; ++j) {
@@ -992,7 +1047,7 @@ template <int I>
 __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
     __shared__ uint64_t s_mask[256];
@@ -1098,7 +1153,7 @@ __global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ 
             const uint32_t sb = s_cnt[dig[i]], size = s_cnt[dig[i] + 1] - sb;
             hd[i] = slot[i] == sb;
             if (valid[i] && size > 1 && !last) {
-                if (size <= (uint32_t)kSmall) {
+                if (size <= small) {
                     const uint32_t me = slot[i] - sb;
                     uint32_t lt = 0, eq = 0;
                     // 4 keys per step (their LDS reads in flight together); indices past the
@@ -1321,6 +1376,26 @@ static unsigned cu_count(gk_ctx *c) {
     return (unsigned)(cus / 8 * 8);
 }
 
+// the packed copy of c->sba (pack2_kernel) over the whole padded array, for ACGT sequences
+static int pack_sequence(gk_ctx *c, const uint64_t **code, const uint32_t **dol) {
+    const uint64_t nwords = (c->sba_len + kSbaPad) / 32;  // sba_cap >= sba_len + kSbaPad
+    uint64_t *pc;
+    uint32_t *pd;
+    GK_TRY_HIP(c, scratch(c, "pk_code", nwords, &pc));
+    GK_TRY_HIP(c, scratch(c, "pk_dol", nwords, &pd));
+    int slot;
+    timer_begin(c, "msd_pack", &slot);
+    timer_units(c, slot, c->sba_len);
+    hipLaunchKernelGGL(pack2_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256), 0,
+                       c->stream, c->sba, nwords, pc, pd);
+    GK_TRY_HIP(c, hipGetLastError());
+    timer_end(c, slot);
+    *code = pc;
+    *dol = pd;
+    c->pk_fresh = true;
+    return GK_OK;
+}
+
 static const char *kLocName[kLocal][2] = {{"loc0a", "loc0b"}, {"loc1a", "loc1b"}, {"loc2a", "loc2b"},
                                           {"loc3a", "loc3b"}, {"loc4a", "loc4b"}};
 static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_r"},
@@ -1357,6 +1432,8 @@ struct MsdDriver {
     uint32_t nbig = 0;
     int cur_big = 0;
     int phase = 0;  // key word being sorted (multi-word keys)
+    const uint64_t *pk_code = nullptr;  // packed sequence for the L0 passes (ACGT, 2-bit keys)
+    const uint32_t *pk_dol = nullptr;
 
     MsdDriver(gk_ctx *c_, const KeySpec &ks_) : c(c_), ks(ks_), B(ks_.total_bits) {
         cus = cu_count(c);
@@ -1454,8 +1531,8 @@ struct MsdDriver {
     void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
                    uint64_t sink, const NextDigits &ndg) {
         if (count)
-            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kPI, R, CANON>), dim3(nt0), dim3(kPT), 0, c->stream, a, d0,
-                               tile_hist);
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kPI, R, CANON>),
+                               dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kPT), 0, c->stream, a, d0, tile_hist, nt0);
         else
             hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kPT, kPI, R, ND, CANON>), dim3(pgrid), dim3(kPT), 0, c->stream,
                                a, d0, tile_hist, kout, vout, nt, sink, ndg);
@@ -1521,6 +1598,8 @@ struct MsdDriver {
         L0Args a{c->sba, lo, hi, ks.symbols, B, ks.acgt_only};
         a.own_lo = own_lo;
         a.own_span = own_span;
+        a.pk_code = pk_code;
+        a.pk_dol = pk_dol;
         l0a = a;
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
@@ -1812,22 +1891,24 @@ struct MsdDriver {
         // common-prefix skip: re-listed buckets, later phases (repeats) and the block class; not
         // the first wave round of phase 0, where random keys differ right below the sorted bits
         const int skip = (round > 0 || phase > 0 || k == 3) ? 1 : 0;
+        const uint32_t small = (round > 0 || phase > 0) ? kSmallLate : kSmall;
         switch (k) {
         case 0:
             hipLaunchKernelGGL((msd_wave_kernel<4>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 1:
             hipLaunchKernelGGL((msd_wave_kernel<8>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 2:
             hipLaunchKernelGGL((msd_wave_kernel<16>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
+                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
-                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip);
+                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
+                               (uint32_t)kSmall);  // the block class keeps kSmall: measured slower at 96
             break;
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
@@ -1916,6 +1997,11 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
+    if (c->acgt && ks.bits == 2 && !ks.acgt_only) {  // both L0 passes read the packed sequence
+        rc = pack_sequence(c, &d.pk_code, &d.pk_dol);
+        if (rc != GK_OK) return rc;
+        c->pk_fresh = false;
+    }
     uint64_t found = 0;
     rc = d.run_l0(0, c->sba_len, c->keys[0], c->vals[0], c->elem_cap + 64, &found);
     if (rc != GK_OK) return rc;
@@ -1979,6 +2065,12 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
     d.B = ks.bits * std::min(ks.symbols, 64 / ks.bits);  // the first key word (see msd_sort)
     d.wsched[0] = range_width(ks);
     GK_TRY_HIP(c, msd_tables());
+    // the packed sequence is made here for the whole sba and kept for the gk_shard_sort_range
+    // that follows (one packing per key-range step)
+    if (c->acgt && ks.bits == 2) {
+        int rp = pack_sequence(c, &d.pk_code, &d.pk_dol);
+        if (rp != GK_OK) return rp;
+    }
     uint64_t cnt = 0;
     int rc = d.l0_count(lo, hi, 0, 0xFFFFFFFFu, &cnt);
     if (rc != GK_OK) return rc;
@@ -2005,6 +2097,21 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     L0Args a{c->sba, 0, L, ks.symbols, d.B, ks.acgt_only};
     a.own_lo = digit_lo;
     a.own_span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
+    if (c->acgt && ks.bits == 2) {  // the packed sequence of this step's gk_shard_histogram, or pack now
+        if (c->pk_fresh) {
+            uint64_t *pc;
+            uint32_t *pd;
+            const uint64_t nwords = (L + kSbaPad) / 32;
+            GK_TRY_HIP(c, scratch(c, "pk_code", nwords, &pc));
+            GK_TRY_HIP(c, scratch(c, "pk_dol", nwords, &pd));
+            a.pk_code = pc;
+            a.pk_dol = pd;
+        } else {
+            int rp = pack_sequence(c, &a.pk_code, &a.pk_dol);
+            if (rp != GK_OK) return rp;
+        }
+        c->pk_fresh = false;
+    }
     const Dig d0 = dig_at(d.B, 0, d.width(0));
     uint32_t *wave_cnt, *wave_off;
     GK_TRY_HIP(c, scratch(c, "sel_wave_cnt", nw + 1, &wave_cnt));

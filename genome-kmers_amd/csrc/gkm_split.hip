@@ -21,6 +21,7 @@
 namespace gkm {
 
 __constant__ uint8_t c_code4_split[256];
+__constant__ uint8_t c_comp_split[256];  // the reference's complement (sequence_collection.py:402-433)
 static bool g_split_tables = false;
 
 static hipError_t split_tables() {
@@ -29,6 +30,15 @@ static hipError_t split_tables() {
     const char *order = "ABCDGHKMNRSTVWY";
     for (int i = 0; order[i]; ++i) code4[(uint8_t)order[i]] = (uint8_t)(i + 1);
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_code4_split), code4, 256);
+    if (e != hipSuccess) return e;
+    uint8_t comp[256];
+    for (int i = 0; i < 256; ++i) comp[i] = (uint8_t)i;
+    const char *pairs[] = {"AT", "CG", "RY", "KM", "BV", "DH"};
+    for (const char *p : pairs) {
+        comp[(uint8_t)p[0]] = (uint8_t)p[1];
+        comp[(uint8_t)p[1]] = (uint8_t)p[0];
+    }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_comp_split), comp, 256);
     if (e == hipSuccess) g_split_tables = true;
     return e;
 }
@@ -48,44 +58,93 @@ __device__ __forceinline__ bool window_clear(const uint32_t *m, uint32_t p, int 
     return (x >> 32) == 0 && (y >> (96 - S)) == 0;
 }
 
+// flags[p] = 1: a class-B k-mer that is not a homopolymer; homo[p] = 1: a class-B k-mer that is
+// one letter repeated k times (N runs: GRCh38's ~150 M N bases give that many "N...N" k-mers, all
+// one group, already in start order -- they skip the B sort, see split_sort)
 __global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
-                                                            uint8_t *__restrict__ flags) {
-    __shared__ uint32_t s_dol[kFlagGroups], s_bad[kFlagGroups];
+                                                            uint8_t *__restrict__ flags, uint8_t *__restrict__ homo) {
+    __shared__ uint32_t s_dol[kFlagGroups], s_bad[kFlagGroups], s_diff[kFlagGroups];
     const uint64_t P0 = (uint64_t)blockIdx.x * kFlagTile;
     for (int g = threadIdx.x; g < kFlagGroups; g += 256) {
         const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
         const uint4 ra = src[0], rb = src[1];
+        const uint32_t nxt = sba[P0 + 32ull * (g + 1)];  // the next group's first byte
         const uint32_t wv[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-        uint32_t dm = 0, bm = 0;
+        uint32_t dm = 0, bm = 0, fm = 0;
 #pragma unroll
         for (int q = 0; q < 32; ++q) {
             const uint32_t ch = (wv[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            const uint32_t cn = q < 31 ? (wv[(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 0xFFu : nxt;
             dm = (dm << 1) | (ch == GK_DOLLAR ? 1u : 0u);
             bm = (bm << 1) | ((ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T') ? 0u : 1u);
+            fm = (fm << 1) | (ch != cn ? 1u : 0u);  // position q differs from q + 1
         }
         s_dol[g] = dm;
         s_bad[g] = bm;
+        s_diff[g] = fm;
     }
     __syncthreads();
-    // thread t: positions 32 t .. 32 t + 31 -> 32 flag bytes (two 16-B stores)
+    // thread t: positions 32 t .. 32 t + 31 -> 32 flag bytes of each kind (two 16-B stores)
     const uint32_t p0 = threadIdx.x * 32;
-    uint32_t out[8];
+    uint32_t out[8], hout[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
-        uint32_t v = 0;
+        uint32_t v = 0, h = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t p = p0 + 4 * w + b;
             const bool f = P0 + p < L && window_clear(s_dol, p, k) && !window_clear(s_bad, p, k);
-            v |= (f ? 1u : 0u) << (8 * b);
+            const bool hp = k == 1 || window_clear(s_diff, p, k - 1);
+            v |= (f && !hp ? 1u : 0u) << (8 * b);
+            h |= (f && hp ? 1u : 0u) << (8 * b);
         }
         out[w] = v;
+        hout[w] = h;
     }
     if (P0 + p0 < L) {
         uint4 *dst = reinterpret_cast<uint4 *>(flags + P0 + p0);
         dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
         dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
+        uint4 *hd = reinterpret_cast<uint4 *>(homo + P0 + p0);
+        hd[0] = make_uint4(hout[0], hout[1], hout[2], hout[3]);
+        hd[1] = make_uint4(hout[4], hout[5], hout[6], hout[7]);
     }
+}
+
+// homopolymer k-mers by (canonical) letter: counts per letter; flags of one letter
+__device__ __forceinline__ uint32_t homo_letter(const uint8_t *sba, uint32_t p, int canonical, const uint8_t *comp) {
+    const uint32_t c = sba[p];
+    return canonical ? min(c, (uint32_t)comp[c]) : c;
+}
+
+__global__ __launch_bounds__(256) void homo_count_kernel(const uint8_t *__restrict__ sba,
+                                                         const uint32_t *__restrict__ hs, uint64_t n, int canonical,
+                                                         uint32_t *__restrict__ counts) {
+    __shared__ uint32_t s_c[256];
+    __shared__ uint8_t s_comp[256];
+    s_c[threadIdx.x] = 0;
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        atomicAdd(&s_c[homo_letter(sba, hs[i], canonical, s_comp)], 1u);
+    __syncthreads();
+    if (s_c[threadIdx.x]) atomicAdd(&counts[threadIdx.x], s_c[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void homo_flags_kernel(const uint8_t *__restrict__ sba,
+                                                         const uint32_t *__restrict__ hs, uint64_t n, int canonical,
+                                                         uint32_t letter, uint8_t *__restrict__ f) {
+    __shared__ uint8_t s_comp[256];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        f[i] = homo_letter(sba, hs[i], canonical, s_comp) == letter ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void gather_u32_kernel(const uint32_t *__restrict__ src,
+                                                         const uint32_t *__restrict__ idx, uint64_t n,
+                                                         uint32_t *__restrict__ dst) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[idx[i]];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -222,46 +281,50 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     if (k > 64 || ks.bits != 4 || ks.lenbits || ks.symbols != ks.min_len) return GK_OK;
     GK_TRY_HIP(c, split_tables());
     int slot;
-    // 1. class B starts
-    uint8_t *fB;
-    uint32_t *b_st[2];
+    // 1. class B starts: homopolymers (one letter k times) apart from the rest
+    uint8_t *fB, *fH;
+    uint32_t *b_st[2], *h_st;
     GK_TRY_HIP(c, scratch(c, "split_flags", L + kFlagTile + 64, &fB));
+    GK_TRY_HIP(c, scratch(c, "split_hflags", L + kFlagTile + 64, &fH));
     timer_begin(c, "split_b_select", &slot);
     hipLaunchKernelGGL(class_b_flags_kernel, dim3((unsigned)((L + kFlagTile - 1) / kFlagTile)), dim3(256), 0,
-                       c->stream, c->sba, L, k, fB);
+                       c->stream, c->sba, L, k, fB, fH);
     GK_TRY_HIP(c, hipGetLastError());
-    uint64_t nB = 0;
-    // count first: the select output needs nB entries, which may be up to n
+    uint64_t nR = 0, nH = 0;
+    // count first: the select outputs need their counts of entries, which may be up to n
     GK_TRY_HIP(c, scratch(c, "split_b_st0", n + 64, &b_st[0]));
-    GK_TRY_HIP(c, select_flags(c, fB, L, b_st[0], &nB));
+    GK_TRY_HIP(c, select_flags(c, fB, L, b_st[0], &nR));
+    GK_TRY_HIP(c, scratch(c, "split_h_st", n + 64, &h_st));
+    GK_TRY_HIP(c, select_flags(c, fH, L, h_st, &nH));
     timer_end(c, slot);
+    const uint64_t nB = nR + nH;
     if (nB > n) return fail(c, GK_E_HIP, "split: more class-B k-mers than k-mers");
     if (nB * 4 > n) return GK_OK;  // mostly non-ACGT k-mers: the plain 4-bit MSD is the better sort
     *used = true;
     const uint64_t nA = n - nB;
 
-    // 2. sort B: 4-bit keys, LSD (on a swapped-in context of nB elements)
+    // 2. sort the non-homopolymer B k-mers: 4-bit keys, LSD (on a swapped-in context of nR elements)
     uint64_t *b_k[2];
     uint8_t *b_heads;
     int bres = 0;
-    if (nB > 0) {
+    GK_TRY_HIP(c, scratch(c, "split_b_st1", nB + 64, &b_st[1]));
+    GK_TRY_HIP(c, scratch(c, "split_b_heads", nB + 64, &b_heads));
+    if (nR > 0) {
         const int W = ks.words;
-        GK_TRY_HIP(c, scratch(c, "split_b_st1", nB + 64, &b_st[1]));
-        GK_TRY_HIP(c, scratch(c, "split_b_k0", W * (nB + 64), &b_k[0]));
-        GK_TRY_HIP(c, scratch(c, "split_b_k1", W * (nB + 64), &b_k[1]));
-        GK_TRY_HIP(c, scratch(c, "split_b_heads", nB + 64, &b_heads));
+        GK_TRY_HIP(c, scratch(c, "split_b_k0", W * (nR + 64), &b_k[0]));
+        GK_TRY_HIP(c, scratch(c, "split_b_k1", W * (nR + 64), &b_k[1]));
         const uint64_t sv_n = c->n;
         uint64_t *sv_k[2] = {c->keys[0], c->keys[1]};
         uint32_t *sv_v[2] = {c->vals[0], c->vals[1]};
         const int sv_cur = c->cur;
-        c->n = nB;
+        c->n = nR;
         c->keys[0] = b_k[0];
         c->keys[1] = b_k[1];
         c->vals[0] = b_st[0];
         c->vals[1] = b_st[1];
         c->cur = 0;
         timer_begin(c, "split_b_encode", &slot);
-        hipError_t e = launch_encode_gather(c, ks, b_st[0], nB, b_k[0]);
+        hipError_t e = launch_encode_gather(c, ks, b_st[0], nR, b_k[0]);
         timer_end(c, slot);
         int rc = e == hipSuccess ? radix_sort(c, W, ks.total_bits, false) : GK_E_HIP;
         bres = c->cur;
@@ -273,8 +336,92 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
         c->cur = sv_cur;
         if (e != hipSuccess) return hip_fail(c, e, "split: encode B");
         if (rc != GK_OK) return rc;
-        hipLaunchKernelGGL(key_heads_kernel, dim3(grid_of_n(nB)), dim3(256), 0, c->stream, b_k[bres], nB, W, b_heads);
+        hipLaunchKernelGGL(key_heads_kernel, dim3(grid_of_n(nR)), dim3(256), 0, c->stream, b_k[bres], nR, W, b_heads);
         GK_TRY_HIP(c, hipGetLastError());
+    }
+    if (nH > 0) {
+        // 2b. the homopolymer groups (one per (canonical) letter, members in start order) go into
+        // the sorted B run at their insertion points: at most 15 segment copies
+        timer_begin(c, "split_b_homo", &slot);
+        uint32_t *cnt;
+        GK_TRY_HIP(c, scratch(c, "split_h_cnt", 256, &cnt));
+        GK_TRY_HIP(c, hipMemsetAsync(cnt, 0, 4 * 256, c->stream));
+        hipLaunchKernelGGL(homo_count_kernel, dim3(grid_of_n(nH)), dim3(256), 0, c->stream, c->sba, h_st, nH,
+                           ks.canonical, cnt);
+        GK_TRY_HIP(c, hipGetLastError());
+        std::vector<uint32_t> hc(256);
+        GK_TRY_HIP(c, hipMemcpyAsync(hc.data(), cnt, 4 * 256, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        std::vector<uint32_t> letters;  // ascending byte = ascending key of letter^k
+        for (int ch = 0; ch < 256; ++ch)
+            if (hc[ch]) letters.push_back((uint32_t)ch);
+        // groups by letter, in letter order, into grp (stable: h_st is in start order)
+        uint32_t *grp = h_st, *tmp_idx, *grp2;
+        if (letters.size() > 1) {
+            uint8_t *lf;
+            GK_TRY_HIP(c, scratch(c, "split_h_lf", nH + 64, &lf));
+            GK_TRY_HIP(c, scratch(c, "split_h_idx", nH + 64, &tmp_idx));
+            GK_TRY_HIP(c, scratch(c, "split_h_grp", nH + 64, &grp2));
+            uint64_t at = 0;
+            for (uint32_t ch : letters) {
+                hipLaunchKernelGGL(homo_flags_kernel, dim3(grid_of_n(nH)), dim3(256), 0, c->stream, c->sba, h_st, nH,
+                                   ks.canonical, ch, lf);
+                uint64_t m = 0;
+                GK_TRY_HIP(c, select_flags(c, lf, nH, tmp_idx, &m));
+                hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_of_n(m)), dim3(256), 0, c->stream, h_st, tmp_idx, m,
+                                   grp2 + at);
+                GK_TRY_HIP(c, hipGetLastError());
+                at += m;
+            }
+            grp = grp2;
+        }
+        // insertion points: the number of sorted non-homopolymer B k-mers below each group's k-mer
+        std::vector<uint32_t> ins(letters.size(), 0), first(letters.size());
+        {
+            uint64_t at = 0;
+            for (size_t g = 0; g < letters.size(); ++g) {
+                first[g] = (uint32_t)at;
+                at += hc[letters[g]];
+            }
+        }
+        if (nR > 0) {
+            uint32_t *d_first, *d_pos;
+            GK_TRY_HIP(c, scratch(c, "split_h_first", letters.size() + 1, &d_first));
+            GK_TRY_HIP(c, scratch(c, "split_h_pos", letters.size() + 1, &d_pos));
+            GK_TRY_HIP(c, hipMemcpyAsync(d_first, first.data(), 4 * letters.size(), hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(b_group_pos_kernel, dim3(1), dim3(256), 0, c->stream, c->sba, k, ks.canonical,
+                               b_st[bres], nR, grp, d_first, (uint64_t)letters.size(), d_pos);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, hipMemcpyAsync(ins.data(), d_pos, 4 * letters.size(), hipMemcpyDeviceToHost, c->stream));
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        }
+        // assemble the B order into the other start buffer (+ heads into a fresh array)
+        uint32_t *fst = b_st[bres ^ 1];
+        uint8_t *fhd;
+        GK_TRY_HIP(c, scratch(c, "split_b_heads2", nB + 64, &fhd));
+        uint64_t rcur = 0, out = 0;
+        auto copy_rest = [&](uint64_t upto) -> hipError_t {
+            const uint64_t m = upto - rcur;
+            if (!m) return hipSuccess;
+            hipError_t e = hipMemcpyAsync(fst + out, b_st[bres] + rcur, 4 * m, hipMemcpyDeviceToDevice, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(fhd + out, b_heads + rcur, m, hipMemcpyDeviceToDevice, c->stream);
+            rcur = upto;
+            out += m;
+            return e;
+        };
+        for (size_t g = 0; g < letters.size(); ++g) {
+            GK_TRY_HIP(c, copy_rest(ins[g]));
+            const uint64_t m = hc[letters[g]];
+            GK_TRY_HIP(c, hipMemcpyAsync(fst + out, grp + first[g], 4 * m, hipMemcpyDeviceToDevice, c->stream));
+            GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 0, m, c->stream));
+            GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 1, 1, c->stream));  // one group: one head
+            out += m;
+        }
+        GK_TRY_HIP(c, copy_rest(nR));
+        b_heads = fhd;
+        bres ^= 1;
+        timer_end(c, slot);
     }
 
     // 3. sort A: the 2-bit MSD over the ACGT-only k-mers (its count is checked against nA)

@@ -125,3 +125,21 @@ def test_canonical_split_n_runs_vs_oracle(k):
         out.append((name, b.decode()))
     km, _ = check_canonical(out, k)
     assert not km._engine.is_acgt()
+
+
+@pytest.mark.parametrize("k", [15, 31])
+def test_canonical_split_complementary_homopolymer_runs(k):
+    """R runs and Y runs (complements) and self-complementary N / S runs: canonical R^k and Y^k are
+    one k-mer, so their homopolymer groups merge in start order across both letters."""
+    rng = np.random.default_rng(700 + k)
+    seqs = genome_with_rc_repeats(rng, [40_000, 20_000], b"ACGT")
+    out = []
+    for name, s in seqs:
+        b = bytearray(s.encode())
+        for letter in b"RYNSMK":
+            for a in rng.integers(100, len(b) - 400, 2):
+                n_run = int(rng.integers(k + 1, k + 200))
+                b[a:a + n_run] = bytes([letter]) * n_run
+        out.append((name, b.decode()))
+    km, _ = check_canonical(out, k)
+    assert not km._engine.is_acgt()

@@ -483,3 +483,34 @@ def test_split_acgt_and_n_kmers_vs_oracle(k):
     assert t == ot
     spec = oracle.key_spec(False, k, k)
     np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [5, 31, 63])
+def test_split_homopolymer_runs_of_several_letters_vs_oracle(k):
+    """Runs of several non-ACGT letters (N, R, Y, K, W) longer than k: their homopolymer k-mers
+    skip the B sort as one group per letter and are spliced into the sorted B run at their
+    insertion points (gkm_split.hip); scattered letters keep some non-homopolymer B k-mers."""
+    rng = np.random.default_rng(900 + k)
+    seqs = n_run_genome(rng, [60_000, 25_000], runs=2)
+    out = []
+    for name, s in seqs:
+        b = bytearray(s.encode())
+        for letter in b"NRYKW":
+            for a in rng.integers(100, len(b) - 500, 2):
+                n_run = int(rng.integers(k + 1, k + 300))
+                b[a:a + n_run] = bytes([letter]) * n_run
+        out.append((name, b.decode()))
+    sc = SequenceCollection(sequence_list=out)
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    eng = km._get_engine()
+    eng.profile_enable(True)
+    km.sort()
+    assert "split_b_homo" in str(eng.profile_report())
+    unsorted = oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k)
+    want = oracle.quicksort(sc.forward_sba, unsorted, k, k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    h, t = km.get_kmer_group_counts(k, max_counts_bin=64)
+    oh, ot = oracle.group_scan(sc.forward_sba, want, k, max_counts_bin=64)
+    np.testing.assert_array_equal(h, oh)
+    assert t == ot

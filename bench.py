@@ -145,6 +145,10 @@ def load_traffic(path: str, kernel: str):
 
 def main():
     args = parse()
+    # the JSON line is the only thing on stdout: libraries (RCCL prints a banner at its first
+    # collective) write to fd 1 as well, so fd 1 goes to stderr and the line to a saved copy
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -314,7 +318,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

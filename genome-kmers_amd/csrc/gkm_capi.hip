@@ -845,6 +845,29 @@ extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     return msd_shard_partition(c, ks, lo, std::max(hi, lo), d_keys, d_starts, cap, h_hist, n_out);
 }
 
+// Key-range shards of a mixed sba (N runs, IUPAC letters; k >= 4): the ranges are top-7-bit
+// digits of the ACGT-only k-mers' 2-bit keys (split_sort with a SplitRange); other k-mers follow
+// the byte-order interval those digits bound.  k < 4: plain 4-bit digits.
+static bool range_split(gk_ctx *c, const KeySpec &ks) { return !c->acgt && ks.bits == 4 && ks.symbols >= 4; }
+
+static KeySpec acgt_spec(KeySpec ks) {
+    ks.bits = 2;
+    ks.total_bits = 2 * ks.symbols;
+    ks.words = (ks.total_bits + 63) / 64;
+    ks.acgt_only = 1;
+    return ks;
+}
+
+// the 4-bit code of the first four symbols of the smallest ACGT k-mer with top-7-bit digit d
+// (three bases, then A or G by the digit's low bit); a range from digit 0 has no lower bound, a
+// range to digit 128 no upper one
+static uint32_t range_prefix4(uint32_t d, bool lower) {
+    if (lower && d == 0) return 0;
+    if (d >= 128) return 0x10000u;
+    static const uint32_t c4[4] = {1, 3, 5, 12};  // A C G T among '$' A B C D G H K M N R S T V W Y
+    return (c4[(d >> 5) & 3] << 12) | (c4[(d >> 3) & 3] << 8) | (c4[(d >> 1) & 3] << 4) | c4[(d & 1) ? 2 : 0];
+}
+
 extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
                                   uint32_t *bits) {
     if (!c || !h_hist || !bits) return GK_E_ARG;
@@ -855,6 +878,7 @@ extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     KeySpec ks;
     int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
+    if (range_split(c, ks)) ks = acgt_spec(ks);  // mixed sba: digits of the ACGT-only k-mers
     for (int i = 0; i < 256; ++i) h_hist[i] = 0;
     int b = 0;
     rc = msd_l0_histogram(c, ks, lo, std::max(hi, lo), h_hist, &b);
@@ -876,7 +900,15 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     c->enumerated = false;
     c->starts_materialized = true;
     c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
-    rc = msd_sort_range(c, ks, digit_lo, digit_hi, n_kept);
+    if (range_split(c, ks)) {  // mixed sba: ACGT-only k-mers by 2-bit digit, the rest by prefix
+        SplitRange rg{digit_lo, digit_hi, range_prefix4(digit_lo, true), range_prefix4(digit_hi, false)};
+        bool used = false;
+        rc = split_sort(c, ks, &used, &rg);
+        if (rc == GK_OK && !used) rc = fail(c, GK_E_HIP, "key-range split sort not applicable");
+        *n_kept = c->n;
+    } else {
+        rc = msd_sort_range(c, ks, digit_lo, digit_hi, n_kept);
+    }
     if (rc != GK_OK) return rc;
     c->spec = ks;
     c->keys_valid = true;

@@ -163,7 +163,13 @@ int ensure_keys(gk_ctx *c);
 int msd_sort(gk_ctx *c, const KeySpec &ks);
 // fixed-length sort of a mixed-alphabet sba: ACGT-only k-mers by the 2-bit MSD, the others by
 // 4-bit keys, merged (gkm_split.hip); *used = false when the split does not pay (caller falls back)
-int split_sort(gk_ctx *c, const KeySpec &ks, bool *used);
+// key-range shards of a mixed sba (gk_shard_sort_range): ACGT-only k-mers whose 2-bit top-7-bit
+// digit is in [d_lo, d_hi), other k-mers whose (canonical) first four 4-bit symbols are in
+// [p4_lo, p4_hi) -- the same byte-order interval
+struct SplitRange {
+    uint32_t d_lo, d_hi, p4_lo, p4_hi;
+};
+int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg = nullptr);
 // multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the
 // top msd_radix_bits() key bits; receive-side sort of buckets given as pieces
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,

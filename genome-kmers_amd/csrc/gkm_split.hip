@@ -61,9 +61,32 @@ __device__ __forceinline__ bool window_clear(const uint32_t *m, uint32_t p, int 
 // flags[p] = 1: a class-B k-mer that is not a homopolymer; homo[p] = 1: a class-B k-mer that is
 // one letter repeated k times (N runs: GRCh38's ~150 M N bases give that many "N...N" k-mers, all
 // one group, already in start order -- they skip the B sort, see split_sort)
+// Key-range shards (p4_lo, p4_hi != 0, 0x10000): only B k-mers whose (canonical) first four
+// symbols, as a 16-bit 4-bit code, lie in [p4_lo, p4_hi) -- the rank's byte-order interval
+// (split_sort's SplitRange).
+__device__ __forceinline__ uint32_t b_prefix4(const uint8_t *sba, uint64_t p, int k, bool hp, int canonical,
+                                              const uint8_t *lut4, const uint8_t *comp) {
+    if (hp) {  // one letter k times; canonical: the smaller of the letter and its complement
+        uint32_t ch = sba[p];
+        if (canonical) ch = min(ch, (uint32_t)comp[ch]);
+        const uint32_t c4 = lut4[ch];
+        return (c4 << 12) | (c4 << 8) | (c4 << 4) | c4;
+    }
+    const uint8_t *b = sba + p;
+    const bool rc = canonical && canon_is_rc<4>(b, k, lut4);
+    uint32_t v = 0;
+    for (int t = 0; t < 4; ++t) v = (v << 4) | canon_sym<4>(b, k, t, rc, lut4);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
-                                                            uint8_t *__restrict__ flags, uint8_t *__restrict__ homo) {
+                                                            uint8_t *__restrict__ flags, uint8_t *__restrict__ homo,
+                                                            int canonical, uint32_t p4_lo, uint32_t p4_hi) {
     __shared__ uint32_t s_dol[kFlagGroups], s_bad[kFlagGroups], s_diff[kFlagGroups];
+    __shared__ uint8_t s_lut4[256], s_comp[256];
+    s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    const bool ranged = p4_lo != 0 || p4_hi != 0x10000u;
     const uint64_t P0 = (uint64_t)blockIdx.x * kFlagTile;
     for (int g = threadIdx.x; g < kFlagGroups; g += 256) {
         const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
@@ -93,8 +116,12 @@ __global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__res
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t p = p0 + 4 * w + b;
-            const bool f = P0 + p < L && window_clear(s_dol, p, k) && !window_clear(s_bad, p, k);
+            bool f = P0 + p < L && window_clear(s_dol, p, k) && !window_clear(s_bad, p, k);
             const bool hp = k == 1 || window_clear(s_diff, p, k - 1);
+            if (ranged && f) {
+                const uint32_t p4 = b_prefix4(sba, P0 + p, k, hp, canonical, s_lut4, s_comp);
+                f = p4 >= p4_lo && p4 < p4_hi;
+            }
             v |= (f && !hp ? 1u : 0u) << (8 * b);
             h |= (f && hp ? 1u : 0u) << (8 * b);
         }
@@ -274,11 +301,13 @@ static unsigned grid_of_n(uint64_t n) { return (unsigned)std::max<uint64_t>(1, s
 // ---------------------------------------------------------------------------------------------
 // driver
 // ---------------------------------------------------------------------------------------------
-int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
+int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     *used = false;
-    const uint64_t n = c->n, L = c->sba_len;
+    const uint64_t L = c->sba_len;
+    const uint64_t n = rg ? L : c->n;  // key-range shards: the k-mer count is not known yet (<= L)
     const int k = ks.symbols;
     if (k > 64 || ks.bits != 4 || ks.lenbits || ks.symbols != ks.min_len) return GK_OK;
+    if (rg && k < 4) return fail(c, GK_E_ARG, "split: key-range shards need k >= 4");
     GK_TRY_HIP(c, split_tables());
     int slot;
     // 1. class B starts: homopolymers (one letter k times) apart from the rest
@@ -288,7 +317,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     GK_TRY_HIP(c, scratch(c, "split_hflags", L + kFlagTile + 64, &fH));
     timer_begin(c, "split_b_select", &slot);
     hipLaunchKernelGGL(class_b_flags_kernel, dim3((unsigned)((L + kFlagTile - 1) / kFlagTile)), dim3(256), 0,
-                       c->stream, c->sba, L, k, fB, fH);
+                       c->stream, c->sba, L, k, fB, fH, ks.canonical, rg ? rg->p4_lo : 0u, rg ? rg->p4_hi : 0x10000u);
     GK_TRY_HIP(c, hipGetLastError());
     uint64_t nR = 0, nH = 0;
     // count first: the select outputs need their counts of entries, which may be up to n
@@ -299,9 +328,9 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     timer_end(c, slot);
     const uint64_t nB = nR + nH;
     if (nB > n) return fail(c, GK_E_HIP, "split: more class-B k-mers than k-mers");
-    if (nB * 4 > n) return GK_OK;  // mostly non-ACGT k-mers: the plain 4-bit MSD is the better sort
+    if (!rg && nB * 4 > n) return GK_OK;  // mostly non-ACGT k-mers: the plain 4-bit MSD is the better sort
     *used = true;
-    const uint64_t nA = n - nB;
+    uint64_t nA = rg ? 0 : n - nB;
 
     // 2. sort the non-homopolymer B k-mers: 4-bit keys, LSD (on a swapped-in context of nR elements)
     uint64_t *b_k[2];
@@ -311,6 +340,13 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     GK_TRY_HIP(c, scratch(c, "split_b_heads", nB + 64, &b_heads));
     if (nR > 0) {
         const int W = ks.words;
+        if (rg) {  // key-range shards: nothing sized the radix state for this context yet
+            const uint64_t sv_n = c->n;
+            c->n = 0;  // (no start array to keep)
+            const int re = ensure_elems(c, std::max<uint64_t>(c->elem_cap, nR + 1), 1);
+            c->n = sv_n;
+            if (re != GK_OK) return re;
+        }
         GK_TRY_HIP(c, scratch(c, "split_b_k0", W * (nR + 64), &b_k[0]));
         GK_TRY_HIP(c, scratch(c, "split_b_k1", W * (nR + 64), &b_k[1]));
         const uint64_t sv_n = c->n;
@@ -430,10 +466,20 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used) {
     ka.total_bits = 2 * k;
     ka.words = (ka.total_bits + 63) / 64;
     ka.acgt_only = 1;
-    c->n = nA;
-    int rc = nA > 0 ? msd_sort(c, ka) : GK_OK;
-    c->n = n;
-    if (rc != GK_OK) return rc;
+    int rc;
+    if (rg) {  // the rank's ACGT-only k-mers: select + MSD (gkm_msd.hip); room for the merge after
+        rc = msd_sort_range(c, ka, rg->d_lo, rg->d_hi, &nA);
+        if (rc != GK_OK) return rc;
+        c->have_starts = true;
+        rc = ensure_elems(c, nA + nB + 1, 1);  // keeps vals[0] (nA)
+        if (rc != GK_OK) return rc;
+        c->n = nA + nB;
+    } else {
+        c->n = nA;
+        rc = nA > 0 ? msd_sort(c, ka) : GK_OK;
+        c->n = n;
+        if (rc != GK_OK) return rc;
+    }
     if (nA == 0) {  // all B: the B order is the order
         GK_TRY_HIP(c, hipMemcpyAsync(c->vals[0], b_st[bres], 4 * nB, hipMemcpyDeviceToDevice, c->stream));
         uint8_t *hd;

@@ -20,6 +20,8 @@
 
 namespace gkm {
 
+hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
+
 __constant__ uint8_t c_code4_split[256];
 __constant__ uint8_t c_comp_split[256];  // the reference's complement (sequence_collection.py:402-433)
 static bool g_split_tables = false;
@@ -58,9 +60,9 @@ __device__ __forceinline__ bool window_clear(const uint32_t *m, uint32_t p, int 
     return (x >> 32) == 0 && (y >> (96 - S)) == 0;
 }
 
-// flags[p] = 1: a class-B k-mer that is not a homopolymer; homo[p] = 1: a class-B k-mer that is
-// one letter repeated k times (N runs: GRCh38's ~150 M N bases give that many "N...N" k-mers, all
-// one group, already in start order -- they skip the B sort, see split_sort)
+// Class-B k-mers: no '$' in [p, p + k) and some byte outside ACGT in it.  Homopolymers (one
+// letter k times: GRCh38's ~150 M N bases give that many "N...N" k-mers, one group already in
+// start order) skip the B sort (split_sort).
 // Key-range shards (p4_lo, p4_hi != 0, 0x10000): only B k-mers whose (canonical) first four
 // symbols, as a 16-bit 4-bit code, lie in [p4_lo, p4_hi) -- the rank's byte-order interval
 // (split_sort's SplitRange).
@@ -79,11 +81,21 @@ __device__ __forceinline__ uint32_t b_prefix4(const uint8_t *sba, uint64_t p, in
     return v;
 }
 
-__global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
-                                                            uint8_t *__restrict__ flags, uint8_t *__restrict__ homo,
-                                                            int canonical, uint32_t p4_lo, uint32_t p4_hi) {
+// The class-B starts without flag arrays: per 8192-position tile, COUNT writes the numbers of
+// non-homopolymer and homopolymer B k-mers (cnt[0][t], cnt[1][t]); after their scans, STORE
+// writes each kind's start positions from the tile's offsets (thread order = position order:
+// thread t owns positions 32 t .. 32 t + 31).  Key-range shards keep only the k-mers whose
+// b_prefix4 lies in their interval.
+template <bool STORE>
+__global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
+                                                             int canonical, uint32_t p4_lo, uint32_t p4_hi,
+                                                             uint32_t *__restrict__ cnt_r, uint32_t *__restrict__ cnt_h,
+                                                             const uint32_t *__restrict__ off_r,
+                                                             const uint32_t *__restrict__ off_h,
+                                                             uint32_t *__restrict__ out_r, uint32_t *__restrict__ out_h) {
     __shared__ uint32_t s_dol[kFlagGroups], s_bad[kFlagGroups], s_diff[kFlagGroups];
     __shared__ uint8_t s_lut4[256], s_comp[256];
+    __shared__ uint32_t s_w[2][4];
     s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
     s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
     const bool ranged = p4_lo != 0 || p4_hi != 0x10000u;
@@ -91,7 +103,7 @@ __global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__res
     for (int g = threadIdx.x; g < kFlagGroups; g += 256) {
         const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
         const uint4 ra = src[0], rb = src[1];
-        const uint32_t nxt = sba[P0 + 32ull * (g + 1)];  // the next group's first byte
+        const uint32_t nxt = sba[P0 + 32ull * (g + 1)];
         const uint32_t wv[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
         uint32_t dm = 0, bm = 0, fm = 0;
 #pragma unroll
@@ -100,42 +112,58 @@ __global__ __launch_bounds__(256) void class_b_flags_kernel(const uint8_t *__res
             const uint32_t cn = q < 31 ? (wv[(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 0xFFu : nxt;
             dm = (dm << 1) | (ch == GK_DOLLAR ? 1u : 0u);
             bm = (bm << 1) | ((ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T') ? 0u : 1u);
-            fm = (fm << 1) | (ch != cn ? 1u : 0u);  // position q differs from q + 1
+            fm = (fm << 1) | (ch != cn ? 1u : 0u);
         }
         s_dol[g] = dm;
         s_bad[g] = bm;
         s_diff[g] = fm;
     }
     __syncthreads();
-    // thread t: positions 32 t .. 32 t + 31 -> 32 flag bytes of each kind (two 16-B stores)
     const uint32_t p0 = threadIdx.x * 32;
-    uint32_t out[8], hout[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        uint32_t v = 0, h = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t p = p0 + 4 * w + b;
+    uint32_t mr = 0, mh = 0;  // bit j: position p0 + j
+    if (s_bad[threadIdx.x] | s_bad[threadIdx.x + 1] | s_bad[threadIdx.x + 2]) {  // a non-ACGT byte nearby
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t p = p0 + j;
             bool f = P0 + p < L && window_clear(s_dol, p, k) && !window_clear(s_bad, p, k);
+            if (!f) continue;
             const bool hp = k == 1 || window_clear(s_diff, p, k - 1);
-            if (ranged && f) {
+            if (ranged) {
                 const uint32_t p4 = b_prefix4(sba, P0 + p, k, hp, canonical, s_lut4, s_comp);
-                f = p4 >= p4_lo && p4 < p4_hi;
+                if (p4 < p4_lo || p4 >= p4_hi) continue;
             }
-            v |= (f && !hp ? 1u : 0u) << (8 * b);
-            h |= (f && hp ? 1u : 0u) << (8 * b);
+            if (hp) mh |= 1u << j;
+            else mr |= 1u << j;
         }
-        out[w] = v;
-        hout[w] = h;
     }
-    if (P0 + p0 < L) {
-        uint4 *dst = reinterpret_cast<uint4 *>(flags + P0 + p0);
-        dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
-        dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
-        uint4 *hd = reinterpret_cast<uint4 *>(homo + P0 + p0);
-        hd[0] = make_uint4(hout[0], hout[1], hout[2], hout[3]);
-        hd[1] = make_uint4(hout[4], hout[5], hout[6], hout[7]);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t cr = (uint32_t)__popc(mr), ch = (uint32_t)__popc(mh), ir = cr, ih = ch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yr = __shfl_up(ir, o), yh = __shfl_up(ih, o);
+        if (lane >= o) {
+            ir += yr;
+            ih += yh;
+        }
     }
+    if (lane == 63) {
+        s_w[0][wave] = ir;
+        s_w[1][wave] = ih;
+    }
+    __syncthreads();
+    if (!STORE) {
+        if (threadIdx.x == 0) {
+            cnt_r[blockIdx.x] = s_w[0][0] + s_w[0][1] + s_w[0][2] + s_w[0][3];
+            cnt_h[blockIdx.x] = s_w[1][0] + s_w[1][1] + s_w[1][2] + s_w[1][3];
+        }
+        return;
+    }
+    uint32_t orr = off_r[blockIdx.x] + ir - cr, oh = off_h[blockIdx.x] + ih - ch;
+    for (uint32_t w = 0; w < wave; ++w) {
+        orr += s_w[0][w];
+        oh += s_w[1][w];
+    }
+    for (uint32_t m = mr; m; m &= m - 1) out_r[orr++] = (uint32_t)(P0 + p0 + __ffs(m) - 1);
+    for (uint32_t m = mh; m; m &= m - 1) out_h[oh++] = (uint32_t)(P0 + p0 + __ffs(m) - 1);
 }
 
 // homopolymer k-mers by (canonical) letter: counts per letter; flags of one letter
@@ -311,20 +339,26 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, split_tables());
     int slot;
     // 1. class B starts: homopolymers (one letter k times) apart from the rest
-    uint8_t *fB, *fH;
     uint32_t *b_st[2], *h_st;
-    GK_TRY_HIP(c, scratch(c, "split_flags", L + kFlagTile + 64, &fB));
-    GK_TRY_HIP(c, scratch(c, "split_hflags", L + kFlagTile + 64, &fH));
+    const unsigned ftiles = (unsigned)((L + kFlagTile - 1) / kFlagTile);
+    uint32_t *cr, *chh, *orr, *ohh;
+    GK_TRY_HIP(c, scratch(c, "split_cnt_r", ftiles + 1, &cr));
+    GK_TRY_HIP(c, scratch(c, "split_cnt_h", ftiles + 1, &chh));
+    GK_TRY_HIP(c, scratch(c, "split_off_r", ftiles + 1, &orr));
+    GK_TRY_HIP(c, scratch(c, "split_off_h", ftiles + 1, &ohh));
+    const uint32_t p4_lo = rg ? rg->p4_lo : 0u, p4_hi = rg ? rg->p4_hi : 0x10000u;
     timer_begin(c, "split_b_select", &slot);
-    hipLaunchKernelGGL(class_b_flags_kernel, dim3((unsigned)((L + kFlagTile - 1) / kFlagTile)), dim3(256), 0,
-                       c->stream, c->sba, L, k, fB, fH, ks.canonical, rg ? rg->p4_lo : 0u, rg ? rg->p4_hi : 0x10000u);
+    hipLaunchKernelGGL(class_b_select_kernel<false>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
+                       ks.canonical, p4_lo, p4_hi, cr, chh, nullptr, nullptr, nullptr, nullptr);
     GK_TRY_HIP(c, hipGetLastError());
     uint64_t nR = 0, nH = 0;
-    // count first: the select outputs need their counts of entries, which may be up to n
-    GK_TRY_HIP(c, scratch(c, "split_b_st0", n + 64, &b_st[0]));
-    GK_TRY_HIP(c, select_flags(c, fB, L, b_st[0], &nR));
-    GK_TRY_HIP(c, scratch(c, "split_h_st", n + 64, &h_st));
-    GK_TRY_HIP(c, select_flags(c, fH, L, h_st, &nH));
+    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cr, ftiles, orr, &nR));
+    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, chh, ftiles, ohh, &nH));
+    GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &b_st[0]));
+    GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &h_st));
+    hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
+                       ks.canonical, p4_lo, p4_hi, nullptr, nullptr, orr, ohh, b_st[0], h_st);
+    GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     const uint64_t nB = nR + nH;
     if (nB > n) return fail(c, GK_E_HIP, "split: more class-B k-mers than k-mers");
@@ -337,6 +371,12 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     uint8_t *b_heads;
     int bres = 0;
     GK_TRY_HIP(c, scratch(c, "split_b_st1", nB + 64, &b_st[1]));
+    if (nH > 0 && nR + 64 < nB + 64) {  // b_st[0] also receives the assembled B order (bres flips)
+        uint32_t *grown;
+        GK_TRY_HIP(c, scratch(c, "split_b_st0g", nB + 64, &grown));
+        GK_TRY_HIP(c, hipMemcpyAsync(grown, b_st[0], 4 * nR, hipMemcpyDeviceToDevice, c->stream));
+        b_st[0] = grown;
+    }
     GK_TRY_HIP(c, scratch(c, "split_b_heads", nB + 64, &b_heads));
     if (nR > 0) {
         const int W = ks.words;

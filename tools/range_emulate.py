@@ -23,8 +23,9 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3")
     ap.add_argument("--genome-len", type=int, default=3_100_000_000)
-    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--worlds", type=str, default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
@@ -33,20 +34,24 @@ def main():
     from genome_kmers import _native
     from genome_kmers import distributed as D
 
-    sba, seg = bench.make_genome(args.genome_len, 42), np.zeros(1, dtype=np.uint32)
-    k = args.k
+    if args.config == "c3":
+        sba, seg = bench.make_genome(args.genome_len, 42), np.zeros(1, dtype=np.uint32)
+    else:
+        sba, seg = bench.make_grch38_surrogate(2)
+    k = args.k or (63 if args.config == "c5" else 31)
+    canonical = args.config == "c5"
     e = _native.Engine(0)
     e.set_sequence(sba, seg)
     e.sync()
     total = D.count_kmers(len(sba), seg, k)
     # single-GPU reference step for the same engine
     e.enumerate(k)
-    e.sort(k)
+    e.sort(k, canonical=canonical)
     e.unique_count_only()
     e.sync()
     t0 = time.perf_counter()
     e.enumerate(k)
-    e.sort(k)
+    e.sort(k, canonical=canonical)
     u1 = e.unique_count_only()
     e.sync()
     single_ms = (time.perf_counter() - t0) * 1e3
@@ -60,7 +65,7 @@ def main():
         # the all-reduced histogram (every rank's share), outside the per-rank timings
         full = np.zeros(256, dtype=np.int64)
         for s in range(world):
-            h, bits = e.shard_histogram(pb[s], pb[s + 1], k)
+            h, bits = e.shard_histogram(pb[s], pb[s + 1], k, canonical=canonical)
             full[:len(h)] += h.astype(np.int64)
         db = D.split_buckets(full[:1 << bits], world)
         for r in range(world):
@@ -69,8 +74,8 @@ def main():
                 e.sync()
                 e.profile_enable(rep == args.reps)
                 t0 = time.perf_counter()
-                e.shard_histogram(pb[r], pb[r + 1], k)  # the rank's own share (its part of the all-reduce)
-                n = e.shard_sort_range(k, db[r], db[r + 1])
+                e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share of the all-reduce
+                n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
                 u = e.unique_count_only()
                 e.sync()
                 dt = time.perf_counter() - t0
@@ -84,7 +89,7 @@ def main():
             per_rank.append(round(best * 1e3, 2))
             uniq += u
             kept += n
-        assert kept == total, (kept, total)
+        assert kept == total, (kept, total)  # every k-mer on exactly one rank
         worst = max(per_rank)
         print(json.dumps({"world": world, "per_rank_ms": per_rank, "max_rank_ms": worst,
                           "kmers_per_s": round(total / (worst * 1e-3), 1),

@@ -1376,6 +1376,13 @@ static unsigned cu_count(gk_ctx *c) {
     return (unsigned)(cus / 8 * 8);
 }
 
+// Packing is opt-in (GKM_PACK=1): measured on MI355X, the L0 partition got slower reading packed
+// words (17.8 vs 16.4 ms at C3) and the key-range passes gained less than the 0.8 ms packing costs.
+static bool use_pack() {
+    static const bool on = std::getenv("GKM_PACK") != nullptr;
+    return on;
+}
+
 // the packed copy of c->sba (pack2_kernel) over the whole padded array, for ACGT sequences
 static int pack_sequence(gk_ctx *c, const uint64_t **code, const uint32_t **dol) {
     const uint64_t nwords = (c->sba_len + kSbaPad) / 32;  // sba_cap >= sba_len + kSbaPad
@@ -1892,22 +1899,30 @@ struct MsdDriver {
         // the first wave round of phase 0, where random keys differ right below the sorted bits
         const int skip = (round > 0 || phase > 0 || k == 3) ? 1 : 0;
         const uint32_t small = (round > 0 || phase > 0) ? kSmallLate : kSmall;
+        // persistent grids of the workgroups that fit at once (occupancy API, per kernel)
+        auto grid = [&](const void *fn, int threads) {
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess || per_cu < 1)
+                per_cu = 1;
+            return dim3((unsigned)std::min<uint64_t>(cnt, (uint64_t)cus * per_cu));
+        };
         switch (k) {
         case 0:
-            hipLaunchKernelGGL((msd_wave_kernel<4>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 32)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+            hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 1:
-            hipLaunchKernelGGL((msd_wave_kernel<8>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 16)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+            hipLaunchKernelGGL((msd_wave_kernel<8>), grid((const void *)msd_wave_kernel<8>, 64), dim3(64), 0,
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 2:
-            hipLaunchKernelGGL((msd_wave_kernel<16>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)), dim3(64),
-                               0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+            hipLaunchKernelGGL((msd_wave_kernel<16>), grid((const void *)msd_wave_kernel<16>, 64), dim3(64), 0,
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 3:
-            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>), dim3((unsigned)std::min<uint64_t>(cnt, cus * 8)),
-                               dim3(kBT), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
+            hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
+                               grid((const void *)msd_local_kernel<kBT, kBI, kBR>, kBT), dim3(kBT), 0, c->stream, lst,
+                               cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
                                (uint32_t)kSmall);  // the block class keeps kSmall: measured slower at 96
             break;
         default:
@@ -1997,7 +2012,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
-    if (c->acgt && ks.bits == 2 && !ks.acgt_only) {  // both L0 passes read the packed sequence
+    if (use_pack() && c->acgt && ks.bits == 2 && !ks.acgt_only) {  // both L0 passes read the packed sequence
         rc = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rc != GK_OK) return rc;
         c->pk_fresh = false;
@@ -2067,7 +2082,7 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
     GK_TRY_HIP(c, msd_tables());
     // the packed sequence is made here for the whole sba and kept for the gk_shard_sort_range
     // that follows (one packing per key-range step)
-    if (c->acgt && ks.bits == 2) {
+    if (use_pack() && c->acgt && ks.bits == 2) {
         int rp = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rp != GK_OK) return rp;
     }
@@ -2097,7 +2112,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     L0Args a{c->sba, 0, L, ks.symbols, d.B, ks.acgt_only};
     a.own_lo = digit_lo;
     a.own_span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
-    if (c->acgt && ks.bits == 2) {  // the packed sequence of this step's gk_shard_histogram, or pack now
+    if (use_pack() && c->acgt && ks.bits == 2) {  // this step's gk_shard_histogram's packing, or pack now
         if (c->pk_fresh) {
             uint64_t *pc;
             uint32_t *pd;
@@ -2118,14 +2133,23 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     GK_TRY_HIP(c, scratch(c, "sel_wave_off", nw + 1, &wave_off));
     c->n = 0;  // nothing in the buffers survives: ensure_elems copies none
     c->cur = 0;
-    const unsigned sgrid = std::min<unsigned>(ntiles, d.cus * 6);
     auto launch = [&](bool store) {
         uint64_t *ko = store ? c->keys[0] : nullptr;
         uint32_t *vo = store ? c->vals[0] : nullptr;
         uint8_t *no = store ? d.nd : nullptr;
-#define GK_SEL(B_, C_, S_)                                                                                   \
-    hipLaunchKernelGGL((msd0_select_kernel<B_, C_, S_>), dim3(sgrid), dim3(kST), 0, c->stream, a, d0, ntiles,    \
-                       wave_cnt, wave_off, ko, vo, no)
+        // persistent grid = the workgroups that fit at once (a second round of workgroups would
+        // start only when the first ones have walked all their tiles)
+#define GK_SEL(B_, C_, S_)                                                                                    \
+    do {                                                                                                      \
+        int per_cu = 0;                                                                                       \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, msd0_select_kernel<B_, C_, S_>, kST, 0) !=  \
+                hipSuccess ||                                                                                 \
+            per_cu < 1)                                                                                       \
+            per_cu = 1;                                                                                       \
+        const unsigned sgrid = std::min<unsigned>(ntiles, d.cus * (unsigned)per_cu);                          \
+        hipLaunchKernelGGL((msd0_select_kernel<B_, C_, S_>), dim3(sgrid), dim3(kST), 0, c->stream, a, d0,     \
+                           ntiles, wave_cnt, wave_off, ko, vo, no);                                           \
+    } while (0)
         if (ks.bits == 2 && ks.canonical) { if (store) GK_SEL(2, true, true); else GK_SEL(2, true, false); }
         else if (ks.bits == 2) { if (store) GK_SEL(2, false, true); else GK_SEL(2, false, false); }
         else if (ks.canonical) { if (store) GK_SEL(4, true, true); else GK_SEL(4, true, false); }

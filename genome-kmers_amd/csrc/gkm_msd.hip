@@ -1255,21 +1255,136 @@ __global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__
     }
 }
 
-// Multi-word keys: the groups of >= 2 equal earlier words, from the head flags of the order so far:
-// f_first[i] = first element of such a group, f_last[i] = its last element.
-__global__ __launch_bounds__(256) void tie_run_flags_kernel(const uint8_t *__restrict__ heads, uint64_t n,
-                                                            uint8_t *__restrict__ f_first, uint8_t *__restrict__ f_last) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const bool h = heads[i] != 0, hn = i + 1 >= n || heads[i + 1] != 0;
-        f_first[i] = h && !hn;
-        f_last[i] = !h && hn;
+// Multi-word keys: the groups of >= 2 equal earlier words, from the head flags of the order so far.
+// The first and last element of every such group, in two light passes over the head flags (no
+// flag arrays): COUNT writes per 8192-element tile the numbers of group firsts and lasts; after
+// their scans, STORE writes the indices from the tile's offsets (thread t owns elements
+// 32 t .. 32 t + 31 of the tile, so thread order = index order).
+constexpr int kTieTile = 8192;
+
+template <bool STORE>
+__global__ __launch_bounds__(256) void tie_bounds_kernel(const uint8_t *__restrict__ heads, uint64_t n,
+                                                         uint32_t *__restrict__ cnt_f, uint32_t *__restrict__ cnt_l,
+                                                         const uint32_t *__restrict__ off_f,
+                                                         const uint32_t *__restrict__ off_l,
+                                                         uint32_t *__restrict__ first, uint32_t *__restrict__ last) {
+    __shared__ uint32_t s_w[2][4];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kTieTile + threadIdx.x * 32;
+    uint32_t mf = 0, ml = 0;
+    if (i0 < n) {
+        // 33 head flags from i0 (past n reads as a head: the group ends there)
+        uint32_t hb = 0;
+        if (i0 + 33 <= n) {
+            const uint4 *h4 = reinterpret_cast<const uint4 *>(heads + i0);  // i0 % 32 == 0
+            const uint4 a = h4[0], b = h4[1];
+            const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int q = 0; q < 32; ++q) hb |= (((wv[q >> 2] >> (8 * (q & 3))) & 0xFFu) != 0 ? 1u : 0u) << q;
+            const bool h32 = heads[i0 + 32] != 0;
+            const uint32_t nxt = (hb >> 1) | ((h32 ? 1u : 0u) << 31);  // bit q: element i0 + q + 1 is a head
+            mf = hb & ~nxt;
+            ml = ~hb & nxt;
+        } else {
+            for (int q = 0; q < 32 && i0 + q < n; ++q) {
+                const bool h = heads[i0 + q] != 0, hn = i0 + q + 1 >= n || heads[i0 + q + 1] != 0;
+                mf |= (h && !hn ? 1u : 0u) << q;
+                ml |= (!h && hn ? 1u : 0u) << q;
+            }
+        }
     }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cf = (uint32_t)__popc(mf), cl = (uint32_t)__popc(ml);
+    uint32_t inf = cf, inl = cl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yf = __shfl_up(inf, o), yl = __shfl_up(inl, o);
+        if (lane >= o) {
+            inf += yf;
+            inl += yl;
+        }
+    }
+    if (lane == 63) {
+        s_w[0][wave] = inf;
+        s_w[1][wave] = inl;
+    }
+    __syncthreads();
+    if (!STORE) {
+        if (threadIdx.x == 0) {
+            cnt_f[blockIdx.x] = s_w[0][0] + s_w[0][1] + s_w[0][2] + s_w[0][3];
+            cnt_l[blockIdx.x] = s_w[1][0] + s_w[1][1] + s_w[1][2] + s_w[1][3];
+        }
+        return;
+    }
+    uint32_t of = off_f[blockIdx.x] + inf - cf, ol = off_l[blockIdx.x] + inl - cl;
+    for (uint32_t w = 0; w < wave; ++w) {
+        of += s_w[0][w];
+        ol += s_w[1][w];
+    }
+    for (uint32_t m = mf; m; m &= m - 1) first[of++] = (uint32_t)(i0 + __ffs(m) - 1);
+    for (uint32_t m = ml; m; m &= m - 1) last[ol++] = (uint32_t)(i0 + __ffs(m) - 1);
 }
 
 __global__ __launch_bounds__(256) void tie_run_lengths_kernel(const uint32_t *__restrict__ first,
                                                               uint32_t *__restrict__ last_to_len, uint64_t ng) {
     for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * 256)
         last_to_len[g] = last_to_len[g] - first[g] + 1;
+}
+
+// Key word of symbols [sym0, sym0 + nsym) of the (canonical) k-mer at p, 2-bit codes, from 17
+// aligned dword loads (issued together) instead of one dependent byte load per symbol: the
+// k-mer's codes as a left-aligned 128-bit value F (SWAR per dword), its reverse complement by
+// two revcomp_word calls and a 128-bit shift, the smaller of the two, then the word.  k <= 64.
+__device__ __forceinline__ uint32_t codes4(uint32_t w) {  // 4 bytes -> 8 bits, byte 0 on top
+    uint32_t t = __builtin_bswap32(((w >> 1) ^ (w >> 2)) & 0x03030303u);
+    t = (t | (t >> 6)) & 0x000F000Fu;
+    return (t | (t >> 12)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint64_t tie_word2(const uint8_t *sba, uint32_t p, int k, int sym0, int nsym,
+                                              bool canonical) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(sba + (p & ~3u));
+    const int off = (int)(p & 3u);
+    uint64_t c0 = 0, c1 = 0;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c0 = (c0 << 8) | codes4(w[j]);
+#pragma unroll
+    for (int j = 8; j < 16; ++j) c1 = (c1 << 8) | codes4(w[j]);
+    c2 = codes4(w[16]);
+    // symbols 0 .. 63 from p: drop the first `off` symbols of the stream
+    const int sh = 2 * off;
+    uint64_t fh = sh ? (c0 << sh) | (c1 >> (64 - sh)) : c0;
+    uint64_t fl = sh ? (c1 << sh) | ((uint64_t)c2 >> (8 - sh)) : c1;
+    if (k < 64) {  // symbols past the k-mer read as 0
+        if (k <= 32) {
+            fh &= k == 32 ? ~0ull : ~(~0ull >> (2 * k));
+            fl = 0;
+        } else {
+            fl &= ~(~0ull >> (2 * (k - 32)));
+        }
+    }
+    if (canonical) {
+        // reverse complement of the 64-symbol value, then shifted left past the (64 - k) pad symbols
+        uint64_t rh = revcomp_word<2>(fl, 32), rl = revcomp_word<2>(fh, 32);
+        const int ps = 2 * (64 - k);
+        if (ps >= 64) {
+            rh = rl << (ps - 64);
+            rl = 0;
+        } else if (ps > 0) {
+            rh = (rh << ps) | (rl >> (64 - ps));
+            rl <<= ps;
+        }
+        if (rh < fh || (rh == fh && rl < fl)) {
+            fh = rh;
+            fl = rl;
+        }
+    }
+    // the word: symbols sym0 .. sym0 + nsym - 1 of (fh, fl)
+    const int b0 = 2 * sym0, nb = 2 * nsym;  // bit offset from the top, width
+    uint64_t x;
+    if (b0 >= 64) x = fl << (b0 - 64);
+    else x = b0 ? (fh << b0) | (fl >> (64 - b0)) : fh;
+    return nb >= 64 ? x : x >> (64 - nb);
 }
 
 // Flat variant of tie_encode_kernel for many groups: every element in a group of >= 2 (a head
@@ -1286,6 +1401,10 @@ __global__ __launch_bounds__(256) void tie_encode_flat_kernel(const uint8_t *__r
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const bool tie = heads[i] == 0 || (i + 1 < n && heads[i + 1] == 0);
         if (!tie) continue;
+        if (BITS == 2 && k <= 64) {
+            keys[i] = tie_word2(sba, vals[i], k, sym0, nsym, canonical != 0);
+            continue;
+        }
         const uint8_t *b = sba + vals[i];
         const bool rc = canonical && canon_is_rc<BITS>(b, k, s_lut4);
         uint64_t key = 0;
@@ -1328,6 +1447,10 @@ __global__ __launch_bounds__(256) void tie_encode_kernel(const uint8_t *__restri
         const uint32_t len = g_len[g];
         if (len < 2) continue;
         for (uint32_t i = lane; i < len; i += 64) {
+            if (BITS == 2 && k <= 64) {
+                keys[st + i] = tie_word2(sba, vals[st + i], k, sym0, nsym, canonical != 0);
+                continue;
+            }
             const uint8_t *b = sba + vals[st + i];
             const bool rc = canonical && canon_is_rc<BITS>(b, k, s_lut4);
             uint64_t key = 0;
@@ -1794,19 +1917,25 @@ struct MsdDriver {
     // Multi-word keys, phase > 0: the head flags of the order so far (buffer 0) mark the groups of
     // equal earlier words; sort each group of >= 2 by the key word of symbols [sym0, sym0 + nsym).
     int next_phase(int sym0, int nsym) {
-        uint8_t *f_first, *f_last;
         uint32_t *g_start, *g_len;
-        GK_TRY_HIP(c, scratch(c, "tie_f_first", n + 64, &f_first));
-        GK_TRY_HIP(c, scratch(c, "tie_f_last", n + 64, &f_last));
         timer_begin(c, "msd_tie_groups", &slot);
-        const unsigned fgrid = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 32);
-        hipLaunchKernelGGL(tie_run_flags_kernel, dim3(fgrid), dim3(256), 0, c->stream, heads, n, f_first, f_last);
+        const unsigned ttiles = (unsigned)std::max<uint64_t>((n + kTieTile - 1) / kTieTile, 1);
+        uint32_t *cf, *cl, *of, *ol;
+        GK_TRY_HIP(c, scratch(c, "tie_cnt_f", ttiles + 1, &cf));
+        GK_TRY_HIP(c, scratch(c, "tie_cnt_l", ttiles + 1, &cl));
+        GK_TRY_HIP(c, scratch(c, "tie_off_f", ttiles + 1, &of));
+        GK_TRY_HIP(c, scratch(c, "tie_off_l", ttiles + 1, &ol));
+        hipLaunchKernelGGL(tie_bounds_kernel<false>, dim3(ttiles), dim3(256), 0, c->stream, heads, n, cf, cl, nullptr,
+                           nullptr, nullptr, nullptr);
         GK_TRY_HIP(c, hipGetLastError());
         uint64_t ng = 0, ng2 = 0;
-        GK_TRY_HIP(c, scratch(c, "tie_start", n / 2 + 64, &g_start));
-        GK_TRY_HIP(c, scratch(c, "tie_len", n / 2 + 64, &g_len));
-        GK_TRY_HIP(c, select_flags(c, f_first, n, g_start, &ng));
-        GK_TRY_HIP(c, select_flags(c, f_last, n, g_len, &ng2));
+        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cf, ttiles, of, &ng));
+        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cl, ttiles, ol, &ng2));
+        GK_TRY_HIP(c, scratch(c, "tie_start", ng + 64, &g_start));
+        GK_TRY_HIP(c, scratch(c, "tie_len", ng2 + 64, &g_len));
+        hipLaunchKernelGGL(tie_bounds_kernel<true>, dim3(ttiles), dim3(256), 0, c->stream, heads, n, nullptr, nullptr,
+                           of, ol, g_start, g_len);
+        GK_TRY_HIP(c, hipGetLastError());
         if (ng != ng2) return fail(c, GK_E_HIP, "msd: tie group bounds do not pair up");
         if (ng > 0)
             hipLaunchKernelGGL(tie_run_lengths_kernel, dim3((unsigned)std::min<uint64_t>((ng + 255) / 256, 8192)),

@@ -1043,8 +1043,8 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 // counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
 // in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
 // -- the ranks are stable.  About 12 VALU per item instead of about 50.
-template <int I>
-__global__ __launch_bounds__(64) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
+template <int I, int MINW = 1>
+__global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
                                                       uint32_t *__restrict__ ctr, int skip, uint32_t small) {
@@ -2036,16 +2036,18 @@ struct MsdDriver {
             return dim3((unsigned)std::min<uint64_t>(cnt, (uint64_t)cus * per_cu));
         };
         switch (k) {
-        case 0:
+        case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)
             hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
                                c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
-        case 1:
-            hipLaunchKernelGGL((msd_wave_kernel<8>), grid((const void *)msd_wave_kernel<8>, 64), dim3(64), 0,
+        case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
+                 // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
+            hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
                                c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
-        case 2:
-            hipLaunchKernelGGL((msd_wave_kernel<16>), grid((const void *)msd_wave_kernel<16>, 64), dim3(64), 0,
+        case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
+                 // on C5 (A/B, one box)
+            hipLaunchKernelGGL((msd_wave_kernel<16, 3>), grid((const void *)msd_wave_kernel<16, 3>, 64), dim3(64), 0,
                                c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
             break;
         case 3:

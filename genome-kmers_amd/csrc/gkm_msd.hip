@@ -31,7 +31,7 @@ constexpr int kGRadix = 1 << kGR;
 constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
 constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk
-constexpr int kBT = 256, kBI = 16, kBR = 8;   // block-local: 256 threads x 16 keys, 8-bit digit
+constexpr int kBT = 512, kBI = 8, kBR = 8;    // block-local: 512 threads x 8 keys, 8-bit digit
 constexpr int kBlockMax = kBT * kBI;    // 4096
 // local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
 // 4 or 16 keys (msd_local_kernel)

@@ -2054,7 +2054,7 @@ struct MsdDriver {
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
                                grid((const void *)msd_local_kernel<kBT, kBI, kBR>, kBT), dim3(kBT), 0, c->stream, lst,
                                cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
-                               (uint32_t)kSmall);  // the block class keeps kSmall: measured slower at 96
+                               (uint32_t)kSmall);  // the block class keeps kSmall: 96 measured slower (A/B)
             break;
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,

@@ -97,6 +97,48 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
+// Many tile sums (a 3.1e9-element selection has 757 k): the single-block scan above walks them in
+// 740 sequential steps (~0.7 ms); instead chunks of 16384 are scanned in parallel, the chunk
+// totals by one block, and the chunk offsets added back.
+constexpr int kScanChunk = 16384;
+
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__ sums, uint64_t ntiles,
+                                                          uint32_t *__restrict__ chunk_tot) {
+    __shared__ uint32_t s_tmp[16];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanChunk;
+    uint32_t carry = 0;
+    for (int j = 0; j < kScanChunk; j += 1024) {
+        const uint64_t i = b0 + j + threadIdx.x;
+        const uint32_t v = i < ntiles ? sums[i] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<1024>(v, s_tmp, &tot);
+        if (i < ntiles) sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) chunk_tot[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(256) void chunk_add_kernel(uint32_t *__restrict__ sums, uint64_t ntiles,
+                                                        const uint32_t *__restrict__ chunk_off) {
+    const uint32_t add = chunk_off[blockIdx.x];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanChunk;
+    for (uint32_t j = threadIdx.x; j < (uint32_t)kScanChunk; j += 256)
+        if (b0 + j < ntiles) sums[b0 + j] += add;
+}
+
+// exclusive scan of ntiles tile sums in place, grand total -> *total (device)
+static void scan_tile_sums(gk_ctx *c, uint32_t *sums, uint64_t ntiles, uint64_t *total) {
+    if (ntiles <= (uint64_t)4 * kScanChunk) {
+        hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, sums, ntiles, total);
+        return;
+    }
+    const uint64_t nch = (ntiles + kScanChunk - 1) / kScanChunk;
+    uint32_t *chunk = sums + ntiles + 16;  // ensure_tile_sums leaves room for the chunk totals
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, c->stream, sums, ntiles, chunk);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, chunk, nch, total);
+    hipLaunchKernelGGL(chunk_add_kernel, dim3((unsigned)nch), dim3(256), 0, c->stream, sums, ntiles, chunk);
+}
+
 // Thread t loads the 16 flags of positions 16t..16t+15 (one 16-B load), writes its selected
 // positions to LDS after a block scan, and the tile's list is then copied out as one contiguous
 // run.  The LDS index is XOR-swizzled within 32-word rows: dense flags (every k-mer distinct)
@@ -163,7 +205,9 @@ __global__ __launch_bounds__(kScanThreads) void u32_scan_apply_kernel(const uint
 }
 
 static hipError_t ensure_tile_sums(gk_ctx *c, uint64_t ntiles) {
-    return ensure(reinterpret_cast<void **>(&c->tile_sums), &c->tile_sums_cap, 4 * (ntiles + 16));
+    // + the chunk totals of scan_tile_sums
+    return ensure(reinterpret_cast<void **>(&c->tile_sums), &c->tile_sums_cap,
+                  4 * (ntiles + 16 + ntiles / kScanChunk + 16));
 }
 
 static hipError_t read_total(gk_ctx *c, uint64_t *count) {
@@ -179,7 +223,7 @@ hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *o
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(flag_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
                        c->tile_sums);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
     hipLaunchKernelGGL(flag_select_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
                        c->tile_sums, out_idx);
     e = hipGetLastError();
@@ -194,7 +238,7 @@ hipError_t scan_flags_inclusive(gk_ctx *c, const uint8_t *flags, uint64_t n, uin
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(flag_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
                        c->tile_sums);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
     hipLaunchKernelGGL(flag_scan_incl_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
                        c->tile_sums, out);
     return hipGetLastError();
@@ -207,7 +251,7 @@ static hipError_t scan_u32_exclusive(gk_ctx *c, const uint32_t *in, uint64_t n, 
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(u32_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
                        c->tile_sums);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, c->tile_sums, ntiles, c->scalars);
+    scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
     hipLaunchKernelGGL(u32_scan_apply_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
                        c->tile_sums, out);
     e = hipGetLastError();

@@ -314,6 +314,40 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     assert uniq == ref.unique_count_only()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,k", [(4, 31), (7, 25)])
+def test_gpu_key_range_repeated_calls(world, k):
+    """Repeated gk_shard_sort_range calls on one engine over hundreds of select tiles, ranges in
+    growing then shrinking size order (buffers grown, then reused): each call keeps exactly its
+    histogram's k-mers, repeats its own first result, and the ranks concatenate to gk_sort."""
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(3_000_017, 11 + world, 1)
+    sba[2_000_000:2_004_000] = sba[10_000:14_000]  # ties across distant tiles
+    bounds = D.position_ranges(len(sba), world)
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    hist = None
+    for r in range(world):
+        h, _ = e.shard_histogram(bounds[r], bounds[r + 1], k)
+        hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
+    db = D.split_buckets(hist, world)
+    order = sorted(range(world), key=lambda r: int(hist[db[r]:db[r + 1]].sum()))  # growing ranges
+    got = {}
+    for r in order + order[::-1]:
+        n = e.shard_sort_range(k, db[r], db[r + 1])
+        assert n == int(hist[db[r]:db[r + 1]].sum())
+        starts = e.copy_starts()
+        if r in got:
+            np.testing.assert_array_equal(starts, got[r])
+        got[r] = starts
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(k)
+    ref.sort(k)
+    np.testing.assert_array_equal(np.concatenate([got[r] for r in range(world)]), ref.copy_starts())
+
+
 def _gpu_range_worker(rank, world, port, sba, seg, k, q):
     import torch
     import torch.distributed as dist

@@ -23,6 +23,7 @@
 #include "gkm_canon.h"
 #include "gkm_internal.h"
 #include "gkm_partition.h"
+#include "gkm_swar.h"
 
 namespace gkm {
 
@@ -110,20 +111,6 @@ __device__ __forceinline__ void l0_load(const L0Args &a, uint64_t P0, uint64_t (
     for (int j = 0; j < U::kPer; ++j) r[j] = s8[min((uint32_t)(threadIdx.x + j * T), (uint32_t)U::kUnits - 1)];
 }
 
-// SWAR over 8 bytes (byte 0 = the first position): bit 7 of each byte set iff the byte is zero
-__device__ __forceinline__ uint64_t zero_bytes(uint64_t y) {
-    constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full;
-    return ~(((y & k7F) + k7F) | y | k7F);
-}
-
-// the 8 flag bits (bit 7 of each byte) as one byte, position 0 in the most significant bit
-__device__ __forceinline__ uint32_t gather_flags8(uint64_t z) {
-    uint64_t t = __builtin_bswap64(z) >> 7;
-    t = (t | (t >> 7)) & 0x0003000300030003ull;
-    t = (t | (t >> 14)) & 0x0000000F0000000Full;
-    return (uint32_t)((t | (t >> 28)) & 0xFFu);
-}
-
 // 2-bit codes (A0 C1 G2 T3) of 8 bytes as 16 bits, position 0 in the most significant pair
 __device__ __forceinline__ uint32_t pack2_8(uint64_t x) {
     uint64_t t = __builtin_bswap64(((x >> 1) ^ (x >> 2)) & 0x0303030303030303ull);
@@ -156,8 +143,7 @@ __device__ __forceinline__ void l0_pack(const uint64_t (&r)[L0Units<BITS, TILE, 
             const uint64_t x = r[j];
             uint64_t z;
             if (acgt_only)
-                z = ~(zero_bytes(x ^ (kOnes * 'A')) | zero_bytes(x ^ (kOnes * 'C')) | zero_bytes(x ^ (kOnes * 'G')) |
-                      zero_bytes(x ^ (kOnes * 'T'))) & (kOnes << 7);
+                z = non_acgt_bytes(x);
             else
                 z = zero_bytes(x ^ (kOnes * GK_DOLLAR));
             reinterpret_cast<uint8_t *>(s_dol)[(u & ~3u) + 3 - (u & 3u)] = (uint8_t)gather_flags8(z);

@@ -17,6 +17,7 @@
 
 #include "gkm_canon.h"
 #include "gkm_internal.h"
+#include "gkm_swar.h"
 
 namespace gkm {
 
@@ -104,15 +105,20 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
         const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
         const uint4 ra = src[0], rb = src[1];
         const uint32_t nxt = sba[P0 + 32ull * (g + 1)];
-        const uint32_t wv[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        // SWAR, 8 positions per step: '$' flags, non-ACGT flags, and "differs from the next byte"
+        // flags (each byte against its successor: the unit shifted down one byte, the next unit's
+        // first byte on top)
+        constexpr uint64_t kOnes = 0x0101010101010101ull;
+        const uint64_t x[4] = {((uint64_t)ra.y << 32) | ra.x, ((uint64_t)ra.w << 32) | ra.z,
+                               ((uint64_t)rb.y << 32) | rb.x, ((uint64_t)rb.w << 32) | rb.z};
         uint32_t dm = 0, bm = 0, fm = 0;
 #pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            const uint32_t ch = (wv[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-            const uint32_t cn = q < 31 ? (wv[(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 0xFFu : nxt;
-            dm = (dm << 1) | (ch == GK_DOLLAR ? 1u : 0u);
-            bm = (bm << 1) | ((ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T') ? 0u : 1u);
-            fm = (fm << 1) | (ch != cn ? 1u : 0u);
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t nb = j < 3 ? (x[j + 1] & 0xFFu) : (uint64_t)nxt;
+            const uint64_t y = (x[j] >> 8) | (nb << 56);
+            dm = (dm << 8) | gather_flags8(zero_bytes(x[j] ^ (kOnes * GK_DOLLAR)));
+            bm = (bm << 8) | gather_flags8(non_acgt_bytes(x[j]));
+            fm = (fm << 8) | gather_flags8(~zero_bytes(x[j] ^ y) & (kOnes << 7));
         }
         s_dol[g] = dm;
         s_bad[g] = bm;
@@ -121,7 +127,19 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
     __syncthreads();
     const uint32_t p0 = threadIdx.x * 32;
     uint32_t mr = 0, mh = 0;  // bit j: position p0 + j
-    if (s_bad[threadIdx.x] | s_bad[threadIdx.x + 1] | s_bad[threadIdx.x + 2]) {  // a non-ACGT byte nearby
+    const uint32_t g = threadIdx.x;
+    // inside a run of one non-ACGT letter (GRCh38's N runs) that covers every window of the
+    // thread's 32 positions, all 32 start homopolymer B k-mers with the same (canonical) prefix
+    const bool run = (s_bad[g] >> 31) != 0 && s_dol[g] == 0 && (k < 2 || window_clear(s_dol, p0 + 32, k - 1)) &&
+                     s_diff[g] == 0 && (k < 3 || window_clear(s_diff, p0 + 32, k - 2)) && P0 + p0 + 31 < L;
+    if (run) {
+        bool keep = true;
+        if (ranged) {
+            const uint32_t p4 = b_prefix4(sba, P0 + p0, k, true, canonical, s_lut4, s_comp);
+            keep = p4 >= p4_lo && p4 < p4_hi;
+        }
+        if (keep) mh = 0xFFFFFFFFu;
+    } else if (s_bad[g] | s_bad[g + 1] | s_bad[g + 2]) {  // a non-ACGT byte nearby
         for (int j = 0; j < 32; ++j) {
             const uint32_t p = p0 + j;
             bool f = P0 + p < L && window_clear(s_dol, p, k) && !window_clear(s_bad, p, k);

@@ -217,6 +217,12 @@ __device__ __forceinline__ uint64_t win8_key(const Win8 &w, int i, int B) {
     return B >= 64 ? Ti : Ti >> (64 - B);
 }
 
+// the 32 symbols from position q of a packed 2-bit tile, MSB first (any q)
+__device__ __forceinline__ uint64_t win32_at(const uint64_t *s_code, uint32_t q) {
+    const uint32_t w = q >> 5, s = (q & 31) * 2;
+    return s ? (s_code[w] << s) | (s_code[w + 1] >> (64 - s)) : s_code[w];
+}
+
 // wave-uniform call (a ballot inside)
 __device__ __forceinline__ uint32_t win8_keep(const Win8 &w, const L0Args &a, Dig d0, int64_t left,
                                               const uint32_t *s_dol, uint32_t q0, uint32_t (&dig)[8]) {
@@ -276,11 +282,37 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                     if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i]], 1u);
             }
         } else {
+            // canonical 2-bit keys in a tile without stops: the digit is the smaller of the forward
+            // and the reverse-complement top 7 bits, 8 consecutive positions per thread from two
+            // 32-symbol windows (at q0 and at q0 + k - 4)
+            bool fast = false;
+            if constexpr (BITS == 2 && CANON) {
+                uint32_t anystop = 0;
+                for (int j = t; j < P::kGroups; j += T) anystop |= s_dol[j];
+                fast = __syncthreads_or(anystop != 0) == 0 && P0 + TILE <= a.hi && d0.mask == 0x7Fu &&
+                       (int)d0.shift == a.total_bits - 7 && a.symbols >= 4;
+                if (fast) {
+                    for (uint32_t g = t; g < TILE / 8; g += T) {
+                        const uint32_t q0 = g * 8;
+                        const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - 4);
 #pragma unroll
-            for (int i = 0; i < I; ++i) {
-                const uint32_t p = i * T + t;
-                const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
-                if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+                        for (int i = 0; i < 8; ++i) {
+                            const uint32_t f7 = (uint32_t)(tf >> (57 - 2 * i)) & 0x7Fu;
+                            const uint32_t v = (uint32_t)(tr >> (56 - 2 * i)) & 0xFFu;  // symbols q0+k-4+i ..
+                            const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
+                            const uint32_t d = min(f7, (~rv & 0xFFu) >> 1);
+                            if (l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+                        }
+                    }
+                }
+            }
+            if (!fast) {
+#pragma unroll
+                for (int i = 0; i < I; ++i) {
+                    const uint32_t p = i * T + t;
+                    const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
+                    if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+                }
             }
         }
         lds_barrier();

@@ -537,12 +537,36 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
         __syncthreads();
         // the next tile's bytes fly while this one is processed
         if (t + gridDim.x < ntiles) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)gridDim.x * kSTile, rr);
-        if constexpr (BITS == 2 && !CANON) {
+        bool win = BITS == 2;
+        // canonical: the count pass takes the digits from windows in a tile without stops; the store
+        // pass keeps the row layout below (a per-lane loop over the kept positions' canonical keys
+        // was slower: 11.9 against 8.3 ms per C5 rank at N = 8).  Both visit a wave's 512 positions
+        // in position order, so their per-wave counts and offsets agree.
+        if constexpr (BITS == 2 && CANON) {
+            if (STORE) win = false;
+            const uint32_t anystop = tid < P::kGroups ? s_dol[tid] : 0u;
+            win = win && __syncthreads_or(anystop != 0) == 0 && P0 + kSTile <= a.hi && d0.mask == 0x7Fu &&
+                  (int)d0.shift == a.total_bits - 7 && a.symbols >= 4;
+        }
+        if (BITS == 2 && win) {
             // 8 consecutive positions per thread (Win8)
             const uint32_t q0 = tid * 8;
-            const Win8 win = win8_load(s_code, s_dol, q0);
-            uint32_t dig[8];
-            const uint32_t keepm = win8_keep(win, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
+            Win8 win8{};
+            uint32_t keepm = 0;
+            if constexpr (!CANON) {
+                win8 = win8_load(s_code, s_dol, q0);
+                uint32_t dig[8];
+                keepm = win8_keep(win8, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
+            } else {  // the smaller of the forward and reverse-complement top 7 bits (msd0_count_kernel)
+                const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - 4);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t f7 = (uint32_t)(tf >> (57 - 2 * i)) & 0x7Fu;
+                    const uint32_t v = (uint32_t)(tr >> (56 - 2 * i)) & 0xFFu;
+                    const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
+                    keepm |= (l0_owned(min(f7, (~rv & 0xFFu) >> 1), a) ? 1u : 0u) << i;
+                }
+            }
             const uint32_t cnt = (uint32_t)__popc(keepm);
             uint32_t incl = cnt;
 #pragma unroll
@@ -561,7 +585,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             uint32_t j = incl - cnt;
             for (uint32_t m = keepm; m; m &= m - 1) {
                 const int i = __ffs(m) - 1;
-                sk[j] = win8_key(win, i, a.total_bits);
+                sk[j] = CANON ? l0_key_of<2, true>(s_code, q0 + i, a.total_bits, a.symbols) : win8_key(win8, i, a.total_bits);
                 sv[j] = (uint32_t)(P0 + q0 + i);
                 ++j;
             }
@@ -576,7 +600,9 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 vout[o + e] = sv[e];
                 nd_out[o + e] = (uint8_t)dg_of(k, d0);
             }
-        } else {
+            continue;
+        }
+        {
             // one ballot per row of 64 positions
             const uint32_t wbase = wave * (kSI * 64);
             uint64_t key[kSI];

@@ -315,8 +315,8 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,k", [(4, 31), (7, 25)])
-def test_gpu_key_range_repeated_calls(world, k):
+@pytest.mark.parametrize("world,k,canonical", [(4, 31, False), (7, 25, False), (4, 31, True), (3, 63, True)])
+def test_gpu_key_range_repeated_calls(world, k, canonical):
     """Repeated gk_shard_sort_range calls on one engine over hundreds of select tiles, ranges in
     growing then shrinking size order (buffers grown, then reused): each call keeps exactly its
     histogram's k-mers, repeats its own first result, and the ranks concatenate to gk_sort."""
@@ -329,13 +329,13 @@ def test_gpu_key_range_repeated_calls(world, k):
     e.set_sequence(sba, seg)
     hist = None
     for r in range(world):
-        h, _ = e.shard_histogram(bounds[r], bounds[r + 1], k)
+        h, _ = e.shard_histogram(bounds[r], bounds[r + 1], k, canonical=canonical)
         hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
     db = D.split_buckets(hist, world)
     order = sorted(range(world), key=lambda r: int(hist[db[r]:db[r + 1]].sum()))  # growing ranges
     got = {}
     for r in order + order[::-1]:
-        n = e.shard_sort_range(k, db[r], db[r + 1])
+        n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
         assert n == int(hist[db[r]:db[r + 1]].sum())
         starts = e.copy_starts()
         if r in got:
@@ -344,7 +344,7 @@ def test_gpu_key_range_repeated_calls(world, k):
     ref = _native.Engine(0)
     ref.set_sequence(sba, seg)
     ref.enumerate(k)
-    ref.sort(k)
+    ref.sort(k, canonical=canonical)
     np.testing.assert_array_equal(np.concatenate([got[r] for r in range(world)]), ref.copy_starts())
 
 

@@ -49,7 +49,13 @@ void timer_begin(gk_ctx *c, const char *name, int *slot) {
     if (!c->profile) return;
     Timer t;
     t.name = name;
-    if (hipEventCreate(&t.start) != hipSuccess || hipEventCreate(&t.stop) != hipSuccess) return;
+    while (c->ev_pool.size() < c->ev_used + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->ev_pool.push_back(e);
+    }
+    t.start = c->ev_pool[c->ev_used++];
+    t.stop = c->ev_pool[c->ev_used++];
     hipEventRecord(t.start, c->stream);
     c->timers.push_back(t);
     *slot = (int)c->timers.size() - 1;
@@ -249,10 +255,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
         if (b) hipFree(b);
     for (auto &e : c->scratch)
         if (e.second.first) hipFree(e.second.first);
-    for (auto &t : c->timers) {
-        hipEventDestroy(t.start);
-        hipEventDestroy(t.stop);
-    }
+    for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -771,12 +774,16 @@ extern "C" int gk_device_views(gk_ctx *c, void **starts, void **keys, uint64_t *
 extern "C" int gk_profile_enable(gk_ctx *c, int on) {
     if (!c) return GK_E_ARG;
     hipStreamSynchronize(c->stream);
-    for (auto &t : c->timers) {
-        hipEventDestroy(t.start);
-        hipEventDestroy(t.stop);
-    }
     c->timers.clear();
+    c->ev_used = 0;
     c->profile = on != 0;
+    // pre-create the events of a few hundred timed stages (a step uses tens): a timed step then
+    // only records events
+    while (c->profile && c->ev_pool.size() < 16384) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) break;
+        c->ev_pool.push_back(e);
+    }
     return GK_OK;
 }
 

@@ -141,6 +141,8 @@ struct gk_ctx {
     // profiling
     bool profile = false;
     std::vector<gkm::Timer> timers;
+    std::vector<hipEvent_t> ev_pool;  // timing events, created when profiling is switched on and
+    size_t ev_used = 0;               // reused (no hipEventCreate inside a timed step)
 };
 
 // ---------------------------------------------------------------------------------------------

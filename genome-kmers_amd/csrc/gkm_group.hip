@@ -244,9 +244,9 @@ hipError_t scan_flags_inclusive(gk_ctx *c, const uint8_t *flags, uint64_t n, uin
     return hipGetLastError();
 }
 
-static hipError_t scan_u32_exclusive(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {
+// the exclusive scan's launches; its total is left in c->scalars[0] (n > 0)
+static hipError_t scan_u32_exclusive_launch(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out) {
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
-    if (n == 0) { *total = 0; return hipSuccess; }
     hipError_t e = ensure_tile_sums(c, ntiles);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(u32_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
@@ -254,7 +254,12 @@ static hipError_t scan_u32_exclusive(gk_ctx *c, const uint32_t *in, uint64_t n, 
     scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
     hipLaunchKernelGGL(u32_scan_apply_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, in, n,
                        c->tile_sums, out);
-    e = hipGetLastError();
+    return hipGetLastError();
+}
+
+static hipError_t scan_u32_exclusive(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {
+    if (n == 0) { *total = 0; return hipSuccess; }
+    hipError_t e = scan_u32_exclusive_launch(c, in, n, out);
     if (e != hipSuccess) return e;
     return read_total(c, total);
 }
@@ -694,5 +699,24 @@ hipError_t unique_counts_device(gk_ctx *c) {
 namespace gkm {
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {
     return scan_u32_exclusive(c, in, n, out, total);
+}
+
+// two exclusive scans of n entries with one host round trip for both totals (scalars[62..63])
+hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
+                                   uint32_t *out2, uint64_t n, uint64_t *total1, uint64_t *total2) {
+    if (n == 0) {
+        *total1 = *total2 = 0;
+        return hipSuccess;
+    }
+    hipError_t e = scan_u32_exclusive_launch(c, in1, n, out1);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->scalars + 63, c->scalars, 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = scan_u32_exclusive_launch(c, in2, n, out2);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->scalars + 62, c->scalars, 8, hipMemcpyDeviceToDevice, c->stream);
+    uint64_t t[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(t, c->scalars + 62, 16, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    *total1 = t[1];
+    *total2 = t[0];
+    return e;
 }
 }  // namespace gkm

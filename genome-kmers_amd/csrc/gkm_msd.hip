@@ -1525,6 +1525,8 @@ __global__ __launch_bounds__(256) void tie_encode_kernel(const uint8_t *__restri
 static int grid_n(uint64_t n) { return (int)std::max<uint64_t>((n + 255) / 256, 1); }
 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
+hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
+                                   uint32_t *out2, uint64_t n, uint64_t *total1, uint64_t *total2);
 hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);
 
 // grow a device array to hold `need` entries, keeping the first `keep` entries
@@ -1988,8 +1990,7 @@ struct MsdDriver {
                            nullptr, nullptr, nullptr);
         GK_TRY_HIP(c, hipGetLastError());
         uint64_t ng = 0, ng2 = 0;
-        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cf, ttiles, of, &ng));
-        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cl, ttiles, ol, &ng2));
+        GK_TRY_HIP(c, scan_u32_exclusive_pair(c, cf, of, cl, ol, ttiles, &ng, &ng2));
         GK_TRY_HIP(c, scratch(c, "tie_start", ng + 64, &g_start));
         GK_TRY_HIP(c, scratch(c, "tie_len", ng2 + 64, &g_len));
         hipLaunchKernelGGL(tie_bounds_kernel<true>, dim3(ttiles), dim3(256), 0, c->stream, heads, n, nullptr, nullptr,
@@ -2057,8 +2058,7 @@ struct MsdDriver {
                                (uint32_t)kPTile, ntl, nch);
             GK_TRY_HIP(c, hipGetLastError());
             uint64_t T = 0, C = 0;
-            GK_TRY_HIP(c, scan_u32_exclusive_pub(c, ntl, nbig, tfirst, &T));
-            GK_TRY_HIP(c, scan_u32_exclusive_pub(c, nch, nbig, cfirst, &C));
+            GK_TRY_HIP(c, scan_u32_exclusive_pair(c, ntl, tfirst, nch, cfirst, nbig, &T, &C));
             uint32_t *t_start, *t_count;
             GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
             GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));

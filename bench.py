@@ -57,64 +57,6 @@ def parse():
     return ap.parse_args()
 
 
-def make_genome(L: int, seed: int) -> np.ndarray:
-    """Uniform i.i.d. random bases over the reference's alphabet order (profiling.py:12-24)."""
-    lut = np.frombuffer(b"ATGC", dtype=np.uint8)
-    out = np.empty(L, dtype=np.uint8)
-    rng = np.random.default_rng(seed)
-    chunk = 1 << 28
-    for at in range(0, L, chunk):
-        m = min(chunk, L - at)
-        out[at:at + m] = lut[rng.integers(0, 4, m, dtype=np.uint8)]
-    return out
-
-
-# GRCh38 primary assembly chromosome lengths, chr1..chr22, chrX, chrY (total 3,088,269,832 bp)
-GRCH38_LENGTHS = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636,
-                  138394717, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,
-                  83257441, 80373285, 58617616, 64444167, 46709983, 50818468, 156040895, 57227415]
-
-
-def make_grch38_surrogate(seed: int, lengths=GRCH38_LENGTHS):
-    """C4/C5 input without a FASTA: GRCh38's 24 contig lengths joined by '$',
-    uniform random ACGT, ~5 % N (runs at both contig ends and the centre), and repeat families with
-    realistic divergence so that k-mer groups of every size exist:
-      Alu-like  300 bp x 400,000 copies, 12 % substitutions;  L1-like 6 kb x 15,000 copies, 8 %;
-      segmental duplications 20 kb x 300 exact copies;  (CA)n microsatellites 40 bp x 50,000."""
-    rng = np.random.default_rng(seed)
-    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
-    L = sum(lengths) + len(lengths) - 1
-    sba = np.empty(L, dtype=np.uint8)
-    chunk = 1 << 28
-    for at in range(0, L, chunk):
-        m = min(chunk, L - at)
-        sba[at:at + m] = lut[rng.integers(0, 4, m, dtype=np.uint8)]
-
-    def plant(unit, copies, div):
-        at = rng.integers(0, L - len(unit), copies)
-        for a in range(0, copies, 20_000):
-            b = min(copies, a + 20_000)
-            rows = np.broadcast_to(unit, (b - a, len(unit))).copy()
-            mut = rng.random(rows.shape) < div
-            rows[mut] = lut[rng.integers(0, 4, int(mut.sum()), dtype=np.uint8)]
-            sba[at[a:b, None] + np.arange(len(unit))[None, :]] = rows
-
-    plant(lut[rng.integers(0, 4, 300)], 400_000, 0.12)
-    plant(lut[rng.integers(0, 4, 6000)], 15_000, 0.08)
-    for _ in range(300):
-        src, dst = rng.integers(0, L - 20_000, 2)
-        sba[dst:dst + 20_000] = sba[src:src + 20_000]
-    plant(np.frombuffer(b"CA" * 20, dtype=np.uint8), 50_000, 0.0)
-    starts = np.concatenate([[0], np.cumsum(np.asarray(lengths[:-1], dtype=np.int64) + 1)])
-    for s0, n in zip(starts, lengths):
-        e, c = int(n * 0.015), int(n * 0.02)
-        sba[s0:s0 + e] = ord("N")
-        sba[s0 + n - e:s0 + n] = ord("N")
-        sba[s0 + n // 2 - c // 2:s0 + n // 2 + c // 2] = ord("N")
-    sba[starts[1:] - 1] = ord("$")
-    return sba, starts.astype(np.uint32)
-
-
 def cpu_baseline(sba: np.ndarray, k: int, sample: int) -> dict:
     """Reference algorithm (Kmers.sort: numba quicksort + byte comparator with validation,
     kmers.py:1624-1731) restated in C (oracle/gk_oracle.c), 1 thread, on the first `sample` k-mers."""
@@ -166,7 +108,7 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
 
-    from genome_kmers import _native
+    from genome_kmers import _native, synthetic
 
     cfg = args.config
     k = args.k or (63 if cfg == "c5" else 31)
@@ -174,11 +116,11 @@ def main():
     seed = args.seed if args.seed is not None else (42 if cfg == "c3" else 2)
     if cfg == "c3":
         L = args.genome_len or 3_100_000_000
-        sba, seg = make_genome(L, seed), np.zeros(1, dtype=np.uint32)
+        sba, seg = synthetic.c3_genome(L, seed)
         workload = f"C3: {L:,}-base synthetic single-contig genome, k={k} (min=max={k})"
         data = f"synthetic: uniform random ACGT, numpy PCG64 seed {seed}"
     else:
-        sba, seg = make_grch38_surrogate(seed)
+        sba, seg = synthetic.grch38_surrogate(seed)
         L = len(sba)
         workload = (f"{cfg.upper()}: GRCh38-shaped surrogate (24 contigs, {L:,} sba bytes), k={k}"
                     + (", canonical" if canonical else ""))

@@ -9,6 +9,7 @@
 //   5. hist[min(size, max_bin)] += 1, total += size for min <= size <= max  (kmers.py:454-520)
 // A generator "yield" is one of the first yield_first_n members of a qualifying group.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gkm_internal.h"
 
@@ -100,14 +101,14 @@ __global__ __launch_bounds__(1024) void scan_tiles_kernel(uint32_t *__restrict__
 // Many tile sums (a 3.1e9-element selection has 757 k): the single-block scan above walks them in
 // 740 sequential steps (~0.7 ms); instead chunks of 16384 are scanned in parallel, the chunk
 // totals by one block, and the chunk offsets added back.
-constexpr int kScanChunk = 16384;
+constexpr int kScanChunk = 16384;  // multiple of 1024 (GKM_TEST_SCAN_CHUNK overrides: tests only)
 
-__global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__ sums, uint64_t ntiles,
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__ sums, uint64_t ntiles, uint32_t chunk,
                                                           uint32_t *__restrict__ chunk_tot) {
     __shared__ uint32_t s_tmp[16];
-    const uint64_t b0 = (uint64_t)blockIdx.x * kScanChunk;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
     uint32_t carry = 0;
-    for (int j = 0; j < kScanChunk; j += 1024) {
+    for (uint32_t j = 0; j < chunk; j += 1024) {
         const uint64_t i = b0 + j + threadIdx.x;
         const uint32_t v = i < ntiles ? sums[i] : 0;
         uint32_t tot;
@@ -118,25 +119,37 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__
     if (threadIdx.x == 0) chunk_tot[blockIdx.x] = carry;
 }
 
-__global__ __launch_bounds__(256) void chunk_add_kernel(uint32_t *__restrict__ sums, uint64_t ntiles,
+__global__ __launch_bounds__(256) void chunk_add_kernel(uint32_t *__restrict__ sums, uint64_t ntiles, uint32_t chunk,
                                                         const uint32_t *__restrict__ chunk_off) {
     const uint32_t add = chunk_off[blockIdx.x];
-    const uint64_t b0 = (uint64_t)blockIdx.x * kScanChunk;
-    for (uint32_t j = threadIdx.x; j < (uint32_t)kScanChunk; j += 256)
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    for (uint32_t j = threadIdx.x; j < chunk; j += 256)
         if (b0 + j < ntiles) sums[b0 + j] += add;
+}
+
+// scan chunk: kScanChunk, or (test-only) a smaller multiple of 1024 so that the parity tests reach
+// the chunked branch, which otherwise runs only above 65536 tiles (about 268 M elements)
+static uint32_t scan_chunk() {
+    if (const char *e = std::getenv("GKM_TEST_SCAN_CHUNK")) {
+        const int v = std::atoi(e);
+        if (v >= 1024) return (uint32_t)(v / 1024 * 1024);
+    }
+    return kScanChunk;
 }
 
 // exclusive scan of ntiles tile sums in place, grand total -> *total (device)
 static void scan_tile_sums(gk_ctx *c, uint32_t *sums, uint64_t ntiles, uint64_t *total) {
-    if (ntiles <= (uint64_t)4 * kScanChunk) {
+    const uint32_t chunk = scan_chunk();
+    const bool test = chunk != (uint32_t)kScanChunk;
+    if (test ? ntiles <= chunk : ntiles <= (uint64_t)4 * kScanChunk) {
         hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, sums, ntiles, total);
         return;
     }
-    const uint64_t nch = (ntiles + kScanChunk - 1) / kScanChunk;
-    uint32_t *chunk = sums + ntiles + 16;  // ensure_tile_sums leaves room for the chunk totals
-    hipLaunchKernelGGL(chunk_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, c->stream, sums, ntiles, chunk);
-    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, chunk, nch, total);
-    hipLaunchKernelGGL(chunk_add_kernel, dim3((unsigned)nch), dim3(256), 0, c->stream, sums, ntiles, chunk);
+    const uint64_t nch = (ntiles + chunk - 1) / chunk;
+    uint32_t *chunk_tot = sums + ntiles + 16;  // ensure_tile_sums leaves room for the chunk totals
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, c->stream, sums, ntiles, chunk, chunk_tot);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, c->stream, chunk_tot, nch, total);
+    hipLaunchKernelGGL(chunk_add_kernel, dim3((unsigned)nch), dim3(256), 0, c->stream, sums, ntiles, chunk, chunk_tot);
 }
 
 // Thread t loads the 16 flags of positions 16t..16t+15 (one 16-B load), writes its selected
@@ -207,7 +220,7 @@ __global__ __launch_bounds__(kScanThreads) void u32_scan_apply_kernel(const uint
 static hipError_t ensure_tile_sums(gk_ctx *c, uint64_t ntiles) {
     // + the chunk totals of scan_tile_sums
     return ensure(reinterpret_cast<void **>(&c->tile_sums), &c->tile_sums_cap,
-                  4 * (ntiles + 16 + ntiles / kScanChunk + 16));
+                  4 * (ntiles + 16 + ntiles / 1024 + 16));
 }
 
 static hipError_t read_total(gk_ctx *c, uint64_t *count) {

@@ -31,7 +31,7 @@ constexpr int kGR = 8;                  // global digit bits
 constexpr int kGRadix = 1 << kGR;
 constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
 constexpr int kPTile = kPT * kPI;
-constexpr int kChunkTiles = 256;        // tiles per scan chunk
+constexpr int kChunkTiles = 256;        // tiles per scan chunk (GKM_TEST_CHUNK_TILES overrides: tests only)
 constexpr int kBT = 512, kBI = 8, kBR = 8;    // block-local: 512 threads x 8 keys, 8-bit digit
 constexpr int kBlockMax = kBT * kBI;    // 4096
 // local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
@@ -884,7 +884,7 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restr
                                                          const uint32_t *__restrict__ s_len,
                                                          const uint32_t *__restrict__ s_tfirst,
                                                          const uint32_t *__restrict__ s_cfirst, uint32_t nseg,
-                                                         uint32_t tile, uint32_t T, uint32_t C,
+                                                         uint32_t tile, uint32_t T, uint32_t C, uint32_t ctiles,
                                                          uint32_t *__restrict__ t_start,
                                                          uint32_t *__restrict__ t_count, uint32_t *__restrict__ c_first,
                                                          uint32_t *__restrict__ c_ntiles) {
@@ -898,19 +898,19 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const uint32_t *__restr
     if (j < C) {
         const uint32_t s = owner_of(s_cfirst, nseg, j);
         const uint32_t r = j - s_cfirst[s], nt = (s_len[s] + tile - 1) / tile;
-        c_first[j] = s_tfirst[s] + r * kChunkTiles;
-        c_ntiles[j] = std::min<uint32_t>(kChunkTiles, nt - r * kChunkTiles);
+        c_first[j] = s_tfirst[s] + r * ctiles;
+        c_ntiles[j] = std::min<uint32_t>(ctiles, nt - r * ctiles);
     }
 }
 
 __global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg,
-                                                         uint32_t tile, uint32_t *__restrict__ ntiles,
+                                                         uint32_t tile, uint32_t ctiles, uint32_t *__restrict__ ntiles,
                                                          uint32_t *__restrict__ nchunks) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
     const uint32_t nt = (s_len[s] + tile - 1) / tile;
     ntiles[s] = nt;
-    nchunks[s] = (nt + kChunkTiles - 1) / kChunkTiles;
+    nchunks[s] = (nt + ctiles - 1) / ctiles;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1623,6 +1623,7 @@ struct MsdDriver {
     uint32_t nbig = 0;
     int cur_big = 0;
     int phase = 0;  // key word being sorted (multi-word keys)
+    uint32_t ctiles = kChunkTiles;  // tiles per column-scan chunk
     const uint64_t *pk_code = nullptr;  // packed sequence for the L0 passes (ACGT, 2-bit keys)
     const uint32_t *pk_dol = nullptr;
 
@@ -1630,6 +1631,9 @@ struct MsdDriver {
         cus = cu_count(c);
         pgrid = cus * 4;  // 4 workgroups per CU, one resident at a time (LDS); measured faster than 1
         set_widths(std::getenv("GKM_LEVEL_BITS"));
+        // test-only: small scan chunks so that parity tests reach the multi-chunk branches of the
+        // column scan and tile tables (otherwise only buckets > 2.9 M keys have more than one chunk)
+        if (const char *e = std::getenv("GKM_TEST_CHUNK_TILES")) ctiles = (uint32_t)std::max(1, std::atoi(e));
     }
 
     // level digit widths "w0,w1,w2,..." (the last one repeats).  Default 7,8,8,...: for 2-bit
@@ -1768,7 +1772,7 @@ struct MsdDriver {
     int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count) {
         const uint64_t span = hi > lo ? hi - lo : 0;
         const uint64_t nt0 = std::max<uint64_t>((span + kPTile - 1) / kPTile, 1);
-        const uint64_t nc0 = (nt0 + kChunkTiles - 1) / kChunkTiles;
+        const uint64_t nc0 = (nt0 + ctiles - 1) / ctiles;
         l0_tiles = nt0;
         int rc = tables(nt0, nc0, 1);
         if (rc != GK_OK) return rc;
@@ -1777,8 +1781,8 @@ struct MsdDriver {
         {
             std::vector<uint32_t> cf(nc0), cn(nc0);
             for (uint64_t j = 0; j < nc0; ++j) {
-                cf[j] = (uint32_t)(j * kChunkTiles);
-                cn[j] = (uint32_t)std::min<uint64_t>(kChunkTiles, nt0 - j * kChunkTiles);
+                cf[j] = (uint32_t)(j * ctiles);
+                cn[j] = (uint32_t)std::min<uint64_t>(ctiles, nt0 - j * ctiles);
             }
             const uint32_t misc[3] = {0, (uint32_t)nc0, 0};  // s_cfirst, s_nchunks, s_start
             GK_TRY_HIP(c, hipMemcpyAsync(c_first, cf.data(), 4 * nc0, hipMemcpyHostToDevice, c->stream));
@@ -1939,9 +1943,9 @@ struct MsdDriver {
             if (tot > 0) {
                 const uint64_t nt = ts.size() - tile0;
                 scf.push_back((uint32_t)cf.size());
-                for (uint64_t t = 0; t < nt; t += kChunkTiles) {
+                for (uint64_t t = 0; t < nt; t += ctiles) {
                     cf.push_back((uint32_t)(tile0 + t));
-                    cn.push_back((uint32_t)std::min<uint64_t>(kChunkTiles, nt - t));
+                    cn.push_back((uint32_t)std::min<uint64_t>(ctiles, nt - t));
                 }
                 snc.push_back((uint32_t)(cf.size() - scf.back()));
                 sst.push_back((uint32_t)out_base);
@@ -2055,7 +2059,7 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
             GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
             hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big], nbig,
-                               (uint32_t)kPTile, ntl, nch);
+                               (uint32_t)kPTile, ctiles, ntl, nch);
             GK_TRY_HIP(c, hipGetLastError());
             uint64_t T = 0, C = 0;
             GK_TRY_HIP(c, scan_u32_exclusive_pair(c, ntl, tfirst, nch, cfirst, nbig, &T, &C));
@@ -2066,7 +2070,7 @@ struct MsdDriver {
             if (rc != GK_OK) return rc;
             hipLaunchKernelGGL(tile_table_kernel, dim3((unsigned)std::max<uint64_t>((std::max(T, C) + 255) / 256, 1)), dim3(256), 0,
                                c->stream, big_start[cur_big], big_len[cur_big], tfirst, cfirst, nbig,
-                               (uint32_t)kPTile, (uint32_t)T, (uint32_t)C, t_start, t_count, c_first, c_ntiles);
+                               (uint32_t)kPTile, (uint32_t)T, (uint32_t)C, ctiles, t_start, t_count, c_first, c_ntiles);
             rc = level_pass(level, hi, t_start, t_count, T, C, cfirst, nch, big_start[cur_big], nbig, c->keys[in],
                             c->vals[in], out);
             if (rc != GK_OK) return rc;

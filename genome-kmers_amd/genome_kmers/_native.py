@@ -425,6 +425,12 @@ class Engine:
                                              ctypes.byref(w)))
         return s.value, k.value, n.value, w.value
 
+    def device_starts(self):
+        """(device pointer of the current start indices, n) -- no key materialisation."""
+        s, n = _P(), ctypes.c_uint64()
+        self._check(self.lib.gk_device_views(self.ctx, ctypes.byref(s), None, ctypes.byref(n), None))
+        return s.value, n.value
+
     def stream_handle(self) -> int:
         s = _P()
         self._check(self.lib.gk_stream(self.ctx, ctypes.byref(s)))

@@ -30,14 +30,13 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
 
-    import bench
-    from genome_kmers import _native
+    from genome_kmers import _native, synthetic
     from genome_kmers import distributed as D
 
     if args.config == "c3":
-        sba, seg = bench.make_genome(args.genome_len, 42), np.zeros(1, dtype=np.uint32)
+        sba, seg = synthetic.c3_genome(args.genome_len, 42)
     else:
-        sba, seg = bench.make_grch38_surrogate(2)
+        sba, seg = synthetic.grch38_surrogate(2)
     k = args.k or (63 if args.config == "c5" else 31)
     canonical = args.config == "c5"
     e = _native.Engine(0)

@@ -249,7 +249,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
-                    c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->cumk, c->tile_sums, c->scalars,
+                    c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
                     c->dhist, c->mask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
         if (b) hipFree(b);
@@ -436,7 +436,9 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         if (rc != GK_OK) return rc;
         c->spec = ks;
         c->keys_valid = true;
-        c->keys_stale = true;  // the MSD sort keeps the start order, not the keys
+        // a one-word MSD sort leaves the sorted keys in keys[0]; the split sort (2-bit class-A keys
+        // under a 4-bit key spec) and multi-word phases leave them to ensure_keys
+        c->keys_stale = split || !c->msd_keys_final;
         c->keys_are_ranks = false;
         return GK_OK;
     }
@@ -919,7 +921,7 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     if (rc != GK_OK) return rc;
     c->spec = ks;
     c->keys_valid = true;
-    c->keys_stale = c->n > 0;  // the MSD sort keeps the start order, not the keys
+    c->keys_stale = c->n > 0 && (range_split(c, ks) || !c->msd_keys_final);  // see sort_direct
     c->keys_are_ranks = false;
     c->sorted = true;
     c->sort_len = k;
@@ -954,7 +956,7 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     }
     c->spec = ks;
     c->keys_valid = true;
-    c->keys_stale = n > 0;  // the MSD sort keeps the start order, not the keys
+    c->keys_stale = n > 0 && !c->msd_keys_final;  // see sort_direct
     c->keys_are_ranks = false;
     c->sorted = true;
     c->sort_len = k;

@@ -179,6 +179,49 @@ __global__ __launch_bounds__(kScanThreads) void flag_select_kernel(const uint8_t
     for (uint32_t j = threadIdx.x; j < tot; j += kScanThreads) dst[j] = s_idx[sel_swz(j)];
 }
 
+// Group starts and multiplicities in one pass (the unique/count output): entry j of a tile also
+// gets its count s_idx[j + 1] - s_idx[j]; the tile's last entry needs the next tile's first start
+// and is completed by tile_last_count_kernel once every tile has stored its starts.
+__global__ __launch_bounds__(kScanThreads) void flag_select_counts_kernel(const uint8_t *__restrict__ f, uint64_t n,
+                                                                          const uint32_t *__restrict__ tile_off,
+                                                                          uint32_t *__restrict__ out,
+                                                                          uint32_t *__restrict__ out_cnt) {
+    __shared__ uint32_t s_tmp[kScanThreads / 64];
+    __shared__ uint32_t s_idx[kScanTile + 1];
+    const uint64_t at = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16;
+    uint8_t v[16];
+    load16_flags(f, n, at, v);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cnt += v[k] != 0;
+    uint32_t tot;
+    uint32_t o = block_excl_scan<kScanThreads>(cnt, s_tmp, &tot);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (v[k]) s_idx[sel_swz(o++)] = (uint32_t)(at + k);
+    __syncthreads();
+    const uint64_t base = tile_off[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < tot; j += kScanThreads) {
+        const uint32_t g0 = s_idx[sel_swz(j)];
+        out[base + j] = g0;
+        if (j + 1 < tot) out_cnt[base + j] = s_idx[sel_swz(j + 1)] - g0;
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_last_count_kernel(const uint32_t *__restrict__ tile_off, uint64_t ntiles,
+                                                              const uint64_t *__restrict__ total,
+                                                              const uint32_t *__restrict__ gstart, uint64_t n,
+                                                              uint32_t *__restrict__ out_cnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint64_t G = *total;
+    const uint64_t end = t + 1 < ntiles ? tile_off[t + 1] : G;
+    if (end == tile_off[t]) return;
+    const uint64_t g = end - 1;
+    const uint64_t next = end < G ? gstart[end] : n;
+    out_cnt[g] = (uint32_t)(next - gstart[g]);
+}
+
 __global__ __launch_bounds__(kScanThreads) void flag_scan_incl_kernel(const uint8_t *__restrict__ f, uint64_t n,
                                                                       const uint32_t *__restrict__ tile_off,
                                                                       uint32_t *__restrict__ out) {
@@ -239,6 +282,25 @@ hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *o
     scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
     hipLaunchKernelGGL(flag_select_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
                        c->tile_sums, out_idx);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return read_total(c, count);
+}
+
+// select_flags + the multiplicity of every selected entry (distance to the next one, or to n)
+hipError_t select_flags_counts(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint32_t *out_cnt,
+                               uint64_t *count) {
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    if (n == 0) { *count = 0; return hipSuccess; }
+    hipError_t e = ensure_tile_sums(c, ntiles);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(flag_count_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums);
+    scan_tile_sums(c, c->tile_sums, ntiles, c->scalars);
+    hipLaunchKernelGGL(flag_select_counts_kernel, dim3((unsigned)ntiles), dim3(kScanThreads), 0, c->stream, flags, n,
+                       c->tile_sums, out_idx, out_cnt);
+    hipLaunchKernelGGL(tile_last_count_kernel, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, c->stream,
+                       c->tile_sums, ntiles, c->scalars, out_idx, n, out_cnt);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     return read_total(c, count);
@@ -488,6 +550,7 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
                        uint64_t *count, uint64_t *G, int32_t *err_code, uint64_t *err_idx) {
     if (err_code) *err_code = 0;
     if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
+    c->unique_valid = false;  // idx_b (the unique output's group starts) is rewritten below
     if (int rc = materialize_starts(c)) return rc;
     const uint64_t n = c->n;
     const uint32_t *starts = c->vals[c->cur];
@@ -666,14 +729,36 @@ extern "C" int gk_group_members(gk_ctx *c, int is_sorted, int64_t kmer_len, cons
     return GK_OK;
 }
 
+// The unique/count output (sorted k-mers -> distinct k-mers + multiplicities), resident in HBM:
+// group starts in idx_b (u32, index of each distinct k-mer's first sorted element) and counts in
+// ucount (u32); with the sorted keys (keys[cur]) and starts (vals[cur]) this is the full product.
 extern "C" int gk_unique_counts(gk_ctx *c, uint64_t *n_unique) {
     if (!c) return GK_E_ARG;
     if (!c->sorted || !c->keys_valid) return fail(c, GK_E_STATE, "unique counts need a sorted k-mer set");
-    const uint32_t *cidx;
-    uint64_t count, G;
     const int64_t kl = c->sort_len == 0 ? -1 : (int64_t)c->sort_len;
-    int rc = group_front(c, 1, kl, nullptr, &cidx, &count, &G, nullptr, nullptr);
-    if (rc != GK_OK) return rc;
+    uint64_t G = 0;
+    if (c->heads_valid && !c->keys_are_ranks && c->spec.lenbits == 0 && kl == c->spec.symbols) {
+        // heads written by the MSD sort: group starts and counts in one selection pass
+        if (int rc = materialize_starts(c)) return rc;
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_b), &c->idx_b_cap, 4 * (c->n + 64)));
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ucount), &c->ucount_cap, 4 * (c->n + 64)));
+        c->unique_valid = false;
+        int slot;
+        timer_begin(c, "unique_counts", &slot);
+        GK_TRY_HIP(c, select_flags_counts(c, c->heads, c->n, c->idx_b, c->ucount, &G));
+        timer_end(c, slot);
+    } else {
+        const uint32_t *cidx;
+        uint64_t count;
+        int rc = group_front(c, 1, kl, nullptr, &cidx, &count, &G, nullptr, nullptr);
+        if (rc != GK_OK) return rc;
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ucount), &c->ucount_cap, 4 * (G + 64)));
+        if (G) {
+            hipLaunchKernelGGL(unique_counts_kernel, dim3(grid_for(G)), dim3(256), 0, c->stream, c->idx_b, G, c->n,
+                               c->ucount);
+            GK_TRY_HIP(c, hipGetLastError());
+        }
+    }
     c->n_unique = G;
     c->unique_valid = true;
     if (n_unique) *n_unique = G;
@@ -685,10 +770,7 @@ extern "C" int gk_copy_unique(gk_ctx *c, uint64_t *group_start, uint32_t *count,
     if (!c->unique_valid) return fail(c, GK_E_STATE, "call gk_unique_counts first");
     if (n != c->n_unique) return fail(c, GK_E_ARG, "n differs from the unique k-mer count");
     if (n == 0) return GK_OK;
-    uint32_t *cnt = c->idx_a;  // idx_a is free after an unfiltered group_front
-    hipLaunchKernelGGL(unique_counts_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, c->idx_b, n, c->n, cnt);
-    GK_TRY_HIP(c, hipGetLastError());
-    if (count) GK_TRY_HIP(c, hipMemcpyAsync(count, cnt, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (count) GK_TRY_HIP(c, hipMemcpyAsync(count, c->ucount, 4 * n, hipMemcpyDeviceToHost, c->stream));
     if (group_start) {
         std::vector<uint32_t> tmp(n);
         GK_TRY_HIP(c, hipMemcpyAsync(tmp.data(), c->idx_b, 4 * n, hipMemcpyDeviceToHost, c->stream));
@@ -699,15 +781,14 @@ extern "C" int gk_copy_unique(gk_ctx *c, uint64_t *group_start, uint32_t *count,
     return GK_OK;
 }
 
-namespace gkm {
-// device-side unique counts for the bench step (no host copy): counts into idx_a
-hipError_t unique_counts_device(gk_ctx *c) {
-    if (c->n_unique == 0) return hipSuccess;
-    hipLaunchKernelGGL(unique_counts_kernel, dim3(grid_for(c->n_unique)), dim3(256), 0, c->stream, c->idx_b,
-                       c->n_unique, c->n, c->idx_a);
-    return hipGetLastError();
+extern "C" int gk_device_unique(gk_ctx *c, void **group_start, void **count, uint64_t *n_unique) {
+    if (!c) return GK_E_ARG;
+    if (!c->unique_valid) return fail(c, GK_E_STATE, "call gk_unique_counts first");
+    if (group_start) *group_start = c->idx_b;
+    if (count) *count = c->ucount;
+    if (n_unique) *n_unique = c->n_unique;
+    return GK_OK;
 }
-}  // namespace gkm
 
 namespace gkm {
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total) {

@@ -86,6 +86,7 @@ struct gk_ctx {
     uint32_t sort_len = 0;     // max_kmer_len of the last sort (0 = None)
     bool canonical = false;    // the last sort ordered canonical k-mers (GK_SORT_CANONICAL)
     bool keys_valid = false;   // keys[cur] encode the k-mers of vals[cur] (sort order)
+    bool msd_keys_final = false;  // the last MSD sort wrote its (one-word) keys in sorted order
     bool keys_stale = false;   // ... once re-encoded from vals[cur]: the MSD sort does not keep them (ensure_keys)
     bool keys_are_ranks = false;
     gkm::KeySpec spec{};
@@ -109,6 +110,8 @@ struct gk_ctx {
     uint64_t flags_cap = 0;
     uint32_t *idx_a = nullptr, *idx_b = nullptr;
     uint64_t idx_cap = 0, idx_b_cap = 0;
+    uint32_t *ucount = nullptr;  // multiplicities of the unique output (gk_unique_counts)
+    uint64_t ucount_cap = 0;
     uint64_t *cumk = nullptr;       // enumerate: cumulative k-mers per segment
     uint64_t cumk_cap = 0;
     std::vector<uint32_t> hseg;     // host copy of the segment table
@@ -207,8 +210,9 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready);
 
 // group / scan
 hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);
+hipError_t select_flags_counts(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint32_t *out_cnt,
+                               uint64_t *count);
 hipError_t scan_flags_inclusive(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out);
-hipError_t unique_counts_device(gk_ctx *c);
 
 // write the lazily enumerated starts into vals[cur] if a reader needs them (gkm_capi.hip)
 int materialize_starts(gk_ctx *c);

@@ -966,7 +966,7 @@ template <int T, int I, int R>
 __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys) {
     using SM = PartSmem<T, I, R>;
     constexpr int TILE = SM::kTile;
     constexpr int RADIX = SM::kRadix;
@@ -1087,7 +1087,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = min((uint32_t)(i * T + tid), len - 1);
-            if (relist) k0[st + p] = s_k[p];  // keys only for a bucket with re-listed elements
+            if (relist || wkeys) k0[st + p] = s_k[p];  // keys: final-key sorts, or re-listed elements
             v0[st + p] = s_v[p];
             heads[st + p] = s_hd[p] & 1;
         }
@@ -1106,10 +1106,11 @@ template <int I, int MINW = 1>
 __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
-    __shared__ uint64_t s_mask[256];
+    // digit masks (256), and the staged starts (CAP + 1 uint32) of the write-back
+    __shared__ uint64_t s_mask[(CAP + 2) / 2 > 256 ? (CAP + 2) / 2 : 256];
     __shared__ uint32_t s_cnt[257];  // digit counts, then exclusive starts (s_cnt[256] = total)
     const int lane = threadIdx.x;
     const uint64_t me_bit = 1ull << lane;
@@ -1245,29 +1246,34 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                 route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
             }
         }
-        // write-back straight from registers: the bucket spans a few cache lines, so the
-        // scattered stores of a wave combine in L2 (no LDS staging); the next bucket's loads are
-        // issued first so they fly during the stores
-        uint64_t wk[I];
-        uint32_t wv[I], wo[I];
-        uint8_t wh[I];
-        bool wl[I];
+        // write-back staged through LDS: every element goes to its final slot (the keys' slots are
+        // read above, and one wave's LDS operations complete in order), then the wave stores the
+        // bucket contiguously -- full-line stores of keys, starts and head flags.  The head flag is
+        // "key differs from its predecessor" read from the sorted keys (a bucket starts a group).
+        // The starts are staged in the digit-mask array, all zero at this point.  The next
+        // bucket's loads are issued first so they fly during the stores.
+        uint32_t *s_v = reinterpret_cast<uint32_t *>(s_mask);
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            wl[i] = i < live && valid[i];
-            wk[i] = key[i];
-            wv[i] = val[i];
-            wo[i] = out[i];
-            wh[i] = hd[i] & 1;  // 0 / 1: final (not) a group head; a re-listed one is redone later
+            const uint32_t o = (i < live && valid[i]) ? out[i] : (uint32_t)CAP;
+            s_k[o] = key[i];
+            s_v[o] = val[i];
         }
         local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket
+        const bool wk = relist || wkeys;  // keys: final-key sorts, or buckets with re-listed elements
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            if (!wl[i]) continue;
-            if (relist) k0[st + wo[i]] = wk[i];  // keys only for a bucket with re-listed elements
-            v0[st + wo[i]] = wv[i];
-            heads[st + wo[i]] = wh[i];
+            const uint32_t j = (uint32_t)(i * 64 + lane);
+            if (i < live && j < len) {
+                const uint64_t kj = s_k[j];
+                const uint64_t kp = s_k[j > 0 ? j - 1 : 0];
+                if (wk) k0[st + j] = kj;
+                v0[st + j] = s_v[j];
+                heads[st + j] = (j == 0 || kj != kp) ? 1 : 0;
+            }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;  // the digit masks of the next bucket
     }
 }
 
@@ -1275,8 +1281,8 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
 // bucket, stable rank-by-count over the full word (ties: load order = start order), write-back of
 // starts and head flags to buffer 0.
 __global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__ list, uint32_t count,
-                                                       const uint64_t *k0, uint32_t *v0, const uint64_t *k1,
-                                                       const uint32_t *v1, uint8_t *__restrict__ heads) {
+                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                       const uint32_t *v1, uint8_t *__restrict__ heads, int wkeys) {
     const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
     const bool live = idx < count;
     const uint2 e = live ? list[idx] : make_uint2(0, 1u << 8);
@@ -1310,6 +1316,7 @@ __global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__
     for (int j = 0; j < kTiny; ++j) {
         if ((uint32_t)j >= len) break;
         v0[st + out[j]] = val[j];
+        if (wkeys) k0[st + out[j]] = key[j];
         heads[st + out[j]] = hd[j] ? 1 : 0;
     }
 }
@@ -1477,13 +1484,15 @@ __global__ __launch_bounds__(256) void tie_encode_flat_kernel(const uint8_t *__r
 __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restrict__ dn_start,
                                                         const uint32_t *__restrict__ dn_len,
                                                         const uint8_t *__restrict__ dn_par, const uint32_t *__restrict__ v1,
-                                                        uint32_t *__restrict__ v0, uint8_t *__restrict__ heads) {
+                                                        uint32_t *__restrict__ v0, const uint64_t *__restrict__ k1,
+                                                        uint64_t *__restrict__ k0, uint8_t *__restrict__ heads) {
     const uint32_t s = blockIdx.x;
     const uint64_t st = dn_start[s];
     const uint32_t len = dn_len[s];
     const bool copy = dn_par[s];
-    for (uint32_t i = threadIdx.x; i < len; i += 256) {  // (keys are not kept: see kSmall)
+    for (uint32_t i = threadIdx.x; i < len; i += 256) {  // keys only in final-key sorts (k1 != null)
         if (copy) v0[st + i] = v1[st + i];
+        if (copy && k1) k0[st + i] = k1[st + i];
         heads[st + i] = i == 0;
     }
 }
@@ -1624,6 +1633,9 @@ struct MsdDriver {
     int cur_big = 0;
     int phase = 0;  // key word being sorted (multi-word keys)
     uint32_t ctiles = kChunkTiles;  // tiles per column-scan chunk
+    // final keys: the finishing kernels also write every key to keys[0], so a one-word sort ends
+    // with sorted keys + starts + heads in HBM (no re-encode by gather afterwards)
+    int wkeys = 0;
     const uint64_t *pk_code = nullptr;  // packed sequence for the L0 passes (ACGT, 2-bit keys)
     const uint32_t *pk_dol = nullptr;
 
@@ -2101,27 +2113,27 @@ struct MsdDriver {
         switch (k) {
         case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)
             hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
             break;
         case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
                  // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
             hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
             break;
         case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
                  // on C5 (A/B, one box)
             hipLaunchKernelGGL((msd_wave_kernel<16, 3>), grid((const void *)msd_wave_kernel<16, 3>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
                                grid((const void *)msd_local_kernel<kBT, kBI, kBR>, kBT), dim3(kBT), 0, c->stream, lst,
                                cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
-                               (uint32_t)kSmall);  // the block class keeps kSmall: 96 measured slower (A/B)
+                               (uint32_t)kSmall, wkeys);  // the block class keeps kSmall: 96 measured slower (A/B)
             break;
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
-                               v1, heads);
+                               v1, heads, wkeys);
         }
     }
 
@@ -2185,7 +2197,7 @@ struct MsdDriver {
         }
         if (ndone > 0) {
             hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len,
-                               dn_par, c->vals[1], c->vals[0], heads);
+                               dn_par, c->vals[1], c->vals[0], wkeys ? c->keys[1] : nullptr, c->keys[0], heads);
             GK_TRY_HIP(c, hipGetLastError());
         }
         c->heads = heads;
@@ -2203,6 +2215,8 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
+    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
@@ -2249,6 +2263,8 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
+    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = kGR;  // pieces are kGR-bit buckets
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
@@ -2297,6 +2313,8 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
+    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = range_width(ks);
     timer_begin(c, "msd_total", &d.total_slot);
     GK_TRY_HIP(c, msd_tables());

@@ -48,7 +48,7 @@ EXPORTED = (
     "gk_create", "gk_destroy", "gk_last_error", "gk_sync", "gk_device_count", "gk_set_sequence",
     "gk_alphabet_is_acgt", "gk_enumerate", "gk_set_start_indices", "gk_sort", "gk_num_kmers",
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
-    "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_views",
+    "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range",
@@ -113,6 +113,7 @@ _SIGS = {
                           _U64P], ctypes.c_int),
     "gk_unique_counts": ([_P, _U64P], ctypes.c_int),
     "gk_copy_unique": ([_P, _U64P, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_device_unique": ([_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _U64P], ctypes.c_int),
     "gk_device_views": ([_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _U64P, _U32P], ctypes.c_int),
     "gk_profile_enable": ([_P, ctypes.c_int], ctypes.c_int),
     "gk_profile_report": ([_P, ctypes.c_char_p, ctypes.c_uint64], ctypes.c_int),
@@ -424,6 +425,20 @@ class Engine:
         self._check(self.lib.gk_device_views(self.ctx, ctypes.byref(s), ctypes.byref(k), ctypes.byref(n),
                                              ctypes.byref(w)))
         return s.value, k.value, n.value, w.value
+
+    def device_unique(self):
+        """(device group starts u32*, device counts u32*, n_unique) of the last unique_counts."""
+        g, c, n = _P(), _P(), ctypes.c_uint64()
+        self._check(self.lib.gk_device_unique(self.ctx, ctypes.byref(g), ctypes.byref(c), ctypes.byref(n)))
+        return g.value, c.value, n.value
+
+    def materialize_keys(self) -> int:
+        """Make the sorted keys resident (re-encoded from the sorted starts if the sort left them
+        stale); returns the key words per k-mer."""
+        s, k, n, w = _P(), _P(), ctypes.c_uint64(), ctypes.c_uint32()
+        self._check(self.lib.gk_device_views(self.ctx, ctypes.byref(s), ctypes.byref(k), ctypes.byref(n),
+                                             ctypes.byref(w)))
+        return w.value
 
     def device_starts(self):
         """(device pointer of the current start indices, n) -- no key materialisation."""

@@ -176,6 +176,7 @@ class ShardedKmerSort:
             torch.cuda.current_stream(self.dev).synchronize()
         self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk, canonical=self.canonical)
         self.local_kmers = R
+        self.engine.materialize_keys()
         return self.engine.unique_count_only()
 
 
@@ -187,7 +188,7 @@ class KeyRangeKmerSort:
     moving k-mers to their owner, each rank re-derives its own from the sequence:
 
     1. ``shard_histogram``: top-digit histogram of the k-mers starting in the rank's position share;
-    2. ``all_reduce`` (sum) of the histograms -- 2 KiB, the only collective -- and the same split of
+    2. ``all_reduce`` (sum) of the histograms -- 1 KiB, the only collective -- and the same split of
        the digits into N contiguous ranges of about n/N k-mers on every rank (``split_buckets``);
     3. ``shard_sort_range``: the rank scans the whole sequence, keeps the k-mers of its digit range
        (compacted per wave before ranking, so the kept share sets the cost) and sorts them.
@@ -231,4 +232,5 @@ class KeyRangeKmerSort:
         self.digit_bounds = bounds
         self.local_kmers = self.engine.shard_sort_range(self.k, bounds[self.rank], bounds[self.rank + 1],
                                                         canonical=self.canonical)
+        self.engine.materialize_keys()  # sorted keys + unique starts and counts stay in HBM
         return self.engine.unique_count_only()

@@ -151,12 +151,19 @@ int gk_group_hist(gk_ctx *ctx, int is_sorted, int64_t kmer_len, const gk_filter 
 int gk_group_members(gk_ctx *ctx, int is_sorted, int64_t kmer_len, const gk_filter *filter, int64_t min_group_size,
                      int64_t max_group_size, int64_t yield_first_n, uint64_t *kmer_num, uint32_t *size_yielded,
                      uint32_t *size_total, uint64_t capacity, uint64_t *n_out, int32_t *err_code, uint64_t *err_idx);
-/* distinct k-mers of the sorted order (kmer_len = sort length): first index and multiplicity */
+/* distinct k-mers of the sorted order (kmer_len = sort length): first sorted index and multiplicity
+ * of each, computed and kept in HBM (after a one-word sort, one selection pass over the sort's
+ * group heads writes both); gk_copy_unique copies them out, gk_device_unique exposes them.
+ * Together with the sorted starts and keys (gk_device_views) this is the unique/count product. */
 int gk_unique_counts(gk_ctx *ctx, uint64_t *n_unique);
 int gk_copy_unique(gk_ctx *ctx, uint64_t *group_start, uint32_t *count, uint64_t n);
+/* device pointers of the unique output: group_start uint32[n_unique], count uint32[n_unique] */
+int gk_device_unique(gk_ctx *ctx, void **group_start, void **count, uint64_t *n_unique);
 
 /* ---- device views / timing (bench + multi-GPU orchestration) --------------------------------- */
-/* device pointers of the current sorted start indices and keys (valid until the next call) */
+/* device pointers of the current sorted start indices and keys (valid until the next call); with
+ * keys != NULL the keys are materialised first if the sort left them stale (multi-word keys, mixed
+ * alphabets: a re-encode from the sorted starts); a one-word sort writes them in sorted order */
 int gk_device_views(gk_ctx *ctx, void **starts, void **keys, uint64_t *n, uint32_t *words_per_key);
 /* enable per-kernel HIP-event timing; gk_profile_report writes a JSON object to buf */
 int gk_profile_enable(gk_ctx *ctx, int on);

@@ -134,10 +134,21 @@ class SortedOutputCheck:
 
     # ------------------------------------------------------------------------------------------
     def check_sorted(self, starts_ptr, n: int, keys_ptr=0, key_words: int = 0,
-                     max_counts_bin: int = 64, chunk: int = 1 << 27):
+                     max_counts_bin: int = 64, chunk: int = 1 << 27, unique=None):
         """Walk n sorted starts (device uint32 at starts_ptr, or a host uint32 array) and the
         product's keys (device uint64 SoA at keys_ptr, or a host (n, words) array; 0 = none).
+        unique = (group_start, count, n_unique) of the product's unique output (device uint32
+        pointers or host arrays): every group start must be a recomputed group head, and every
+        count the distance to the next head.
         Returns (n_groups, hist) and asserts order, tie order, permutation and keys."""
+        ubuf = torch.empty(chunk + 1, dtype=torch.int32, device=self.dev)
+
+        def read_u32(src, a, m):
+            if isinstance(src, np.ndarray):
+                ubuf[:m] = torch.from_numpy(src[a:a + m].astype(np.uint32).view(np.int32))
+            else:
+                d2d(ubuf, src + 4 * a, 4 * m)
+            return ubuf[:m].to(torch.int64) & 0xFFFFFFFF
         pk = self.position_keys()
         valid = self.valid_starts()
         n_valid = int(valid.sum().item())
@@ -183,6 +194,10 @@ class SortedOutputCheck:
             heads = torch.nonzero(~eq).flatten() + base + 1
             if prev_key is None:
                 heads = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.dev), heads])
+            if unique is not None and heads.numel():
+                assert groups + heads.numel() <= unique[2], "fewer unique k-mers in the product than groups"
+                got = read_u32(unique[0], groups, heads.numel())
+                assert torch.equal(got, heads), f"product group starts differ from the groups near {a}"
             if heads.numel():
                 bounds = torch.cat([torch.tensor([last_head], device=self.dev), heads])
                 sizes = bounds[1:] - bounds[:-1]
@@ -196,6 +211,20 @@ class SortedOutputCheck:
             del g, s
         if n:
             hist[min(n - last_head, max_counts_bin)] += 1
+        if unique is not None:
+            G = unique[2]
+            assert G == groups, f"product has {G} unique k-mers, the sorted order {groups} groups"
+            total = 0
+            for a in range(0, G, chunk):
+                m = min(chunk, G - a)
+                gs = read_u32(unique[0], a, m).clone()
+                nxt = read_u32(unique[0], a + 1, m - 1) if m > 1 else gs[:0]
+                end = n if a + m >= G else int(read_u32(unique[0], a + m, 1)[0].item())
+                want = torch.cat([nxt, torch.tensor([end], device=self.dev)]) - gs
+                cnt = read_u32(unique[1], a, m)
+                assert torch.equal(cnt, want), f"product multiplicities differ near unique k-mer {a}"
+                total += int(cnt.sum().item())
+            assert total == n, "multiplicities do not sum to the number of k-mers"
         assert torch.equal(seen.bool(), valid), "sorted starts are not a permutation of the enumerated starts"
         del pk, seen, valid
         torch.cuda.empty_cache()

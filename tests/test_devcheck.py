@@ -32,10 +32,41 @@ def _case(k=9, canonical=False, seed=3):
 def test_accepts_oracle_output(k, canonical):
     sba, srt, keys, hist = _case(k, canonical)
     chk = devcheck.SortedOutputCheck(sba, k, 4, canonical=canonical, device="cpu")
+    gs, cnt = _unique(keys)
     groups, h = chk.check_sorted(srt, len(srt), keys_ptr=keys, key_words=keys.shape[1], max_counts_bin=8,
-                                 chunk=257)
+                                 chunk=257, unique=(gs, cnt, len(gs)))
     np.testing.assert_array_equal(h, hist)
     assert groups == int(hist.sum())
+
+
+def _unique(keys):
+    heads = np.concatenate([[True], (keys[1:] != keys[:-1]).any(axis=1)])
+    gs = np.flatnonzero(heads).astype(np.uint32)
+    cnt = np.diff(np.append(gs.astype(np.int64), len(keys))).astype(np.uint32)
+    return gs, cnt
+
+
+def test_rejects_wrong_multiplicity():
+    sba, srt, keys, _ = _case()
+    gs, cnt = _unique(keys)
+    i = int(np.argmax(cnt > 1))
+    cnt = cnt.copy()
+    cnt[i] -= 1
+    chk = devcheck.SortedOutputCheck(sba, 9, 4, device="cpu")
+    with pytest.raises(AssertionError, match="multiplicities"):
+        chk.check_sorted(srt, len(srt), keys_ptr=keys, key_words=keys.shape[1], max_counts_bin=8, chunk=257,
+                         unique=(gs, cnt, len(gs)))
+
+
+def test_rejects_wrong_group_start():
+    sba, srt, keys, _ = _case()
+    gs, cnt = _unique(keys)
+    gs = gs.copy()
+    gs[300] += 1
+    chk = devcheck.SortedOutputCheck(sba, 9, 4, device="cpu")
+    with pytest.raises(AssertionError, match="group starts"):
+        chk.check_sorted(srt, len(srt), keys_ptr=keys, key_words=keys.shape[1], max_counts_bin=8, chunk=257,
+                         unique=(gs, cnt, len(gs)))
 
 
 def _expect_fail(sba, srt, keys, k=9, match=None):

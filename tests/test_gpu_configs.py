@@ -90,8 +90,9 @@ def _full_size_check(sba, seg, k, canonical, product_keys, expect_n):
     assert n == expect_n
     _log(f"sorted {n:,} {k}-mers in {time.time() - t0:.1f} s (incl. H2D)")
     hist_dev, total = km.get_kmer_group_counts(k, max_counts_bin=64)
-    n_unique = eng.unique_count_only()
-    assert total == n
+    n_unique = eng.unique_count_only()  # group starts + multiplicities, resident in HBM
+    gs_ptr, cnt_ptr, n_unique2 = eng.device_unique()
+    assert total == n and n_unique2 == n_unique
     bits = 2 if eng.is_acgt() else 4
     if product_keys:
         starts_ptr, keys_ptr, n2, words = eng.device_views()
@@ -100,7 +101,8 @@ def _full_size_check(sba, seg, k, canonical, product_keys, expect_n):
     assert n2 == n
     chk = devcheck.SortedOutputCheck(sba, k, bits, canonical=canonical)
     groups, hist = chk.check_sorted(starts_ptr, n, keys_ptr=keys_ptr if product_keys else 0,
-                                    key_words=words if product_keys else 0, max_counts_bin=64)
+                                    key_words=words if product_keys else 0, max_counts_bin=64,
+                                    unique=(gs_ptr, cnt_ptr, n_unique))
     del chk
     _log(f"device property checks done ({time.time() - t0:.1f} s): {groups:,} groups")
     assert groups == n_unique

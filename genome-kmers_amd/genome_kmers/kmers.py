@@ -483,6 +483,10 @@ class Kmers:
                 raise TypeError("kmer_sba_start_indices is None")
             self._get_engine().set_start_indices(np.asarray(self._host_starts, dtype=np.uint32), self.min_kmer_len)
             self._device_stale = False
+            if self._canonical and self._is_sorted:
+                # a canonical order loaded from a file: the device re-derives its canonical sorted
+                # state (the same order: equal canonical k-mers are in start order either way)
+                self._engine.sort(self.max_kmer_len, canonical=True)
         if self._engine is None:
             raise TypeError("Kmers has no sequence collection / k-mers")
 
@@ -728,10 +732,12 @@ class Kmers:
             g["_is_sorted"] = self._is_sorted
             s = self.kmer_sba_start_indices
             g["kmer_sba_start_indices"] = np.array([], dtype=np.uint32) if s is None else s
+            if self._canonical:  # this build's extension; the reference's loader ignores the extra key
+                g["_canonical"] = True
         if include_sequence_collection:
             self.seq_coll.save(save_file_path, mode="a", format="hdf5")
 
-    def _restore(self, starts, seq_coll):
+    def _restore(self, starts, seq_coll, canonical=False):
         self.seq_coll = seq_coll
         self._engine = None
         if starts is not None and seq_coll is not None and seq_coll.forward_sba is not None:
@@ -740,6 +746,9 @@ class Kmers:
             self._host_starts = starts
             self._host_valid = True
             self._device_stale = starts is not None
+        # a canonical sort saved by this build (the reference has no canonical order); any other
+        # file restores a forward order, whatever this object held before
+        self._canonical = bool(canonical)
 
     def _load_hdf5(self, load_file_path, seq_coll=None):
         import h5py
@@ -756,10 +765,11 @@ class Kmers:
             self._is_sorted = g["_is_sorted"][()]
             s = g["kmer_sba_start_indices"][:]
             starts = None if s.shape == (0,) else s
+            canonical = bool(g["_canonical"][()]) if "_canonical" in g else False
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="hdf5")
-        self._restore(starts, seq_coll)
+        self._restore(starts, seq_coll, canonical)
 
     def _save_shelve(self, save_file_path, include_sequence_collection=False):
         with shelve.open(str(save_file_path)) as db:
@@ -767,6 +777,8 @@ class Kmers:
                       "_is_initialized", "_is_set", "_is_sorted"):
                 db[k] = getattr(self, k)
             db["kmer_sba_start_indices"] = self.kmer_sba_start_indices
+            if self._canonical:  # this build's extension; the reference's loader ignores the extra key
+                db["_canonical"] = True
         if include_sequence_collection:
             self.seq_coll.save(save_file_path, format="shelve")
 
@@ -776,10 +788,11 @@ class Kmers:
                       "_is_initialized", "_is_set", "_is_sorted"):
                 setattr(self, k, db[k])
             starts = db["kmer_sba_start_indices"]
+            canonical = bool(db.get("_canonical", False))
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="shelve")
-        self._restore(starts, seq_coll)
+        self._restore(starts, seq_coll, canonical)
 
     # ---- readback (kmers.py:1533-1622) -------------------------------------------------------
     def _start_at(self, kmer_num: int) -> int:

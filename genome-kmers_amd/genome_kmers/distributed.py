@@ -85,7 +85,8 @@ class ShardedKmerSort:
     """
 
     def __init__(self, sba: np.ndarray, seg_starts: np.ndarray, k: int, rank: int, world: int, device: int = 0,
-                 engine=None, torch_device=None, group=None, chunk: int = None, canonical: bool = False):
+                 engine=None, torch_device=None, group=None, chunk: int = None, canonical: bool = False,
+                 stage_host: bool = None):
         import torch
         import torch.distributed as dist
 
@@ -115,6 +116,11 @@ class ShardedKmerSort:
         self.bucket_bounds = None
         if chunk:
             self.CHUNK_BYTES = chunk
+        # device buffers over a backend without device point-to-point (gloo): the exchange is
+        # staged through host copies of the send and receive segments
+        if stage_host is None:
+            stage_host = self.dev.type != "cpu" and dist.is_initialized() and dist.get_backend(group) == "gloo"
+        self.stage_host = stage_host
 
     def _ensure_recv(self, n: int):
         if self.recv_k.numel() < n + 64:
@@ -133,6 +139,10 @@ class ShardedKmerSort:
         dist = self.dist
         so = np.concatenate(([0], np.cumsum(send_counts)[:-1])).astype(np.int64)
         ro = np.concatenate(([0], np.cumsum(recv_counts)[:-1])).astype(np.int64)
+        if self.stage_host:
+            dev_recv = recv
+            send = send[:int(np.sum(send_counts))].cpu()
+            recv = self.torch.empty(int(np.sum(recv_counts)), dtype=recv.dtype)
         step = max(1, self.CHUNK_BYTES // send.element_size())
         me = self.rank
         ops = []
@@ -151,13 +161,15 @@ class ShardedKmerSort:
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+        if self.stage_host and recv.numel():
+            dev_recv[:recv.numel()].copy_(recv)
 
     def run(self) -> int:
         """One sort; returns this rank's number of distinct k-mers."""
         torch, dist = self.torch, self.dist
         hist, n = self.engine.shard_partition(self.lo, self.hi, self.k, self.send_k, self.send_v,
                                               canonical=self.canonical)
-        h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to(self.dev)
+        h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to("cpu" if self.stage_host else self.dev)
         gathered = [torch.empty_like(h) for _ in range(self.world)]
         dist.all_gather(gathered, h, group=self.group)
         H = torch.stack(gathered).cpu().numpy()

@@ -351,6 +351,64 @@ def test_gpu_key_range_repeated_calls(world, k, canonical):
     np.testing.assert_array_equal(np.concatenate([got[r] for r in range(world)]), ref.copy_starts())
 
 
+def _gpu_a2a_worker(rank, world, port, sba, seg, k, canonical, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # device send / receive buffers, the exchange staged through host memory (gloo)
+        job = D.ShardedKmerSort(sba, seg, k, rank, world, device=0, torch_device=torch.device("cuda", 0),
+                                canonical=canonical, chunk=1 << 16)
+        assert job.stage_host
+        u = job.run()
+        q.put((rank, job.engine.copy_starts().tolist(), u, job.local_kmers))
+    except Exception as exc:  # report instead of leaving the parent waiting
+        q.put((rank, repr(exc), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,canonical,iupac", [(31, False, False), (63, False, True), (31, True, False)])
+def test_gpu_all_to_all_two_processes(k, canonical, iupac):
+    """The north star's exchange path as two real processes, each with its own libgkm engine on GPU
+    0: gk_shard_partition of the rank's position share, the all-to-all of (key, start) over gloo
+    (device buffers staged through the host, messages of 64 KiB), gk_shard_sort of the received
+    buckets; the rank-ordered concatenation equals the single-GPU sort."""
+    import torch.multiprocessing as mp
+
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(300_000 + 5, 13, 3)
+    sba[250_000:251_000] = sba[2000:3000]  # a repeat across ranks (inside the third contig)
+    sba[150_000:150_900] = oracle.reverse_complement(sba[5000:5900])
+    if iupac:
+        sba[60_000:60_400] = ord("N")
+        sba[90_000:90_050:7] = ord("R")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_a2a_worker, args=(r, 2, port, sba, seg, k, canonical, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[2] is not None for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    n = ref.enumerate(k)
+    ref.sort(k, canonical=canonical)
+    assert sum(r[3] for r in res) == n
+    np.testing.assert_array_equal(np.concatenate([np.asarray(r[1], dtype=np.uint32) for r in res]), ref.copy_starts())
+    assert sum(r[2] for r in res) == ref.unique_count_only()
+
+
 def _gpu_range_worker(rank, world, port, sba, seg, k, q):
     import torch
     import torch.distributed as dist

@@ -182,13 +182,16 @@ int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
         }
         c->elem_cap = n;
         c->key_words_cap = 0;
+        c->key_words_b[0] = c->key_words_b[1] = 0;
         c->keys_valid = false;
     }
     if (words > c->key_words_cap) {
         for (int b = 0; b < 2; ++b) {
+            if (c->key_words_b[b] >= words) continue;
             if (c->keys[b]) hipFree(c->keys[b]);
             c->keys[b] = nullptr;
             GK_TRY_HIP(c, hipMalloc(&c->keys[b], 8 * (uint64_t)words * (c->elem_cap + 64)));
+            c->key_words_b[b] = words;
         }
         c->key_words_cap = words;
         c->keys_valid = false;
@@ -201,6 +204,17 @@ int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
         GK_TRY_HIP(c, hipMemsetAsync(c->status, 0, 8 * tiles * 256, c->stream));
         c->status_cap = tiles * 256;
     }
+    return GK_OK;
+}
+
+int gkm::grow_key_buffer(gk_ctx *c, int b, int words) {
+    if (c->key_words_b[b] >= words) return GK_OK;
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->keys[b]) hipFree(c->keys[b]);
+    c->keys[b] = nullptr;
+    GK_TRY_HIP(c, hipMalloc(&c->keys[b], 8 * (uint64_t)words * (c->elem_cap + 64)));
+    c->key_words_b[b] = words;
+    c->key_words_cap = std::min(c->key_words_b[0], c->key_words_b[1]);
     return GK_OK;
 }
 
@@ -438,7 +452,7 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         c->keys_valid = true;
         // a one-word MSD sort leaves the sorted keys in keys[0]; the split sort (2-bit class-A keys
         // under a 4-bit key spec) and multi-word phases leave them to ensure_keys
-        c->keys_stale = split || !c->msd_keys_final;
+        c->keys_stale = split ? !c->split_keys_final : !c->msd_keys_final;
         c->keys_are_ranks = false;
         return GK_OK;
     }
@@ -921,7 +935,7 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     if (rc != GK_OK) return rc;
     c->spec = ks;
     c->keys_valid = true;
-    c->keys_stale = c->n > 0 && (range_split(c, ks) || !c->msd_keys_final);  // see sort_direct
+    c->keys_stale = c->n > 0 && (range_split(c, ks) ? !c->split_keys_final : !c->msd_keys_final);  // see sort_direct
     c->keys_are_ranks = false;
     c->sorted = true;
     c->sort_len = k;

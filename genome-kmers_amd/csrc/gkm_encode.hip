@@ -6,8 +6,11 @@
 //   alphabet    sequence_collection.py:441-458, 694-697  {A,C,G,T,R,Y,S,W,K,M,B,D,H,V,N,$}
 // The encoders turn the k-mer at a start into an integer whose unsigned order equals that byte
 // order: 2-bit codes when the sba is pure ACGT, 4-bit codes ('$' = 0) otherwise.
+#include <cstdlib>
+
 #include "gkm_canon.h"
 #include "gkm_internal.h"
+#include "gkm_swar.h"
 
 namespace gkm {
 
@@ -361,6 +364,113 @@ __global__ __launch_bounds__(256) void encode_generic_kernel(const uint8_t *__re
 // ---------------------------------------------------------------------------------------------
 // gather encode: keys of arbitrary starts (user-provided or re-sorted arrays)
 // ---------------------------------------------------------------------------------------------
+// Fixed-length keys (k <= 64) of windows holding only A, C, G, T -- ~95 % of a GRCh38-like genome,
+// all of a random one -- without a per-byte loop: the window is read as 8-byte words (a funnel
+// shift per word aligns it to the start), 8 bytes become 16 bits of 2-bit codes by SWAR
+// (pack2_8), the canonical choice is one 128-bit compare against the bit-reversed complement, and
+// 4-bit keys expand the 2-bit codes nibble by nibble (A 1, C 3, G 5, T 12: 2 s + 1, + 5 for T).
+// Windows with another byte take the per-byte path below.
+
+// 2-bit codes (A0 C1 G2 T3) of 8 bytes as 16 bits, byte 0 in the most significant pair
+__device__ __forceinline__ uint32_t pack2_8e(uint64_t x) {
+    uint64_t t = __builtin_bswap64(((x >> 1) ^ (x >> 2)) & 0x0303030303030303ull);
+    t = (t | (t >> 6)) & 0x000F000F000F000Full;
+    t = (t | (t >> 12)) & 0x000000FF000000FFull;
+    return (uint32_t)((t | (t >> 24)) & 0xFFFFu);
+}
+
+// the k (<= 64) symbols from sba[s] as a right-aligned 2k-bit value (hi:lo); false if a window
+// byte is not A, C, G or T (reads up to 72 bytes from s & ~7: the sba carries a '$' pad)
+__device__ __forceinline__ bool window2_acgt(const uint8_t *sba, uint64_t s, int k, uint64_t &hi, uint64_t &lo) {
+    const uint64_t a = s & ~7ull;
+    const int sh = (int)(s - a) * 8;
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(sba + a);
+    uint64_t prev = p[0];
+    uint64_t bad = 0;
+    hi = lo = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (8 * j >= k) break;
+        const uint64_t nxt = p[j + 1];
+        const uint64_t w = sh ? (prev >> sh) | (nxt << (64 - sh)) : prev;
+        prev = nxt;
+        const int nb = min(8, k - 8 * j);
+        const uint64_t m = nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        bad |= non_acgt_bytes(w) & m;
+        const uint32_t v = pack2_8e(w) >> (16 - 2 * nb);
+        hi = (hi << (2 * nb)) | (lo >> (64 - 2 * nb));
+        lo = (lo << (2 * nb)) | v;
+    }
+    return bad == 0;
+}
+
+// the 32 2-bit groups of x in reverse order
+__device__ __forceinline__ uint64_t rev_pairs(uint64_t x) {
+    x = __builtin_bswap64(x);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    return ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+}
+
+// canonical = min(k-mer, reverse complement) of a right-aligned 2k-bit value, in place
+__device__ __forceinline__ void canon2(int k, uint64_t &hi, uint64_t &lo) {
+    uint64_t rh = rev_pairs(~lo), rl = rev_pairs(~hi);  // complement, 64 groups reversed (left-aligned)
+    const int s = 128 - 2 * k;
+    if (s >= 64) {
+        rl = rh >> (s - 64);
+        rh = 0;
+    } else if (s > 0) {
+        rl = (rl >> s) | (rh << (64 - s));
+        rh >>= s;
+    }
+    if (rh < hi || (rh == hi && rl < lo)) {
+        hi = rh;
+        lo = rl;
+    }
+}
+
+template <int W, int BITS>
+__global__ __launch_bounds__(256) void encode_gather_fast_kernel(const uint8_t *__restrict__ sba, KS ks,
+                                                                 const uint32_t *__restrict__ starts, uint64_t n,
+                                                                 uint64_t *__restrict__ keys) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    __syncthreads();
+    const int k = ks.symbols;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t st = starts[i];
+        uint64_t hi, lo;
+        uint64_t w[W];
+        if (window2_acgt(sba, st, k, hi, lo)) {
+            if (ks.canonical) canon2(k, hi, lo);
+            if (BITS == 2) {
+                w[W - 1] = lo;
+                if (W > 1) w[0] = hi;
+            } else {
+                const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
+#pragma unroll
+                for (int q = 0; q < W; ++q) {  // q: word from the least significant end
+                    uint64_t e = expand4_16((uint32_t)part[q]);
+                    const int left = k - 16 * q;  // symbols in this word
+                    if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
+                    w[W - 1 - q] = e;
+                }
+            }
+        } else {
+            const uint8_t *b = sba + st;
+            if (ks.canonical) {
+                const bool rc = canon_is_rc<BITS>(b, k, s_lut4);
+#pragma unroll
+                for (int q = 0; q < W; ++q) w[q] = 0;
+                for (int t = 0; t < k; ++t) bi_shl_or<W>(w, BITS, canon_sym<BITS>(b, k, t, rc, s_lut4));
+            } else {
+                window_key<W, BITS, false>(ks, [&](int q) { return (uint32_t)b[q]; }, s_lut4, w);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < W; ++q) keys[(uint64_t)q * n + i] = w[q];
+    }
+}
+
 template <int W, int BITS, bool BOUNDED>
 __global__ __launch_bounds__(256) void encode_gather_kernel(const uint8_t *__restrict__ sba, KS ks,
                                                             const uint32_t *__restrict__ starts, uint64_t n,
@@ -460,6 +570,13 @@ template <int W, int BITS, bool BOUNDED>
 static hipError_t gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys) {
     int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);
     if (grid < 1) grid = 1;
+    static const bool slow = std::getenv("GKM_GATHER_SLOW") != nullptr;  // A/B of the per-byte path
+    if constexpr (!BOUNDED && (BITS == 2 || BITS == 4))
+        if (k.symbols <= 64 && !slow) {
+            hipLaunchKernelGGL((encode_gather_fast_kernel<W, BITS>), dim3(grid), dim3(256), 0, c->stream, c->sba, k,
+                               starts, n, keys);
+            return hipGetLastError();
+        }
     hipLaunchKernelGGL((encode_gather_kernel<W, BITS, BOUNDED>), dim3(grid), dim3(256), 0, c->stream, c->sba, k,
                        starts, n, keys);
     return hipGetLastError();

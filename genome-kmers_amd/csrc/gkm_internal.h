@@ -87,6 +87,8 @@ struct gk_ctx {
     bool canonical = false;    // the last sort ordered canonical k-mers (GK_SORT_CANONICAL)
     bool keys_valid = false;   // keys[cur] encode the k-mers of vals[cur] (sort order)
     bool msd_keys_final = false;  // the last MSD sort wrote its (one-word) keys in sorted order
+    bool msd_force_keys = false;  // split_sort: the class-A MSD (acgt_only) writes its final keys too
+    bool split_keys_final = false;  // the last split sort wrote the final (4-bit) keys in sorted order
     bool keys_stale = false;   // ... once re-encoded from vals[cur]: the MSD sort does not keep them (ensure_keys)
     bool keys_are_ranks = false;
     gkm::KeySpec spec{};
@@ -94,7 +96,8 @@ struct gk_ctx {
     uint32_t *vals[2] = {nullptr, nullptr};
     uint64_t *keys[2] = {nullptr, nullptr};
     uint64_t elem_cap = 0;     // capacity (elements) of vals/keys buffers
-    int key_words_cap = 0;
+    int key_words_cap = 0;     // key words both key buffers hold (the smaller of key_words_b)
+    int key_words_b[2] = {0, 0};
     int cur = 0;
 
     // radix pass state
@@ -189,6 +192,8 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
 int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t digit_hi, uint64_t *n_kept);
 // key / start buffers for n elements and `words` key words (gkm_capi.hip)
 int ensure_elems(gk_ctx *c, uint64_t n, int words);
+// key buffer b alone grown to `words` key words of elem_cap elements (contents not kept)
+int grow_key_buffer(gk_ctx *c, int b, int words);
 void timer_begin(gk_ctx *c, const char *name, int *slot);
 void timer_end(gk_ctx *c, int slot);
 void timer_units(gk_ctx *c, int slot, uint64_t units);

@@ -2215,7 +2215,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
-    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
@@ -2263,7 +2263,7 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
-    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = kGR;  // pieces are kGR-bit buckets
     timer_begin(c, "msd_total", &d.total_slot);
@@ -2313,7 +2313,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
-    d.wkeys = (nphase == 1 && !ks.acgt_only) ? 1 : 0;  // one-word keys end final in keys[0]
+    d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = range_width(ks);
     timer_begin(c, "msd_total", &d.total_slot);

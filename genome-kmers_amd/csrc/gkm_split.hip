@@ -14,6 +14,7 @@
 // complement, so the split applies to them unchanged.
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 
 #include "gkm_canon.h"
 #include "gkm_internal.h"
@@ -288,11 +289,25 @@ __device__ __forceinline__ uint64_t bound_in(const uint32_t *v, uint64_t lo, uin
     return lo;
 }
 
+// With keys (W > 0): the A k-mers' final 2-bit keys (a_keys) are expanded to the W-word 4-bit keys
+// of the merged order (out_keys, word-major with stride n).
+template <int W>
+__device__ __forceinline__ void put_key4(const uint64_t *a_keys, uint64_t i, int k, uint64_t *out_keys, uint64_t n,
+                                         uint64_t o) {
+    uint64_t w[W];
+    expand4_key<W>(a_keys[i], k, w);
+#pragma unroll
+    for (int q = 0; q < W; ++q) out_keys[(uint64_t)q * n + o] = w[q];
+}
+
+template <int W>
 __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict__ a_starts,
                                                       const uint8_t *__restrict__ a_heads, uint64_t nA,
                                                       const uint32_t *__restrict__ pos,
                                                       const uint32_t *__restrict__ g_first, uint64_t G, uint64_t nB,
-                                                      uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads) {
+                                                      uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads,
+                                                      const uint64_t *__restrict__ a_keys, int k,
+                                                      uint64_t *__restrict__ out_keys) {
     __shared__ uint64_t s_g[3];  // ub(i0), lb(i0), groups with pos < i1
     const uint64_t i0 = (uint64_t)blockIdx.x * kMTile;
     const uint64_t i1 = min(i0 + kMTile, nA);
@@ -308,6 +323,7 @@ __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict
         for (uint64_t i = i0 + threadIdx.x; i < i1; i += kMT) {
             out[i + shift] = a_starts[i];
             out_heads[i + shift] = (a_heads[i] || (i == i0 && g0 > lb0)) ? 1 : 0;
+            if (W) put_key4<(W ? W : 1)>(a_keys, i, k, out_keys, nA + nB, i + shift);
         }
         return;
     }
@@ -317,15 +333,20 @@ __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict
         const uint64_t shift = ub < G ? g_first[ub] : nB;
         out[i + shift] = a_starts[i];
         out_heads[i + shift] = (a_heads[i] || ub > lb) ? 1 : 0;
+        if (W) put_key4<(W ? W : 1)>(a_keys, i, k, out_keys, nA + nB, i + shift);
     }
 }
 
 // B element j of group g goes to j + pos[g]; per 4096 B elements, the groups they span
+// With keys (W > 0): the B k-mers' 4-bit keys (b_keys, word-major with stride nB) go along.
+template <int W>
 __global__ __launch_bounds__(kMT) void merge_b_kernel(const uint32_t *__restrict__ b_starts,
                                                       const uint8_t *__restrict__ b_heads, uint64_t nB,
                                                       const uint32_t *__restrict__ pos,
                                                       const uint32_t *__restrict__ g_first, uint64_t G,
-                                                      uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads) {
+                                                      uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads,
+                                                      const uint64_t *__restrict__ b_keys, uint64_t n,
+                                                      uint64_t *__restrict__ out_keys) {
     __shared__ uint64_t s_g[2];  // group of j0, groups starting at or before j1 - 1
     const uint64_t j0 = (uint64_t)blockIdx.x * kMTile;
     const uint64_t j1 = min(j0 + kMTile, nB);
@@ -339,7 +360,21 @@ __global__ __launch_bounds__(kMT) void merge_b_kernel(const uint32_t *__restrict
         const uint64_t g = gb == ga + 1 ? ga : bound_in(g_first, ga, gb, j, true) - 1;
         out[j + pos[g]] = b_starts[j];
         out_heads[j + pos[g]] = b_heads[j];
+#pragma unroll
+        for (int q = 0; q < W; ++q) out_keys[(uint64_t)q * n + j + pos[g]] = b_keys[(uint64_t)q * nB + j];
     }
+}
+
+// keys of the A k-mers when no B k-mer exists: the 2-bit keys expanded in place of the merge
+template <int W>
+__global__ __launch_bounds__(256) void expand_keys_kernel(const uint64_t *__restrict__ a_keys, uint64_t n, int k,
+                                                          uint64_t *__restrict__ out_keys) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        put_key4<W>(a_keys, i, k, out_keys, n, i);
+}
+
+__global__ __launch_bounds__(256) void fill_u64_kernel(uint64_t *__restrict__ p, uint64_t n, uint64_t v) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] = v;
 }
 
 static unsigned grid_of_n(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384)); }
@@ -355,6 +390,10 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     if (k > 64 || ks.bits != 4 || ks.lenbits || ks.symbols != ks.min_len) return GK_OK;
     if (rg && k < 4) return fail(c, GK_E_ARG, "split: key-range shards need k >= 4");
     GK_TRY_HIP(c, split_tables());
+    c->split_keys_final = false;
+    // final keys: with one-word 2-bit class-A keys (k <= 32) the sorted order leaves with its W-word
+    // 4-bit keys -- A's expanded in the merge, B's from their own sort -- and needs no re-encode
+    const int WK = k <= 32 ? ks.words : 0;
     int slot;
     // 1. class B starts: homopolymers (one letter k times) apart from the rest
     uint32_t *b_st[2], *h_st;
@@ -433,6 +472,11 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         hipLaunchKernelGGL(key_heads_kernel, dim3(grid_of_n(nR)), dim3(256), 0, c->stream, b_k[bres], nR, W, b_heads);
         GK_TRY_HIP(c, hipGetLastError());
     }
+    // B's final keys (word-major, stride nB): the rest's sorted keys, with the homopolymer groups'
+    // constant keys spliced in below
+    const uint64_t *b_keys = nR > 0 ? b_k[bres] : nullptr;
+    uint64_t *bkf = nullptr;
+    if (WK && nH > 0) GK_TRY_HIP(c, scratch(c, "split_b_kf", (uint64_t)WK * (nB + 64), &bkf));
     if (nH > 0) {
         // 2b. the homopolymer groups (one per (canonical) letter, members in start order) go into
         // the sorted B run at their insertion points: at most 15 segment copies
@@ -500,21 +544,38 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
             hipError_t e = hipMemcpyAsync(fst + out, b_st[bres] + rcur, 4 * m, hipMemcpyDeviceToDevice, c->stream);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(fhd + out, b_heads + rcur, m, hipMemcpyDeviceToDevice, c->stream);
+            for (int q = 0; q < WK && e == hipSuccess; ++q)
+                e = hipMemcpyAsync(bkf + (uint64_t)q * nB + out, b_keys + (uint64_t)q * nR + rcur, 8 * m,
+                                   hipMemcpyDeviceToDevice, c->stream);
             rcur = upto;
             out += m;
             return e;
         };
+        static const char kAlpha4[] = "$ABCDGHKMNRSTVWY";  // 4-bit code = index
         for (size_t g = 0; g < letters.size(); ++g) {
             GK_TRY_HIP(c, copy_rest(ins[g]));
             const uint64_t m = hc[letters[g]];
             GK_TRY_HIP(c, hipMemcpyAsync(fst + out, grp + first[g], 4 * m, hipMemcpyDeviceToDevice, c->stream));
             GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 0, m, c->stream));
             GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 1, 1, c->stream));  // one group: one head
+            if (WK) {  // the group's k-mer: its (canonical) letter k times
+                const char *at = std::strchr(kAlpha4, (int)letters[g]);
+                const uint64_t c4 = at && letters[g] ? (uint64_t)(at - kAlpha4) : 0;
+                for (int q = 0; q < WK; ++q) {  // q: word from the most significant end
+                    uint64_t v = 0;
+                    const int lo_sym = 16 * (WK - 1 - q);  // nibble index of the word's bit 0
+                    for (int j = lo_sym; j < std::min(lo_sym + 16, k); ++j) v |= c4 << (4 * (j - lo_sym));
+                    hipLaunchKernelGGL(fill_u64_kernel, dim3(grid_of_n(m)), dim3(256), 0, c->stream,
+                                       bkf + (uint64_t)q * nB + out, m, v);
+                }
+                GK_TRY_HIP(c, hipGetLastError());
+            }
             out += m;
         }
         GK_TRY_HIP(c, copy_rest(nR));
         b_heads = fhd;
         bres ^= 1;
+        b_keys = bkf;
         timer_end(c, slot);
     }
 
@@ -525,30 +586,64 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     ka.words = (ka.total_bits + 63) / 64;
     ka.acgt_only = 1;
     int rc;
+    const uint64_t *a_keys = nullptr;  // A's final 2-bit keys (WK)
+    c->msd_force_keys = WK > 0;
     if (rg) {  // the rank's ACGT-only k-mers: select + MSD (gkm_msd.hip); room for the merge after
         rc = msd_sort_range(c, ka, rg->d_lo, rg->d_hi, &nA);
+        c->msd_force_keys = false;
         if (rc != GK_OK) return rc;
         c->have_starts = true;
+        a_keys = c->keys[0];
+        if (WK && nA + nB + 1 > c->elem_cap) {  // growing the buffers below does not keep the keys
+            uint64_t *ak;
+            GK_TRY_HIP(c, scratch(c, "split_a_keys", nA + 64, &ak));
+            GK_TRY_HIP(c, hipMemcpyAsync(ak, c->keys[0], 8 * nA, hipMemcpyDeviceToDevice, c->stream));
+            a_keys = ak;
+        }
         rc = ensure_elems(c, nA + nB + 1, 1);  // keeps vals[0] (nA)
         if (rc != GK_OK) return rc;
         c->n = nA + nB;
     } else {
         c->n = nA;
         rc = nA > 0 ? msd_sort(c, ka) : GK_OK;
+        c->msd_force_keys = false;
         c->n = n;
         if (rc != GK_OK) return rc;
+        a_keys = c->keys[0];
     }
     if (nA == 0) {  // all B: the B order is the order
         GK_TRY_HIP(c, hipMemcpyAsync(c->vals[0], b_st[bres], 4 * nB, hipMemcpyDeviceToDevice, c->stream));
         uint8_t *hd;
         GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
         GK_TRY_HIP(c, hipMemcpyAsync(hd, b_heads, nB, hipMemcpyDeviceToDevice, c->stream));
+        if (WK) {
+            if (int r = grow_key_buffer(c, 0, WK)) return r;
+            GK_TRY_HIP(c, hipMemcpyAsync(c->keys[0], b_keys, 8 * (uint64_t)WK * nB, hipMemcpyDeviceToDevice,
+                                         c->stream));  // stride nB == n
+            c->split_keys_final = true;
+        }
         c->cur = 0;
         c->heads = hd;
         c->heads_valid = true;
         return GK_OK;
     }
-    if (nB == 0) return GK_OK;  // msd_sort left vals[0] / heads in place
+    if (nB == 0) {  // msd_sort left vals[0] / heads in place; A's keys expanded next to them
+        if (WK) {
+            if (int r = grow_key_buffer(c, 1, WK)) return r;
+            const uint64_t nn = nA;
+            if (WK == 1)
+                hipLaunchKernelGGL(expand_keys_kernel<1>, dim3(grid_of_n(nn)), dim3(256), 0, c->stream, a_keys, nn, k,
+                                   c->keys[1]);
+            else
+                hipLaunchKernelGGL(expand_keys_kernel<2>, dim3(grid_of_n(nn)), dim3(256), 0, c->stream, a_keys, nn, k,
+                                   c->keys[1]);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, hipMemcpyAsync(c->vals[1], c->vals[0], 4 * nn, hipMemcpyDeviceToDevice, c->stream));
+            c->cur = 1;
+            c->split_keys_final = true;
+        }
+        return GK_OK;
+    }
 
     // 4. merge: B groups, their insertion points in A, the interleave into vals[1] + heads
     timer_begin(c, "split_merge", &slot);
@@ -562,11 +657,33 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, hipGetLastError());
     uint8_t *hd;
     GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
-    hipLaunchKernelGGL(merge_a_kernel, dim3((unsigned)((nA + kMTile - 1) / kMTile)), dim3(kMT), 0, c->stream,
-                       c->vals[0], c->heads, nA, pos, g_first, G, nB, c->vals[1], hd);
-    hipLaunchKernelGGL(merge_b_kernel, dim3((unsigned)((nB + kMTile - 1) / kMTile)), dim3(kMT), 0, c->stream,
-                       b_st[bres], b_heads, nB, pos, g_first, G, c->vals[1], hd);
+    if (WK) {
+        int r = grow_key_buffer(c, 1, WK);
+        if (r != GK_OK) return r;
+    }
+    const dim3 ga((unsigned)((nA + kMTile - 1) / kMTile)), gb((unsigned)((nB + kMTile - 1) / kMTile));
+    uint64_t *ok = c->keys[1];
+    switch (WK) {
+    case 0:
+        hipLaunchKernelGGL(merge_a_kernel<0>, ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA, pos, g_first, G,
+                           nB, c->vals[1], hd, nullptr, k, nullptr);
+        hipLaunchKernelGGL(merge_b_kernel<0>, gb, dim3(kMT), 0, c->stream, b_st[bres], b_heads, nB, pos, g_first, G,
+                           c->vals[1], hd, nullptr, n, nullptr);
+        break;
+    case 1:
+        hipLaunchKernelGGL(merge_a_kernel<1>, ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA, pos, g_first, G,
+                           nB, c->vals[1], hd, a_keys, k, ok);
+        hipLaunchKernelGGL(merge_b_kernel<1>, gb, dim3(kMT), 0, c->stream, b_st[bres], b_heads, nB, pos, g_first, G,
+                           c->vals[1], hd, b_keys, nA + nB, ok);
+        break;
+    default:
+        hipLaunchKernelGGL(merge_a_kernel<2>, ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA, pos, g_first, G,
+                           nB, c->vals[1], hd, a_keys, k, ok);
+        hipLaunchKernelGGL(merge_b_kernel<2>, gb, dim3(kMT), 0, c->stream, b_st[bres], b_heads, nB, pos, g_first, G,
+                           c->vals[1], hd, b_keys, nA + nB, ok);
+    }
     GK_TRY_HIP(c, hipGetLastError());
+    c->split_keys_final = WK > 0;
     timer_end(c, slot);
     c->cur = 1;
     c->heads = hd;

@@ -28,4 +28,29 @@ __device__ __forceinline__ uint64_t non_acgt_bytes(uint64_t x) {
            (kOnes << 7);
 }
 
+// 16 2-bit symbols (x, right-aligned, A0 C1 G2 T3) as 16 4-bit codes of the 4-bit alphabet
+// '$' A B C D G H K M N R S T V W Y (A 1, C 3, G 5, T 12: 2 s + 1, plus 5 for T), one per nibble
+__device__ __forceinline__ uint64_t expand4_16(uint32_t x) {
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;  // one symbol per nibble
+    const uint64_t t = v & (v >> 1) & 0x1111111111111111ull;  // T
+    return (v << 1) + 0x1111111111111111ull + t * 5;
+}
+
+// the W-word 4-bit key (most significant word first) of k <= 32 symbols given as a right-aligned
+// 2-bit key (the ACGT-only k-mers' MSD keys)
+template <int W>
+__device__ __forceinline__ void expand4_key(uint64_t key2, int k, uint64_t (&w)[W]) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {  // q: word from the least significant end
+        uint64_t e = q < 2 ? expand4_16((uint32_t)(key2 >> (32 * q))) : 0ull;
+        const int left = k - 16 * q;  // symbols in this word
+        if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
+        w[W - 1 - q] = e;
+    }
+}
+
 }  // namespace gkm

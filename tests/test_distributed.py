@@ -303,10 +303,11 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     else:
         assert int(hist.sum()) == total
     db = D.split_buckets(hist, world)
-    got, uniq, kept = [], 0, 0
+    got, keys, uniq, kept = [], [], 0, 0
     for r in range(world):
         kept += e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
         got.append(e.copy_starts())
+        keys.append(e.copy_keys())
         uniq += e.unique_count_only()
     assert kept == total
     ref = _native.Engine(0)
@@ -314,6 +315,7 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     ref.enumerate(k)
     ref.sort(k, canonical=canonical)
     np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
+    np.testing.assert_array_equal(np.concatenate(keys), ref.copy_keys())
     assert uniq == ref.unique_count_only()
 
 

@@ -514,3 +514,52 @@ def test_split_homopolymer_runs_of_several_letters_vs_oracle(k):
     oh, ot = oracle.group_scan(sc.forward_sba, want, k, max_counts_bin=64)
     np.testing.assert_array_equal(h, oh)
     assert t == ot
+    spec = oracle.key_spec(False, k, k)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+
+
+def _split_keys_check(seqs, k, canonical=False):
+    """Through the engine (gk_enumerate / gk_sort / gk_copy_keys): records shorter than k are legal
+    there, while Kmers.__init__ rejects them (kmers.py:744-749)."""
+    sc = SequenceCollection(sequence_list=seqs)
+    sba, seg = sc.forward_sba, sc._forward_sba_seg_starts
+    e = _native.Engine()
+    e.set_sequence(sba, seg)
+    e.enumerate(k)
+    e.sort(k, canonical=canonical)
+    unsorted = oracle.enumerate_starts(sba, seg, k)
+    if canonical:
+        want = oracle.canonical_sort(sba, unsorted, k)
+        keys = oracle.canonical_keys(sba, want, k, 4)
+    else:
+        want = oracle.quicksort(sba, unsorted, k, k, break_ties=True)
+        keys = oracle.encode_keys(sba, want, *oracle.key_spec(False, k, k))
+    np.testing.assert_array_equal(e.copy_starts(), want)
+    np.testing.assert_array_equal(e.copy_keys(), keys)
+    first, counts = e.unique_counts()
+    assert int(counts.sum()) == len(want)
+
+
+@pytest.mark.parametrize("k", [5, 20, 31])
+def test_split_only_class_b_kmers_keys(k):
+    """Every k-mer holds a non-ACGT letter (the split sort has no class-A k-mer): the keys come from
+    the B sort and the homopolymer groups' constant keys."""
+    rng = np.random.default_rng(80 + k)
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 20_000)].copy()
+    s[::max(2, k // 2)] = ord("N")  # a non-ACGT byte in every window
+    s[5000:5000 + 3 * k] = ord("R")
+    _split_keys_check([("a", s.tobytes().decode())], k)
+
+
+@pytest.mark.parametrize("k,canonical", [(31, False), (21, True), (32, True)])
+def test_split_keys_with_homopolymers(k, canonical):
+    rng = np.random.default_rng(95 + k)
+    seqs = n_run_genome(rng, [40_000, 9_000], runs=3)
+    out = []
+    for name, s in seqs:
+        b = bytearray(s.encode())
+        for letter in b"NYR":
+            a = int(rng.integers(100, len(b) - 400))
+            b[a:a + k + 40] = bytes([letter]) * (k + 40)
+        out.append((name, b.decode()))
+    _split_keys_check(out, k, canonical)

@@ -1,11 +1,21 @@
-"""Per-rank cost of the key-range multi-GPU scheme, measured on ONE GPU.
+"""Per-rank cost of the multi-GPU schemes, measured on ONE GPU.
 
-The key-range scheme (genome_kmers.distributed.KeyRangeKmerSort) has no inter-GPU data path: rank
-r's work is gk_shard_histogram over its position share plus gk_shard_sort_range over its digit
-range.  Running every rank's share one after another on a single MI355X therefore measures each
-rank's device time exactly; only the 2 KiB all-reduce is missing.  Prints one JSON line per N.
+Every rank's device work runs on a single MI355X one after another, so each rank's device time is
+measured exactly; what a real N-GPU run adds is the collective:
 
-Usage: python tools/range_emulate.py [--genome-len L] [--worlds 1,2,4,8] [--reps 2]
+  --scheme range (KeyRangeKmerSort): gk_shard_histogram over the rank's position share, then
+      gk_shard_sort_range over its digit range (keys materialised, unique counts); the missing
+      collective is the 1 KiB all-reduce of the histograms.
+  --scheme a2a (ShardedKmerSort): gk_shard_partition of the rank's position share, then
+      gk_shard_sort of the buckets it owns (pieces sliced from every rank's send buffer on the same
+      GPU); the missing collective is the all-to-all, reported as a link-bound estimate: the
+      largest per-peer message of the rank (send or receive) / 153 GB/s (one xGMI link per peer,
+      MI355X_MICROARCH.md), which no RCCL run can beat.
+
+The single-GPU step (enumerate + sort + keys + unique counts, as bench.py) and every rank are timed
+as the best of --reps runs after one warm-up.  Prints one JSON line per N.
+
+Usage: python tools/range_emulate.py [--config c3|c4|c5] [--scheme range|a2a] [--worlds 8,4,2] [--reps 2]
 """
 
 import argparse
@@ -20,13 +30,29 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "genome-kmers_amd"))
 sys.path.insert(0, str(ROOT))
 
+LINK_GBS = 153.0  # one xGMI link, per direction (MI355X_MICROARCH.md)
+
+
+def best_of(fn, reps, sync):
+    best, out = None, None
+    for rep in range(reps + 1):  # the first one warms up
+        sync()
+        t0 = time.perf_counter()
+        out = fn(rep == reps)
+        sync()
+        dt = time.perf_counter() - t0
+        if rep > 0 and (best is None or dt < best):
+            best = dt
+    return best * 1e3, out
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3")
+    ap.add_argument("--scheme", choices=("range", "a2a"), default="range")
     ap.add_argument("--genome-len", type=int, default=3_100_000_000)
     ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--worlds", type=str, default="1,2,4,8")
+    ap.add_argument("--worlds", type=str, default="8,4,2")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
 
@@ -43,57 +69,105 @@ def main():
     e.set_sequence(sba, seg)
     e.sync()
     total = D.count_kmers(len(sba), seg, k)
-    # single-GPU reference step for the same engine
-    e.enumerate(k)
-    e.sort(k, canonical=canonical)
-    e.unique_count_only()
-    e.sync()
-    t0 = time.perf_counter()
-    e.enumerate(k)
-    e.sort(k, canonical=canonical)
-    u1 = e.unique_count_only()
-    e.sync()
-    single_ms = (time.perf_counter() - t0) * 1e3
-    print(json.dumps({"single_gpu_ms": round(single_ms, 2), "kmers": total, "unique": u1}), flush=True)
+
+    def single(_last):
+        e.enumerate(k)
+        e.sort(k, canonical=canonical)
+        e.materialize_keys()
+        return e.unique_count_only()
+
+    single_ms, u1 = best_of(single, args.reps, e.sync)
+    print(json.dumps({"config": args.config, "scheme": args.scheme, "single_gpu_ms": round(single_ms, 2),
+                      "kmers": total, "unique": u1, "timing": f"best of {args.reps} after a warm-up"}), flush=True)
+
     for world in [int(x) for x in args.worlds.split(",")]:
         pb = D.position_ranges(len(sba), world)
-        per_rank = []
-        uniq = 0
-        kept = 0
-        stages = None
-        # the all-reduced histogram (every rank's share), outside the per-rank timings
-        full = np.zeros(256, dtype=np.int64)
-        for s in range(world):
-            h, bits = e.shard_histogram(pb[s], pb[s + 1], k, canonical=canonical)
-            full[:len(h)] += h.astype(np.int64)
-        db = D.split_buckets(full[:1 << bits], world)
-        for r in range(world):
-            best = None
-            for rep in range(args.reps + 1):  # the first one warms up
-                e.sync()
-                e.profile_enable(rep == args.reps)
-                t0 = time.perf_counter()
-                e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share of the all-reduce
-                n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
-                u = e.unique_count_only()
-                e.sync()
-                dt = time.perf_counter() - t0
-                if rep == args.reps:
-                    rep_stages = e.profile_report()
-                e.profile_enable(False)
-                if rep > 0 and (best is None or dt < best):
-                    best = dt
-            if not per_rank or best * 1e3 > max(per_rank):
+        per_rank, extra, stages, uniq, kept = [], [], None, 0, 0
+
+        def record(ms, rep_stages):
+            nonlocal stages
+            if not per_rank or ms > max(per_rank):
                 stages = {name: round(v["total_ms"], 3) for name, v in rep_stages.items()}
-            per_rank.append(round(best * 1e3, 2))
-            uniq += u
-            kept += n
+            per_rank.append(round(ms, 2))
+
+        if args.scheme == "range":
+            full = np.zeros(4096, dtype=np.int64)
+            for s in range(world):
+                h, bits = e.shard_histogram(pb[s], pb[s + 1], k, canonical=canonical)
+                full[:len(h)] += h.astype(np.int64)
+            db = D.split_buckets(full[:1 << bits], world)
+            for r in range(world):
+                def rank(last, r=r):
+                    e.profile_enable(last)
+                    e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share
+                    n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
+                    e.materialize_keys()
+                    u = e.unique_count_only()
+                    rep = e.profile_report() if last else None
+                    e.profile_enable(False)
+                    return n, u, rep
+                ms, (n, u, rep) = best_of(rank, args.reps, e.sync)
+                record(ms, rep)
+                uniq += u
+                kept += n
+        else:
+            import torch
+
+            dev = torch.device("cuda", 0)
+            sends, hists, part_ms = [], [], []
+            for r in range(world):
+                cap = pb[r + 1] - pb[r] + 64
+                sk = torch.empty(cap, dtype=torch.int64, device=dev)
+                sv = torch.empty(cap, dtype=torch.int32, device=dev)
+                ms, (hist, n) = best_of(lambda _l, r=r, sk=sk, sv=sv: e.shard_partition(
+                    pb[r], pb[r + 1], k, sk, sv, canonical=canonical), args.reps, e.sync)
+                sends.append((sk, sv))
+                hists.append(np.asarray(hist, dtype=np.int64))
+                part_ms.append(ms)
+            H = np.stack(hists)
+            bb = D.split_buckets(H.sum(axis=0), world)
+            to = np.stack([[int(H[s, bb[d]:bb[d + 1]].sum()) for d in range(world)] for s in range(world)])
+            for r in range(world):
+                parts_k, parts_v = [], []
+                for s in range(world):
+                    lo = int(H[s, :bb[r]].sum())
+                    parts_k.append(sends[s][0][lo:lo + to[s, r]])
+                    parts_v.append(sends[s][1][lo:lo + to[s, r]])
+                R = int(to[:, r].sum())
+                rk = torch.cat(parts_k + [torch.empty(64, dtype=torch.int64, device=dev)])
+                rv = torch.cat(parts_v + [torch.empty(64, dtype=torch.int32, device=dev)])
+                off, ln, bk = D.receive_pieces(H, bb[r], bb[r + 1], list(to[:, r]))
+                torch.cuda.synchronize()
+
+                def rank(last, r=r, rk=rk, rv=rv, R=R, off=off, ln=ln, bk=bk):
+                    e.profile_enable(last)
+                    e.shard_sort(rk, rv, R, k, off, ln, bk, canonical=canonical)
+                    e.materialize_keys()
+                    u = e.unique_count_only()
+                    rep = e.profile_report() if last else None
+                    e.profile_enable(False)
+                    return u, rep
+                ms, (u, rep) = best_of(rank, args.reps, e.sync)
+                peers = [d for d in range(world) if d != r]
+                x_bytes = 12 * max([int(to[r, d]) for d in peers] + [int(to[s, r]) for s in peers] + [0])
+                x_ms = x_bytes / (LINK_GBS * 1e9) * 1e3
+                extra.append({"partition_ms": round(part_ms[r], 2), "sort_ms": round(ms, 2),
+                              "exchange_link_bound_ms": round(x_ms, 2),
+                              "sent_gb": round(12 * (int(to[r].sum()) - int(to[r, r])) / 1e9, 3)})
+                record(part_ms[r] + x_ms + ms, rep)
+                uniq += u
+                kept += R
+                del rk, rv
         assert kept == total, (kept, total)  # every k-mer on exactly one rank
         worst = max(per_rank)
-        print(json.dumps({"world": world, "per_rank_ms": per_rank, "max_rank_ms": worst,
-                          "kmers_per_s": round(total / (worst * 1e-3), 1),
-                          "speedup_vs_single": round(single_ms / worst, 2), "unique": uniq,
-                          "slowest_rank_stages_ms": stages}), flush=True)
+        line = {"world": world, "per_rank_ms": per_rank, "max_rank_ms": worst,
+                "mean_rank_ms": round(float(np.mean(per_rank)), 2),
+                "kmers_per_s": round(total / (worst * 1e-3), 1),
+                "speedup_vs_single": round(single_ms / worst, 2), "unique": uniq,
+                "slowest_rank_stages_ms": stages}
+        if extra:
+            line["ranks"] = extra
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ Timed with a barrier + device synchronisation on both sides, max over ranks.
 N = 1: the genome on one MI355X.  N > 1 (torch.distributed, one rank per GPU), total work fixed,
 "scaling": "strong".  Every rank holds the whole sequence byte array (1 B per k-mer) and owns one
 contiguous range of top key digits (genome_kmers.distributed):
-  --exchange range (default): the digit ranges come from a 1 KiB all-reduce of per-rank digit
+  --exchange range (default): the digit ranges come from a 32 KiB all-reduce of per-rank 12-bit digit
       histograms; each rank re-derives its own k-mers from the whole sequence and sorts them --
       no k-mer crosses xGMI;
   --exchange a2a: each rank encodes its position share and the k-mers go to their owners in ONE
@@ -373,7 +373,7 @@ def main():
             "config": {"workload": workload,
                        "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
                        "parallelism": ("1 GPU" if dist is None else
-                                       f"key-range shards x{world}: whole sba per rank, 1 KiB RCCL all-reduce, "
+                                       f"key-range shards x{world}: whole sba per rank, 32 KiB RCCL all-reduce, "
                                        "no k-mer exchange" if args.exchange == "range" else
                                        f"position-range shards x{world} + 1 RCCL all-to-all of the k-mers"),
                        "h2d_sba_pageable_ms": round(h2d_ms, 2), "transfers": boundary,

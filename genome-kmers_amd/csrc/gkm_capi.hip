@@ -881,14 +881,18 @@ static KeySpec acgt_spec(KeySpec ks) {
     return ks;
 }
 
-// the 4-bit code of the first four symbols of the smallest ACGT k-mer with top-7-bit digit d
-// (three bases, then A or G by the digit's low bit); a range from digit 0 has no lower bound, a
-// range to digit 128 no upper one
-static uint32_t range_prefix4(uint32_t d, bool lower) {
+// the 4-bit code of the first ceil(ob / 2) symbols of the smallest ACGT k-mer with top-ob-bit
+// digit d (an odd width ends in a half symbol: A or G by the digit's low bit); a range from digit
+// 0 has no lower bound, a range to digit 1 << ob no upper one
+static uint32_t range_prefix(uint32_t d, bool lower, int ob) {
+    const int ns = (ob + 1) / 2;
     if (lower && d == 0) return 0;
-    if (d >= 128) return 0x10000u;
+    if (d >= (1u << ob)) return 1u << (4 * ns);
     static const uint32_t c4[4] = {1, 3, 5, 12};  // A C G T among '$' A B C D G H K M N R S T V W Y
-    return (c4[(d >> 5) & 3] << 12) | (c4[(d >> 3) & 3] << 8) | (c4[(d >> 1) & 3] << 4) | c4[(d & 1) ? 2 : 0];
+    const uint32_t dd = (ob & 1) ? d << 1 : d;
+    uint32_t v = 0;
+    for (int j = 0; j < ns; ++j) v = (v << 4) | c4[(dd >> (2 * (ns - 1 - j))) & 3];
+    return v;
 }
 
 extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
@@ -902,7 +906,7 @@ extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
     if (range_split(c, ks)) ks = acgt_spec(ks);  // mixed sba: digits of the ACGT-only k-mers
-    for (int i = 0; i < 256; ++i) h_hist[i] = 0;
+    for (int i = 0; i < 4096; ++i) h_hist[i] = 0;
     int b = 0;
     rc = msd_l0_histogram(c, ks, lo, std::max(hi, lo), h_hist, &b);
     *bits = (uint32_t)b;
@@ -914,7 +918,7 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     if (!c || !n_kept) return GK_E_ARG;
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
-    if (digit_lo > digit_hi || digit_hi > 256u) return fail(c, GK_E_ARG, "digit range outside [0, 256]");
+    if (digit_lo > digit_hi || digit_hi > 4096u) return fail(c, GK_E_ARG, "digit range outside [0, 4096]");
     KeySpec ks;
     int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
@@ -924,7 +928,8 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     c->starts_materialized = true;
     c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
     if (range_split(c, ks)) {  // mixed sba: ACGT-only k-mers by 2-bit digit, the rest by prefix
-        SplitRange rg{digit_lo, digit_hi, range_prefix4(digit_lo, true), range_prefix4(digit_hi, false)};
+        const int ob = range_own_bits(acgt_spec(ks));
+        SplitRange rg{digit_lo, digit_hi, range_prefix(digit_lo, true, ob), range_prefix(digit_hi, false, ob), (ob + 1) / 2};
         bool used = false;
         rc = split_sort(c, ks, &used, &rg);
         if (rc == GK_OK && !used) rc = fail(c, GK_E_HIP, "key-range split sort not applicable");

@@ -176,6 +176,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks);
 // [p4_lo, p4_hi) -- the same byte-order interval
 struct SplitRange {
     uint32_t d_lo, d_hi, p4_lo, p4_hi;
+    int pns = 4;  // symbols of the (4-bit) prefixes p4_lo / p4_hi (no upper bound: 1 << 4 pns)
 };
 int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg = nullptr);
 // multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the
@@ -190,6 +191,8 @@ int msd_radix_bits();
 // [digit_lo, digit_hi) into keys[0] / vals[0] (c->n = *n_kept)
 int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *hist, int *bits);
 int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t digit_hi, uint64_t *n_kept);
+// width of the key-range ownership digits (gk_shard_histogram's bins: 1 << width)
+int range_own_bits(const KeySpec &ks);
 // key / start buffers for n elements and `words` key words (gkm_capi.hip)
 int ensure_elems(gk_ctx *c, uint64_t n, int words);
 // key buffer b alone grown to `words` key words of elem_cap elements (contents not kept)

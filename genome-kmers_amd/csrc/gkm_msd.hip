@@ -73,14 +73,20 @@ struct L0Args {
     uint64_t lo, hi;  // k-mer starts in [lo, hi) (lo a multiple of 32: 16-B aligned tiles)
     int symbols, total_bits;
     int acgt_only;    // 2-bit keys of a mixed sba: k-mers holding a non-ACGT byte are not started
-    // key-range shard: only k-mers whose L0 digit d has d - own_lo < own_span are kept (all: 0, ~0)
+    // key-range shard: only k-mers whose ownership digit o (the top own_bits key bits) has
+    // o - own_lo < own_span are kept (all: 0, ~0)
     uint32_t own_lo = 0, own_span = 0xFFFFFFFFu;
+    int own_bits = 7;
     // 2-bit packed copy of an ACGT sba (pack2_kernel, 32 positions per word; null: pack bytes)
     const uint64_t *pk_code = nullptr;
     const uint32_t *pk_dol = nullptr;
 };
 
 __device__ __forceinline__ bool l0_owned(uint32_t d, const L0Args &a) { return d - a.own_lo < a.own_span; }
+// the ownership digit of a total_bits-bit key (own_bits <= total_bits)
+__device__ __forceinline__ bool l0_owned_key(uint64_t key, const L0Args &a) {
+    return l0_owned((uint32_t)(key >> (a.total_bits - a.own_bits)), a);
+}
 
 template <int BITS, int TILE>
 struct L0Pack {
@@ -229,21 +235,24 @@ __device__ __forceinline__ uint32_t win8_keep(const Win8 &w, const L0Args &a, Di
     const uint32_t Th = (uint32_t)(w.T >> 32);
     const bool top7 = d0.mask == 0x7Fu && (int)d0.shift == a.total_bits - 7 && a.symbols <= 56;
     uint32_t keepm = 0;
-    if (top7 && __ballot(w.D != 0 || left < 8) == 0) {
+    // ownership digits of up to 18 bits come from the same 32-bit window (2 i + own_bits <= 32)
+    const uint32_t omask = (1u << a.own_bits) - 1;
+    if (top7 && a.own_bits <= a.total_bits && a.own_bits <= 18 && __ballot(w.D != 0 || left < 8) == 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             dig[i] = (Th >> (25 - 2 * i)) & 0x7Fu;
-            keepm |= (l0_owned(dig[i], a) ? 1u : 0u) << i;
+            keepm |= (l0_owned((Th >> (32 - 2 * i - a.own_bits)) & omask, a) ? 1u : 0u) << i;
         }
         return keepm;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        dig[i] = dg_of(win8_key(w, i, a.total_bits), d0);
+        const uint64_t key = win8_key(w, i, a.total_bits);
+        dig[i] = dg_of(key, d0);
         const uint64_t Di = w.D << i;
         const bool valid = a.symbols <= 56 ? (Di == 0 || (int)__clzll((long long)Di) >= a.symbols)
                                            : l0_valid(s_dol, q0 + i, a.symbols);
-        keepm |= ((valid && i < left && l0_owned(dig[i], a)) ? 1u : 0u) << i;
+        keepm |= ((valid && i < left && l0_owned_key(key, a)) ? 1u : 0u) << i;
     }
     return keepm;
 }
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             if (STORE) win = false;
             const uint32_t anystop = tid < P::kGroups ? s_dol[tid] : 0u;
             win = win && __syncthreads_or(anystop != 0) == 0 && P0 + kSTile <= a.hi && d0.mask == 0x7Fu &&
-                  (int)d0.shift == a.total_bits - 7 && a.symbols >= 4;
+                  (int)d0.shift == a.total_bits - 7 && a.symbols >= (a.own_bits + 1) / 2 && a.own_bits <= a.total_bits;
         }
         if (BITS == 2 && win) {
             // 8 consecutive positions per thread (Win8)
@@ -557,14 +566,20 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 win8 = win8_load(s_code, s_dol, q0);
                 uint32_t dig[8];
                 keepm = win8_keep(win8, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
-            } else {  // the smaller of the forward and reverse-complement top 7 bits (msd0_count_kernel)
-                const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - 4);
+            } else {  // the smaller of the forward and reverse-complement top own_bits bits
+                // (msd0_count_kernel): the reverse complement's first ns symbols are the complement
+                // of the k-mer's last ns symbols, reversed
+                const int ob = a.own_bits, ns = (ob + 1) >> 1;
+                const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - ns);
+                const uint32_t om = (1u << ob) - 1;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    const uint32_t f7 = (uint32_t)(tf >> (57 - 2 * i)) & 0x7Fu;
-                    const uint32_t v = (uint32_t)(tr >> (56 - 2 * i)) & 0xFFu;
-                    const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
-                    keepm |= (l0_owned(min(f7, (~rv & 0xFFu) >> 1), a) ? 1u : 0u) << i;
+                    const uint32_t f = (uint32_t)(tf >> (64 - ob - 2 * i)) & om;
+                    const uint32_t v = (uint32_t)(tr >> (64 - 2 * ns - 2 * i)) & ((1u << (2 * ns)) - 1);
+                    const uint32_t r = (uint32_t)(__builtin_bitreverse64(~(uint64_t)v) >> (64 - 2 * ns));
+                    // bitreverse flips each pair's bit order too: swap the bits of every pair back
+                    const uint32_t rr = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
+                    keepm |= (l0_owned(min(f, rr >> (2 * ns - ob)), a) ? 1u : 0u) << i;
                 }
             }
             const uint32_t cnt = (uint32_t)__popc(keepm);
@@ -612,7 +627,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             for (int i = 0; i < kSI; ++i) {
                 const uint32_t p = wbase + i * 64 + lane;
                 key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
-                const bool keep = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(dg_of(key[i], d0), a);
+                const bool keep = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned_key(key[i], a);
                 const uint64_t m = __ballot(keep);
                 at[i] = kept + lanes_below(m);
                 kept += (uint32_t)__popcll(m);
@@ -634,6 +649,39 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             }
         }
     }
+}
+
+// Ownership-digit histogram of a key-range shard's position share: the top own_bits (<= 12) bits
+// of every k-mer starting in [a.lo, a.hi), one LDS table per workgroup flushed into ghist.
+template <int BITS, bool CANON>
+__global__ __launch_bounds__(kST) void own_hist_kernel(L0Args a, uint32_t ntiles, uint32_t *__restrict__ ghist) {
+    using P = L0Pack<BITS, kSTile>;
+    __shared__ uint64_t s_code[P::kCodeWords];
+    __shared__ uint32_t s_dol[P::kGroups];
+    __shared__ uint8_t s_lut4[256];
+    __shared__ uint32_t s_hist[4096];
+    const int tid = threadIdx.x;
+    if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    for (int i = tid; i < 4096; i += kST) s_hist[i] = 0;
+    const int osh = a.total_bits - a.own_bits;
+    uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
+    if (blockIdx.x < ntiles) l0_load<BITS, kSTile, kST>(a, a.lo + (uint64_t)blockIdx.x * kSTile, rr);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t P0 = a.lo + (uint64_t)t * kSTile;
+        __syncthreads();  // the LUT and the zeroed table; the previous tile's codes have been read
+        l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
+        __syncthreads();
+        if (t + gridDim.x < ntiles) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)gridDim.x * kSTile, rr);
+#pragma unroll
+        for (int i = 0; i < kSI; ++i) {
+            const uint32_t p = i * kST + tid;
+            const uint64_t key = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
+            if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi) atomicAdd(&s_hist[(uint32_t)(key >> osh)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < (1 << a.own_bits); i += kST)
+        if (s_hist[i]) atomicAdd(&ghist[i], s_hist[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2285,10 +2333,17 @@ int msd_radix_bits() { return kGR; }
 // L0 digit width of the key-range shards: 7 bits for 2-bit keys (as msd_sort), 8 otherwise
 static int range_width(const KeySpec &ks) { return ks.bits == 2 ? 7 : kGR; }
 
+// Ownership digits of the key-range shards: the ranks' ranges are cut on the top 12 bits of 2-bit
+// keys (k >= 6; 2k bits below), so a hot 7-bit L0 digit of a skewed genome is split between ranks;
+// 4-bit keys keep 8 bits.  The first partition level after the select still uses range_width.
+int range_own_bits(const KeySpec &ks) {
+    const int B = ks.bits * std::min(ks.symbols, 64 / ks.bits);
+    return ks.bits == 2 ? std::min(12, B) : std::min(kGR, B);
+}
+
 int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *hist, int *bits) {
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, 64 / ks.bits);  // the first key word (see msd_sort)
-    d.wsched[0] = range_width(ks);
     GK_TRY_HIP(c, msd_tables());
     // the packed sequence is made here for the whole sba and kept for the gk_shard_sort_range
     // that follows (one packing per key-range step)
@@ -2296,15 +2351,37 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
         int rp = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rp != GK_OK) return rp;
     }
-    uint64_t cnt = 0;
-    int rc = d.l0_count(lo, hi, 0, 0xFFFFFFFFu, &cnt);
-    if (rc != GK_OK) return rc;
-    const int R = d.width(0);
-    std::vector<uint32_t> hc(1u << R);
-    GK_TRY_HIP(c, hipMemcpyAsync(hc.data(), d.seg_cnt, 4u << R, hipMemcpyDeviceToHost, c->stream));
+    const int ob = range_own_bits(ks);
+    L0Args a{c->sba, lo, std::max(hi, lo), ks.symbols, d.B, ks.acgt_only};
+    a.own_bits = ob;
+    a.pk_code = d.pk_code;
+    a.pk_dol = d.pk_dol;
+    uint32_t *gh;
+    GK_TRY_HIP(c, scratch(c, "own_hist", 4096, &gh));
+    GK_TRY_HIP(c, hipMemsetAsync(gh, 0, 4 * 4096, c->stream));
+    const uint32_t ntiles = (uint32_t)std::max<uint64_t>((a.hi - lo + kSTile - 1) / kSTile, 1);
+    int slot;
+    timer_begin(c, "histogram", &slot);
+    timer_units(c, slot, a.hi - lo);
+#define GK_HIST(B_, C_)                                                                                        \
+    do {                                                                                                       \
+        int per_cu = 0;                                                                                        \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, own_hist_kernel<B_, C_>, kST, 0) !=          \
+                hipSuccess || per_cu < 1)                                                                      \
+            per_cu = 1;                                                                                        \
+        const unsigned g = std::min<unsigned>(ntiles, d.cus * (unsigned)per_cu);                               \
+        hipLaunchKernelGGL((own_hist_kernel<B_, C_>), dim3(g), dim3(kST), 0, c->stream, a, ntiles, gh);        \
+    } while (0)
+    if (ks.bits == 2) { if (ks.canonical) GK_HIST(2, true); else GK_HIST(2, false); }
+    else { if (ks.canonical) GK_HIST(4, true); else GK_HIST(4, false); }
+#undef GK_HIST
+    GK_TRY_HIP(c, hipGetLastError());
+    timer_end(c, slot);
+    std::vector<uint32_t> hc(1u << ob);
+    GK_TRY_HIP(c, hipMemcpyAsync(hc.data(), gh, 4u << ob, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < (1 << R); ++i) hist[i] = hc[i];
-    *bits = R;
+    for (int i = 0; i < (1 << ob); ++i) hist[i] = hc[i];
+    *bits = ob;
     return GK_OK;
 }
 
@@ -2324,6 +2401,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     L0Args a{c->sba, 0, L, ks.symbols, d.B, ks.acgt_only};
     a.own_lo = digit_lo;
     a.own_span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
+    a.own_bits = range_own_bits(ks);
     if (use_pack() && c->acgt && ks.bits == 2) {  // this step's gk_shard_histogram's packing, or pack now
         if (c->pk_fresh) {
             uint64_t *pc;

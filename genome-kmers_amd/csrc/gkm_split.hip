@@ -68,18 +68,19 @@ __device__ __forceinline__ bool window_clear(const uint32_t *m, uint32_t p, int 
 // Key-range shards (p4_lo, p4_hi != 0, 0x10000): only B k-mers whose (canonical) first four
 // symbols, as a 16-bit 4-bit code, lie in [p4_lo, p4_hi) -- the rank's byte-order interval
 // (split_sort's SplitRange).
-__device__ __forceinline__ uint32_t b_prefix4(const uint8_t *sba, uint64_t p, int k, bool hp, int canonical,
-                                              const uint8_t *lut4, const uint8_t *comp) {
+__device__ __forceinline__ uint32_t b_prefix(const uint8_t *sba, uint64_t p, int k, bool hp, int canonical,
+                                             const uint8_t *lut4, const uint8_t *comp, int ns) {
+    uint32_t v = 0;
     if (hp) {  // one letter k times; canonical: the smaller of the letter and its complement
         uint32_t ch = sba[p];
         if (canonical) ch = min(ch, (uint32_t)comp[ch]);
         const uint32_t c4 = lut4[ch];
-        return (c4 << 12) | (c4 << 8) | (c4 << 4) | c4;
+        for (int t = 0; t < ns; ++t) v = (v << 4) | c4;
+        return v;
     }
     const uint8_t *b = sba + p;
     const bool rc = canonical && canon_is_rc<4>(b, k, lut4);
-    uint32_t v = 0;
-    for (int t = 0; t < 4; ++t) v = (v << 4) | canon_sym<4>(b, k, t, rc, lut4);
+    for (int t = 0; t < ns; ++t) v = (v << 4) | canon_sym<4>(b, k, t, rc, lut4);
     return v;
 }
 
@@ -90,7 +91,7 @@ __device__ __forceinline__ uint32_t b_prefix4(const uint8_t *sba, uint64_t p, in
 // b_prefix4 lies in their interval.
 template <bool STORE>
 __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
-                                                             int canonical, uint32_t p4_lo, uint32_t p4_hi,
+                                                             int canonical, uint32_t p4_lo, uint32_t p4_hi, int pns,
                                                              uint32_t *__restrict__ cnt_r, uint32_t *__restrict__ cnt_h,
                                                              const uint32_t *__restrict__ off_r,
                                                              const uint32_t *__restrict__ off_h,
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
     __shared__ uint32_t s_w[2][4];
     s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
     s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
-    const bool ranged = p4_lo != 0 || p4_hi != 0x10000u;
+    const bool ranged = p4_lo != 0 || p4_hi != (1u << (4 * pns));
     const uint64_t P0 = (uint64_t)blockIdx.x * kFlagTile;
     for (int g = threadIdx.x; g < kFlagGroups; g += 256) {
         const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
     if (run) {
         bool keep = true;
         if (ranged) {
-            const uint32_t p4 = b_prefix4(sba, P0 + p0, k, true, canonical, s_lut4, s_comp);
+            const uint32_t p4 = b_prefix(sba, P0 + p0, k, true, canonical, s_lut4, s_comp, pns);
             keep = p4 >= p4_lo && p4 < p4_hi;
         }
         if (keep) mh = 0xFFFFFFFFu;
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
             if (!f) continue;
             const bool hp = k == 1 || window_clear(s_diff, p, k - 1);
             if (ranged) {
-                const uint32_t p4 = b_prefix4(sba, P0 + p, k, hp, canonical, s_lut4, s_comp);
+                const uint32_t p4 = b_prefix(sba, P0 + p, k, hp, canonical, s_lut4, s_comp, pns);
                 if (p4 < p4_lo || p4 >= p4_hi) continue;
             }
             if (hp) mh |= 1u << j;
@@ -388,7 +389,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     const uint64_t n = rg ? L : c->n;  // key-range shards: the k-mer count is not known yet (<= L)
     const int k = ks.symbols;
     if (k > 64 || ks.bits != 4 || ks.lenbits || ks.symbols != ks.min_len) return GK_OK;
-    if (rg && k < 4) return fail(c, GK_E_ARG, "split: key-range shards need k >= 4");
+    if (rg && k < rg->pns) return fail(c, GK_E_ARG, "split: key-range shards need k >= the prefix length");
     GK_TRY_HIP(c, split_tables());
     c->split_keys_final = false;
     // final keys: with one-word 2-bit class-A keys (k <= 32) the sorted order leaves with its W-word
@@ -403,10 +404,11 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, scratch(c, "split_cnt_h", ftiles + 1, &chh));
     GK_TRY_HIP(c, scratch(c, "split_off_r", ftiles + 1, &orr));
     GK_TRY_HIP(c, scratch(c, "split_off_h", ftiles + 1, &ohh));
-    const uint32_t p4_lo = rg ? rg->p4_lo : 0u, p4_hi = rg ? rg->p4_hi : 0x10000u;
+    const int pns = rg ? rg->pns : 4;
+    const uint32_t p4_lo = rg ? rg->p4_lo : 0u, p4_hi = rg ? rg->p4_hi : (1u << (4 * pns));
     timer_begin(c, "split_b_select", &slot);
     hipLaunchKernelGGL(class_b_select_kernel<false>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
-                       ks.canonical, p4_lo, p4_hi, cr, chh, nullptr, nullptr, nullptr, nullptr);
+                       ks.canonical, p4_lo, p4_hi, pns, cr, chh, nullptr, nullptr, nullptr, nullptr);
     GK_TRY_HIP(c, hipGetLastError());
     uint64_t nR = 0, nH = 0;
     GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cr, ftiles, orr, &nR));
@@ -414,7 +416,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &b_st[0]));
     GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &h_st));
     hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
-                       ks.canonical, p4_lo, p4_hi, nullptr, nullptr, orr, ohh, b_st[0], h_st);
+                       ks.canonical, p4_lo, p4_hi, pns, nullptr, nullptr, orr, ohh, b_st[0], h_st);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     const uint64_t nB = nR + nH;

@@ -400,7 +400,7 @@ class Engine:
 
     def shard_histogram(self, lo: int, hi: int, k: int, canonical: bool = False):
         """Top-digit histogram of the k-mers starting in [lo, hi): (numpy uint64[1 << bits], bits)."""
-        hist = np.zeros(256, dtype=np.uint64)
+        hist = np.zeros(4096, dtype=np.uint64)
         bits = ctypes.c_uint32(0)
         self._check(self.lib.gk_shard_histogram(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
                                                 _ptr(hist, ctypes.c_uint64), ctypes.byref(bits)))

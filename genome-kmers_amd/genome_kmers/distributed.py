@@ -7,7 +7,7 @@ are ``Kmers.sort``'s order with ``break_ties=True`` (kmers.py:1710-1711) -- the 
 and unique counts stay local (equal keys share a digit).  Two drivers:
 
 ``KeyRangeKmerSort`` (default): no k-mer moves between GPUs.  Histograms of the rank's position
-share are all-reduced (1 KiB), the digits are cut into ranges of about n/N k-mers, and each rank
+share are all-reduced (4096 12-bit ownership digits, 32 KiB), the digits are cut into ranges of about n/N k-mers, and each rank
 selects its k-mers from the whole resident sequence and sorts them.
 
 ``ShardedKmerSort`` (all-to-all):
@@ -200,7 +200,7 @@ class KeyRangeKmerSort:
     moving k-mers to their owner, each rank re-derives its own from the sequence:
 
     1. ``shard_histogram``: top-digit histogram of the k-mers starting in the rank's position share;
-    2. ``all_reduce`` (sum) of the histograms -- 1 KiB, the only collective -- and the same split of
+    2. ``all_reduce`` (sum) of the 4096-digit histograms -- 32 KiB, the only collective -- and the same split of
        the digits into N contiguous ranges of about n/N k-mers on every rank (``split_buckets``);
     3. ``shard_sort_range``: the rank scans the whole sequence, keeps the k-mers of its digit range
        (compacted per wave before ranking, so the kept share sets the cost) and sorts them.

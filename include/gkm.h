@@ -203,11 +203,13 @@ int gk_shard_sort(gk_ctx *ctx, const uint64_t *d_keys, const uint32_t *d_starts,
  * sorts them, so the ranks' outputs concatenated in rank order are the single-GPU gk_sort order
  * (kmers.py:1624-1652 with break_ties=True, kmers.py:1710-1711).  Replaces the same reference call
  * as gk_sort; the reference has no multi-process path.
- * gk_shard_histogram: histogram of the top *bits key bits (h_hist[256], entries >= 1 << *bits are
- * 0) of the fixed-length k-mers starting in [lo, hi) (lo a multiple of 32) -- each rank counts its
- * position share, the caller sums the histograms over ranks (a 2 KiB all-reduce) and cuts the
- * digits into contiguous ranges of about n / N k-mers.
- * gk_shard_sort_range: sort every k-mer of the sba whose top digit d has digit_lo <= d < digit_hi;
+ * gk_shard_histogram: histogram of the ownership digits -- the top *bits key bits, 12 for 2-bit
+ * keys (k >= 6), 8 for 4-bit keys -- (h_hist[4096], entries >= 1 << *bits are 0) of the
+ * fixed-length k-mers starting in [lo, hi) (lo a multiple of 32); on a mixed sba the digits of
+ * the ACGT-only k-mers.  Each rank counts its position share, the caller sums the histograms over
+ * ranks (an all-reduce of 1 << *bits counts, 32 KiB as int64) and cuts the digits into contiguous
+ * ranges of about n / N k-mers: 4096 digits let a hot digit of a skewed genome be split finely.
+ * gk_shard_sort_range: sort every k-mer of the sba whose ownership digit d has digit_lo <= d < digit_hi;
  * *n_kept receives their number and the context then holds them as after gk_sort(k).
  */
 int gk_shard_histogram(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,

@@ -87,8 +87,8 @@ class NumpyShardEngine:
         order = np.argsort(key, kind="stable")  # the device sort is stable in piece order
         self.keys, self.starts = key[order], st[order]
 
-    # key-range contract (gk_shard_histogram / gk_shard_sort_range): 7-bit top digits of 2-bit keys
-    range_bits = 7
+    # key-range contract (gk_shard_histogram / gk_shard_sort_range): 12-bit top digits of 2-bit keys
+    range_bits = 12
 
     def _top(self, key, k):
         return (key >> np.uint64(max(0, 2 * k - self.range_bits))).astype(np.int64)
@@ -296,7 +296,7 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     for r in range(world):
         h, bits = e.shard_histogram(bounds[r], bounds[r + 1], k, canonical=canonical)
         hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
-    assert bits == 7  # mixed sba: digits of the ACGT-only k-mers (split sort)
+    assert bits == min(12, 2 * k)  # ownership digits: the top 12 bits of the (ACGT-only k-mers') 2-bit keys
     total = D.count_kmers(len(sba), seg, k)
     if iupac:  # the digits count the ACGT-only k-mers; the others follow their byte-order interval
         assert 0 < int(hist.sum()) < total

@@ -385,7 +385,9 @@ __global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const
 }
 
 // software-pipelined L0 (see msd_pipe_kernel): the previous tile's stores overlap this tile's
-// packing, key extraction and ranking; the next tile's bytes are loaded after the staging
+// packing, key extraction and ranking; the next tile's bytes are loaded as soon as this tile's
+// are packed (one workgroup per CU: loaded after the staging, every tile waited a full HBM
+// latency at the top of the loop)
 template <int BITS, int T, int I, int R, bool ND, bool CANON = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
@@ -428,6 +430,9 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
         if (tid < RADIX) s_toff[cur][tid] = toff;
         l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
+        // rr and toff are consumed: the next tile's bytes fly during this whole tile (the last
+        // tile re-loads itself, so every iteration issues the same loads: static wait counts)
+        load(min(t + walk.step, walk.end - 1));
         const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
         for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
@@ -496,7 +501,6 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         }
         pcnt = s_start[RADIX];
         lds_barrier();  // staging complete; counters and codes read
-        if (t + walk.step < walk.end) load(t + walk.step);
         cur ^= 1;
     }
     if (walk.first < walk.end) {
@@ -521,12 +525,18 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
 constexpr int kST = 512, kSI = 8, kSTile = kST * kSI;  // 4096 positions per tile, 512 per wave
 constexpr int kSW = kST / 64;                          // waves per tile
 
-template <int BITS, bool CANON, bool STORE>
-__global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint32_t ntiles,
+// MODE 0 / 1 are the two passes above.  MODE 2 is a single pass: workgroup w walks its own chunk of
+// tpw consecutive tiles and appends its kept k-mers at a running offset into its own region of
+// the output, [t0 * kSTile, (t0 + tpw) * kSTile) (room for every position of the chunk, so no
+// count pass is needed); wave_cnt[w] receives the chunk's kept count.  The regions, in workgroup
+// order, are the pieces of one bucket in position order (first_level_from_pieces).
+template <int BITS, bool CANON, int MODE>
+__global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint32_t ntiles, uint32_t tpw,
                                                           uint32_t *__restrict__ wave_cnt,
                                                           const uint32_t *__restrict__ wave_off,
                                                           uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                           uint8_t *__restrict__ nd_out) {
+    constexpr bool STORE = MODE != 0;
     using P = L0Pack<BITS, kSTile>;
     constexpr int kStage = STORE ? kSTile : 1;  // per-wave staging of the kept (key, start): 512 each
     __shared__ uint64_t s_code[P::kCodeWords];
@@ -534,21 +544,44 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
     __shared__ uint8_t s_lut4[256];
     __shared__ uint64_t s_skey[kStage];
     __shared__ uint32_t s_sval[kStage];
+    __shared__ uint32_t s_wtot[kSW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    // tiles of this workgroup: a strided walk (MODE 0 / 1) or a chunk (MODE 2)
+    const uint32_t tfirst = MODE == 2 ? blockIdx.x * tpw : blockIdx.x;
+    const uint32_t tend = MODE == 2 ? min(tfirst + tpw, ntiles) : ntiles;
+    const uint32_t tstep = MODE == 2 ? 1u : gridDim.x;
+    const uint64_t region = (uint64_t)tfirst * kSTile;  // MODE 2: this chunk's output region
+    uint64_t run = 0;                                   // MODE 2: kept so far in the chunk
     uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
-    if (blockIdx.x < ntiles) l0_load<BITS, kSTile, kST>(a, a.lo + (uint64_t)blockIdx.x * kSTile, rr);
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    if (tfirst < tend) l0_load<BITS, kSTile, kST>(a, a.lo + (uint64_t)tfirst * kSTile, rr);
+    for (uint32_t t = tfirst; t < tend; t += tstep) {
         const uint64_t wslot = (uint64_t)t * kSW + wave;
         const uint64_t P0 = a.lo + (uint64_t)t * kSTile;
-        __syncthreads();  // the LUT; the previous tile's codes have been read
+        __syncthreads();  // the LUT; the previous tile's codes and wave totals have been read
         l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         __syncthreads();
         // the next tile's bytes fly while this one is processed
-        if (t + gridDim.x < ntiles) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)gridDim.x * kSTile, rr);
+        if (t + tstep < tend) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)tstep * kSTile, rr);
+        // MODE 2: the wave's output offset from the kept counts of the tile's waves (block-uniform
+        // call: both paths below reach it)
+        auto chunk_offset = [&](uint32_t wcount) -> uint64_t {
+            if (lane == 0) s_wtot[wave] = wcount;
+            __syncthreads();
+            uint32_t pre = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kSW; ++w) {
+                const uint32_t v = s_wtot[w];
+                pre += w < wave ? v : 0u;
+                tot += v;
+            }
+            const uint64_t o = region + run + pre;
+            run += tot;
+            return o;
+        };
         bool win = BITS == 2;
         // canonical: the count pass takes the digits from windows in a tile without stops; the store
-        // pass keeps the row layout below (a per-lane loop over the kept positions' canonical keys
+        // passes keep the row layout below (a per-lane loop over the kept positions' canonical keys
         // was slower: 11.9 against 8.3 ms per C5 rank at N = 8).  Both visit a wave's 512 positions
         // in position order, so their per-wave counts and offsets agree.
         if constexpr (BITS == 2 && CANON) {
@@ -589,10 +622,12 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 const uint32_t y = __shfl_up(incl, off);
                 if (lane >= off) incl += y;
             }
+            const uint32_t total = __shfl(incl, 63);
             if (!STORE) {
                 if (lane == 63) wave_cnt[wslot] = incl;
                 continue;
             }
+            const uint64_t o = MODE == 2 ? chunk_offset(total) : (uint64_t)wave_off[wslot];
             // stage the wave's kept k-mers in position order (keys only for them), then store them
             // as one coalesced run
             uint64_t *sk = s_skey + wave * 512;
@@ -604,11 +639,9 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 sv[j] = (uint32_t)(P0 + q0 + i);
                 ++j;
             }
-            const uint32_t total = __shfl(incl, 63);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-            const uint64_t o = wave_off[wslot];
             for (uint32_t e = lane; e < total; e += 64) {
                 const uint64_t k = sk[e];
                 kout[o + e] = k;
@@ -637,7 +670,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 if (lane == 0) wave_cnt[wslot] = kept;
                 continue;
             }
-            const uint64_t base = wave_off[wslot];
+            const uint64_t base = MODE == 2 ? chunk_offset(kept) : (uint64_t)wave_off[wslot];
 #pragma unroll
             for (int i = 0; i < kSI; ++i) {
                 if ((keepm >> i) & 1u) {
@@ -649,6 +682,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
             }
         }
     }
+    if (MODE == 2 && tid == 0 && blockIdx.x * tpw < ntiles) wave_cnt[blockIdx.x] = (uint32_t)run;
 }
 
 // Ownership-digit histogram of a key-range shard's position share: the top own_bits (<= 12) bits
@@ -1619,6 +1653,19 @@ static unsigned cu_count(gk_ctx *c) {
 
 // Packing is opt-in (GKM_PACK=1): measured on MI355X, the L0 partition got slower reading packed
 // words (17.8 vs 16.4 ms at C3) and the key-range passes gained less than the 0.8 ms packing costs.
+// tuning only (A/B runs): GKM_SELECT_2PASS=1 selects a key-range shard's k-mers by a count pass,
+// a scan and a store pass (the single chunked pass is the default)
+static bool select_two_pass() {
+    static const bool v = std::getenv("GKM_SELECT_2PASS") != nullptr;
+    return v;
+}
+
+// tuning only (A/B runs): GKM_WAVE_OCC=4 runs the 8-key wave class at 4 waves per SIMD
+static int wave_occ() {
+    static const int v = std::getenv("GKM_WAVE_OCC") ? std::atoi(std::getenv("GKM_WAVE_OCC")) : 5;
+    return v;
+}
+
 static bool use_pack() {
     static const bool on = std::getenv("GKM_PACK") != nullptr;
     return on;
@@ -1984,8 +2031,10 @@ struct MsdDriver {
 
     // first level from received buckets: pieces (off, len) of kin / vin, grouped by top-kGR-bit
     // bucket in ascending bucket order, pieces of a bucket in the order their elements must keep
+    // level / hi: the level the pieces are partitioned at and the key bits already sorted (the
+    // exchange's pieces: level 1 after kGR bits; the key-range select's chunks: level 0, no bits)
     int first_level_from_pieces(const uint64_t *kin, const uint32_t *vin, const uint64_t *poff, const uint64_t *plen,
-                                const uint32_t *pbucket, uint32_t np) {
+                                const uint32_t *pbucket, uint32_t np, int level = 1, int hi = kGR) {
         std::vector<uint32_t> ts, tc, cf, cn, scf, snc, sst;
         uint64_t out_base = 0;
         for (uint32_t i = 0; i < np;) {
@@ -2033,10 +2082,10 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemcpyAsync(s_st, sst.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         big_elems = n;
-        rc = level_pass(1, kGR, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
+        rc = level_pass(level, hi, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
         if (rc != GK_OK) return rc;
         cur_big = 0;
-        return classify(nseg << width(1), kGR + width(1), 0, cur_big);
+        return classify(nseg << width(level), hi + width(level), 0, cur_big);
     }
 
     // Multi-word keys, phase > 0: the head flags of the order so far (buffer 0) mark the groups of
@@ -2165,8 +2214,12 @@ struct MsdDriver {
             break;
         case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
                  // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
-            hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+            if (wave_occ() == 4)
+                hipLaunchKernelGGL((msd_wave_kernel<8, 4>), grid((const void *)msd_wave_kernel<8, 4>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+            else
+                hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
             break;
         case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
                  // on C5 (A/B, one box)
@@ -2418,51 +2471,90 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         c->pk_fresh = false;
     }
     const Dig d0 = dig_at(d.B, 0, d.width(0));
+    const bool two_pass = select_two_pass();
     uint32_t *wave_cnt, *wave_off;
     GK_TRY_HIP(c, scratch(c, "sel_wave_cnt", nw + 1, &wave_cnt));
     GK_TRY_HIP(c, scratch(c, "sel_wave_off", nw + 1, &wave_off));
     c->n = 0;  // nothing in the buffers survives: ensure_elems copies none
     c->cur = 0;
-    auto launch = [&](bool store) {
-        uint64_t *ko = store ? c->keys[0] : nullptr;
-        uint32_t *vo = store ? c->vals[0] : nullptr;
-        uint8_t *no = store ? d.nd : nullptr;
+    // single pass: chunks of tpw tiles per workgroup, one region of tpw * kSTile elements each in
+    // keys[1] / vals[1] (room for every position: no count pass)
+    uint32_t tpw = 1, nchunk = 0;
+    auto launch = [&](int mode) {
+        uint64_t *ko = mode ? c->keys[mode == 2 ? 1 : 0] : nullptr;
+        uint32_t *vo = mode ? c->vals[mode == 2 ? 1 : 0] : nullptr;
+        uint8_t *no = mode ? d.nd : nullptr;
         // persistent grid = the workgroups that fit at once (a second round of workgroups would
         // start only when the first ones have walked all their tiles)
-#define GK_SEL(B_, C_, S_)                                                                                    \
+#define GK_SEL(B_, C_, M_)                                                                                    \
     do {                                                                                                      \
         int per_cu = 0;                                                                                       \
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, msd0_select_kernel<B_, C_, S_>, kST, 0) !=  \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, msd0_select_kernel<B_, C_, M_>, kST, 0) !=  \
                 hipSuccess ||                                                                                 \
             per_cu < 1)                                                                                       \
             per_cu = 1;                                                                                       \
-        const unsigned sgrid = std::min<unsigned>(ntiles, d.cus * (unsigned)per_cu);                          \
-        hipLaunchKernelGGL((msd0_select_kernel<B_, C_, S_>), dim3(sgrid), dim3(kST), 0, c->stream, a, d0,     \
-                           ntiles, wave_cnt, wave_off, ko, vo, no);                                           \
+        unsigned sgrid = std::min<unsigned>(ntiles, d.cus * (unsigned)per_cu);                                \
+        if (M_ == 2) {                                                                                        \
+            tpw = (ntiles + sgrid - 1) / sgrid;                                                               \
+            sgrid = nchunk = (ntiles + tpw - 1) / tpw;                                                        \
+        }                                                                                                     \
+        hipLaunchKernelGGL((msd0_select_kernel<B_, C_, M_>), dim3(sgrid), dim3(kST), 0, c->stream, a, d0,     \
+                           ntiles, tpw, wave_cnt, wave_off, ko, vo, no);                                      \
     } while (0)
-        if (ks.bits == 2 && ks.canonical) { if (store) GK_SEL(2, true, true); else GK_SEL(2, true, false); }
-        else if (ks.bits == 2) { if (store) GK_SEL(2, false, true); else GK_SEL(2, false, false); }
-        else if (ks.canonical) { if (store) GK_SEL(4, true, true); else GK_SEL(4, true, false); }
-        else { if (store) GK_SEL(4, false, true); else GK_SEL(4, false, false); }
+#define GK_SEL_M(B_, C_)                                                                                      \
+    do {                                                                                                      \
+        if (mode == 0) GK_SEL(B_, C_, 0);                                                                     \
+        else if (mode == 1) GK_SEL(B_, C_, 1);                                                                \
+        else GK_SEL(B_, C_, 2);                                                                               \
+    } while (0)
+        if (ks.bits == 2 && ks.canonical) GK_SEL_M(2, true);
+        else if (ks.bits == 2) GK_SEL_M(2, false);
+        else if (ks.canonical) GK_SEL_M(4, true);
+        else GK_SEL_M(4, false);
+#undef GK_SEL_M
 #undef GK_SEL
     };
     int slot;
-    timer_begin(c, "msd_select_count", &slot);
-    timer_units(c, slot, L);
-    launch(false);
-    GK_TRY_HIP(c, hipGetLastError());
     uint64_t found = 0;
-    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, wave_cnt, nw, wave_off, &found));
-    timer_end(c, slot);
-    if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
-    int rc = ensure_elems(c, std::max<uint64_t>(found, 1), 1);
-    if (rc != GK_OK) return rc;
-    GK_TRY_HIP(c, scratch(c, "msd_nd", found + 64, &d.nd));
-    timer_begin(c, "msd_select", &slot);
-    timer_units(c, slot, found);
-    launch(true);
-    GK_TRY_HIP(c, hipGetLastError());
-    timer_end(c, slot);
+    std::vector<uint64_t> poff, plen;
+    if (two_pass) {
+        timer_begin(c, "msd_select_count", &slot);
+        timer_units(c, slot, L);
+        launch(0);
+        GK_TRY_HIP(c, hipGetLastError());
+        GK_TRY_HIP(c, scan_u32_exclusive_pub(c, wave_cnt, nw, wave_off, &found));
+        timer_end(c, slot);
+        if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
+        int rc = ensure_elems(c, std::max<uint64_t>(found, 1), 1);
+        if (rc != GK_OK) return rc;
+        GK_TRY_HIP(c, scratch(c, "msd_nd", found + 64, &d.nd));
+        timer_begin(c, "msd_select", &slot);
+        timer_units(c, slot, found);
+        launch(1);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+    } else {
+        const uint64_t cap = (uint64_t)ntiles * kSTile;  // every chunk region is full-size
+        if (cap > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "sequence too long for uint32 start indices");
+        int rc = ensure_elems(c, cap, 1);
+        if (rc != GK_OK) return rc;
+        GK_TRY_HIP(c, scratch(c, "msd_nd", cap + 64, &d.nd));
+        timer_begin(c, "msd_select", &slot);
+        timer_units(c, slot, L);
+        launch(2);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        std::vector<uint32_t> kc(nchunk);
+        GK_TRY_HIP(c, hipMemcpyAsync(kc.data(), wave_cnt, 4 * (uint64_t)nchunk, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint32_t w = 0; w < nchunk; ++w) {
+            if (!kc[w]) continue;
+            poff.push_back((uint64_t)w * tpw * kSTile);
+            plen.push_back(kc[w]);
+            found += kc[w];
+        }
+        if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
+    }
     *n_kept = found;
     c->n = found;
     if (found == 0) {
@@ -2470,17 +2562,26 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         return GK_OK;
     }
     uint8_t *nd_keep = d.nd;
-    rc = d.init(found);
+    int rc = d.init(found);
     if (rc != GK_OK) return rc;
     d.nd = nd_keep;
     d.nd_ready = true;  // the select wrote the L0 digit bytes
-    // the kept k-mers as one bucket [0, found) with no key bits sorted
-    uint32_t *one;
-    GK_TRY_HIP(c, scratch(c, "sel_bucket", 2, &one));
-    const uint32_t hb[2] = {0, (uint32_t)found};
-    GK_TRY_HIP(c, hipMemcpyAsync(one, hb, 8, hipMemcpyHostToDevice, c->stream));
-    rc = d.classify(1, 0, 0, 0, one, one + 1);
-    if (rc == GK_OK) rc = d.levels(0, 0, 0);
+    if (two_pass) {
+        // the kept k-mers as one bucket [0, found) with no key bits sorted
+        uint32_t *one;
+        GK_TRY_HIP(c, scratch(c, "sel_bucket", 2, &one));
+        const uint32_t hb[2] = {0, (uint32_t)found};
+        GK_TRY_HIP(c, hipMemcpyAsync(one, hb, 8, hipMemcpyHostToDevice, c->stream));
+        rc = d.classify(1, 0, 0, 0, one, one + 1);
+        if (rc == GK_OK) rc = d.levels(0, 0, 0);
+    } else {
+        // the chunks' regions of keys[1] / vals[1] are the pieces of one bucket, in position order;
+        // the first level partitions them into [0, found) of keys[0] / vals[0]
+        const std::vector<uint32_t> pb(poff.size(), 0u);
+        rc = d.first_level_from_pieces(c->keys[1], c->vals[1], poff.data(), plen.data(), pb.data(),
+                                       (uint32_t)poff.size(), 0, 0);
+        if (rc == GK_OK) rc = d.levels(1, d.width(0), 0);
+    }
     if (rc == GK_OK) rc = d.finish();
     for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
         rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));

@@ -1196,8 +1196,18 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
     __shared__ uint32_t s_cnt[257];  // digit counts, then exclusive starts (s_cnt[256] = total)
     const int lane = threadIdx.x;
     const uint64_t me_bit = 1ull << lane;
-    uint32_t idx = blockIdx.x;
-    if (idx >= count) return;
+    // XCD-aware walk (grid a multiple of 8): workgroup b takes the (b % 8)-th eighth of the list,
+    // so the list's neighbouring buckets -- neighbours in memory, since classify appends a level's
+    // sub-buckets in runs of address order -- are finished at about the same time on one XCD and
+    // share the L2 lines at their edges; other grids walk the list with the plain stride
+    uint32_t idx = blockIdx.x, lend = count, lstep = gridDim.x;
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+        const uint32_t x = blockIdx.x & 7;
+        idx = (uint32_t)((uint64_t)count * x / 8) + (blockIdx.x >> 3);
+        lend = (uint32_t)((uint64_t)count * (x + 1) / 8);
+        lstep = gridDim.x >> 3;
+    }
+    if (idx >= lend) return;
 #pragma unroll
     for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;
     uint2 e = list[idx];
@@ -1205,7 +1215,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
     uint32_t val[I];
     local_load<64, I>(e, k0, v0, k1, v1, key, val);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    for (; idx < count; idx += gridDim.x) {
+    for (; idx < lend; idx += lstep) {
         const uint2 ce = e;
         const uint64_t st = ce.x;
         const uint32_t len = ce.y >> 8;
@@ -1221,7 +1231,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
         const Dig dd = dig_at(B, hi, 8);
         const int nhi = hi + 8;
         const bool last = nhi >= B;
-        if (idx + gridDim.x < count) e = list[idx + gridDim.x];
+        if (idx + lstep < lend) e = list[idx + lstep];
         const int live = min(I, (int)((len + 63) >> 6));
 
 #pragma unroll
@@ -1657,6 +1667,13 @@ static unsigned cu_count(gk_ctx *c) {
 // a scan and a store pass (the single chunked pass is the default)
 static bool select_two_pass() {
     static const bool v = std::getenv("GKM_SELECT_2PASS") != nullptr;
+    return v;
+}
+
+// tuning only (A/B runs): GKM_XCD_WALK_OFF=1 gives the wave kernels a grid that is not a multiple
+// of 8 (plain strided walk of the bucket list)
+static bool xcd_walk_off() {
+    static const bool v = std::getenv("GKM_XCD_WALK_OFF") != nullptr;
     return v;
 }
 
@@ -2205,7 +2222,9 @@ struct MsdDriver {
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess || per_cu < 1)
                 per_cu = 1;
-            return dim3((unsigned)std::min<uint64_t>(cnt, (uint64_t)cus * per_cu));
+            uint64_t g = std::min<uint64_t>(cnt, (uint64_t)cus * per_cu);
+            if (g >= 8) g = xcd_walk_off() ? g - ((g & 7) == 0) : (g & ~7ull);  // the wave kernels' XCD-aware walk
+            return dim3((unsigned)g);
         };
         switch (k) {
         case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)

@@ -80,6 +80,9 @@ struct L0Args {
     // 2-bit packed copy of an ACGT sba (pack2_kernel, 32 positions per word; null: pack bytes)
     const uint64_t *pk_code = nullptr;
     const uint32_t *pk_dol = nullptr;
+    // timing builds only (GKM_L0_PROF): per-phase clock sums of the L0 partition's first and last
+    // wave of every workgroup
+    unsigned long long *prof = nullptr;
 };
 
 __device__ __forceinline__ bool l0_owned(uint32_t d, const L0Args &a) { return d - a.own_lo < a.own_span; }
@@ -106,15 +109,19 @@ template <int BITS, int TILE, int T>
 __device__ __forceinline__ void l0_load(const L0Args &a, uint64_t P0, uint64_t (&r)[L0Units<BITS, TILE, T>::kPer]) {
     using U = L0Units<BITS, TILE, T>;
     static_assert(U::kPer >= 2, "the packed path keeps a code word and a stop word");
+    // every element of r is written on both paths (a path that leaves some unwritten made the
+    // compiler keep r in scratch memory at kPer = 3)
     if (BITS == 2 && a.pk_code) {  // pre-packed: thread g < kGroups holds group g's words
         const uint64_t g = (P0 >> 5) + min((uint32_t)threadIdx.x, (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
         r[0] = a.pk_code[g];
         r[1] = a.pk_dol[g];
-        return;
-    }
-    const uint64_t *s8 = reinterpret_cast<const uint64_t *>(a.sba + P0);
 #pragma unroll
-    for (int j = 0; j < U::kPer; ++j) r[j] = s8[min((uint32_t)(threadIdx.x + j * T), (uint32_t)U::kUnits - 1)];
+        for (int j = 2; j < U::kPer; ++j) r[j] = 0;
+    } else {
+        const uint64_t *s8 = reinterpret_cast<const uint64_t *>(a.sba + P0);
+#pragma unroll
+        for (int j = 0; j < U::kPer; ++j) r[j] = s8[min((uint32_t)(threadIdx.x + j * T), (uint32_t)U::kUnits - 1)];
+    }
 }
 
 // 2-bit codes (A0 C1 G2 T3) of 8 bytes as 16 bits, position 0 in the most significant pair
@@ -329,88 +336,47 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     }
 }
 
-// persistent (see msd_scatter_kernel): the next tile's bytes are loaded while runs are stored
-template <int BITS, int T, int I, int R>
-__global__ __launch_bounds__(T) void msd0_scatter_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
-                                                         uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                         uint32_t ntiles, uint64_t sink) {
-    constexpr int TILE = T * I;
-    using P = L0Pack<BITS, TILE>;
-    using SM = PartSmem<T, I, R>;
-    constexpr int RADIX = SM::kRadix;
-    __shared__ __attribute__((aligned(16))) unsigned char s_raw[SM::kUnion];
-    __shared__ uint64_t s_code[P::kCodeWords];
-    __shared__ uint32_t s_dol[P::kGroups];
-    __shared__ uint32_t s_toff[RADIX];
-    __shared__ uint32_t s_wsum[SM::kWaves];
-    __shared__ uint32_t s_start[RADIX + 1];
-    __shared__ uint8_t s_lut4[256];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
-    if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
-    lds_barrier();  // the LUT, read by every thread's pack
-    const TileWalk walk(ntiles);
-    uint64_t rr[L0Units<BITS, TILE, T>::kPer];
-    uint32_t toff = 0;
-    auto load = [&](uint32_t t) {
-        l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)t * TILE, rr);
-        toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];  // every lane loads: no branch
-    };
-    if (walk.first < walk.end) load(walk.first);
-    __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see msd_scatter_kernel
-    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
-        lds_barrier();  // the previous tile's runs have been read out of LDS
-        for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
-        if (tid < RADIX) s_toff[tid] = toff;
-        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
-        lds_barrier();
-        const uint64_t P0 = a.lo + (uint64_t)t * TILE;
-        uint64_t key[I];
-        uint32_t val[I], slot[I];
-        bool valid[I];
-        uint32_t p0 = wave * (I * 64) + lane;
-        asm volatile("" : "+v"(p0));  // keep the per-item offsets inside the loop (no hoisting)
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            const uint32_t p = p0 + i * 64;
-            valid[i] = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi;
-            key[i] = l0_key<BITS>(s_code, p, a.total_bits);
-            val[i] = (uint32_t)(P0 + p);
-        }
-        partition_stage<T, I, R>(key, val, valid, d0, s_raw, s_toff, s_wsum, s_start, slot);
-        const uint32_t cnt = s_start[RADIX];
-        if (t + walk.step < walk.end) load(t + walk.step);
-        partition_store<T, I, R, 0>(d0, s_raw, s_toff, cnt, sink, kout, vout);
-    }
-}
+// L0 partition, software-pipelined with position staging.  The L0 input is the packed tile
+// itself, so a staged element needs only its tile position (u16): its key is re-derived from the
+// tile's codes when it is stored, and its start is the tile base + position.  Positions and codes
+// are double-buffered (2 x (45 + 6) KB at 22,528 positions), so the previous tile's stores are
+// spread over EVERY phase of this tile -- packing, ranking, scan, staging -- and the memory pipe
+// never idles (staged as (key, start) in one 135 KB buffer, the stores had to finish before the
+// staging: a phase profile (GKM_L0_PROF) showed them issued in 45 % of the tile time, backed up,
+// and the pipe idle for the rest).  Twice the tile of the level passes: runs of ~176 per digit.
+// PROF (timing builds, GKM_L0_PROF): the first and the last wave of each workgroup add the clock
+// ticks of every phase of the tile loop to a.prof[wave != 0][phase]
+constexpr int kL0Phases = 9;
+constexpr int kP0I = 18;                 // L0 tile: kPT threads x kP0I positions
+constexpr int kP0Tile = kPT * kP0I;      // 22,528 (< 65,536: positions staged as u16)
 
-// software-pipelined L0 (see msd_pipe_kernel): the previous tile's stores overlap this tile's
-// packing, key extraction and ranking; the next tile's bytes are loaded as soon as this tile's
-// are packed (one workgroup per CU: loaded after the staging, every tile waited a full HBM
-// latency at the top of the loop)
-template <int BITS, int T, int I, int R, bool ND, bool CANON = false>
+template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t ntiles, uint64_t sink, NextDigits nd) {
     constexpr int TILE = T * I;
+    static_assert(TILE < 65536, "tile positions are staged as u16");
     constexpr int RADIX = 1 << R;
     constexpr int NW = T / 64;
-    constexpr int PRE = (I + 2) / 3;
+    // store groups of the previous tile: 2 after the packing, one per ranked item, 2 during the
+    // scan, the rest after the staging
+    constexpr int G_TOP = 2, G_SCAN = 2;
+    constexpr int G_RANK = I - G_TOP - G_SCAN - 2 > 0 ? I - G_TOP - G_SCAN - 2 : 0;
     using P = L0Pack<BITS, TILE>;
-    using SM = PipeSmem<T, I>;
     static_assert(T >= RADIX, "one thread per digit");
-    __shared__ __attribute__((aligned(16))) unsigned char s_stage[SM::kStage];
-    __shared__ uint32_t s_wc[NW * RADIX];
-    __shared__ uint64_t s_code[P::kCodeWords];
+    __shared__ uint16_t s_pos[2][TILE + 2];          // positions in digit order (slot TILE: sink)
+    __shared__ uint64_t s_code[2][P::kCodeWords];   // this tile's and the staged tile's codes
     __shared__ uint32_t s_dol[P::kGroups];
+    __shared__ uint32_t s_wc[NW * RADIX];
     __shared__ uint32_t s_toff[2][RADIX];
     __shared__ uint32_t s_start[RADIX + 1];
-    __shared__ uint32_t s_wsum[RADIX / 64];
+    __shared__ uint32_t s_wsum[RADIX / 64 > 0 ? RADIX / 64 : 1];
     __shared__ uint8_t s_lut4[256];
-    uint64_t *s_keys = reinterpret_cast<uint64_t *>(s_stage);
-    uint32_t *s_vals = reinterpret_cast<uint32_t *>(s_stage + SM::kValOff);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    // the first iteration's stores read buffer 1 before anything was staged (they go to the
+    // sink): keep their positions inside the tile
+    for (int i = tid; i < TILE + 2; i += T) s_pos[1][i] = 0;
     lds_barrier();  // the LUT, read by every thread's pack
     const TileWalk walk(ntiles);
     uint64_t rr[L0Units<BITS, TILE, T>::kPer];
@@ -419,24 +385,52 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         toff = tile_off[(uint64_t)t * RADIX + (tid & (RADIX - 1))];
         l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)t * TILE, rr);
     };
-    uint32_t pcnt = 0;
-    int cur = 0;
+    uint32_t pcnt = 0;  // staged elements of the previous tile (0: none -> its stores go to the sink)
+    uint64_t pP0 = 0;   // the previous tile's first position
+    int b = 0;          // this tile's buffers; b ^ 1: the staged previous tile
+    // one store group of the previous tile: slot s -> position -> key (from the staged codes)
+    auto store_group = [&](int g) {
+        const uint32_t s = min((uint32_t)(tid + g * T), pcnt - 1);  // pcnt == 0: stays in the tile
+        const uint32_t p = s_pos[b ^ 1][s];
+        const uint64_t key = l0_key_of<BITS, CANON>(s_code[b ^ 1], p, a.total_bits, a.symbols);
+        const uint64_t o = pcnt ? (uint64_t)(s_toff[b ^ 1][dg_of(key, d0)] + s) : sink;
+        kout[o] = key;
+        vout[o] = (uint32_t)(pP0 + p);
+        if (ND) nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        // keep each group's loads and stores in place: hoisting the groups' LDS reads ahead (the
+        // scheduler's choice) keeps 22 groups' positions and keys live and spills them to scratch,
+        // whose vmcnt waits then drain every store in flight
+        __builtin_amdgcn_sched_barrier(0);
+    };
     if (walk.first < walk.end) load(walk.first);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    const bool pw = PROF && lane == 0 && (wave == 0 || wave == NW - 1);
+    unsigned long long ph[kL0Phases] = {0}, tp = PROF ? clock64() : 0;
+    auto mark = [&](int k) {
+        if constexpr (PROF) {
+            if (pw) {
+                const unsigned long long t1 = clock64();
+                ph[k] += t1 - tp;
+                tp = t1;
+            }
+        }
+    };
     for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
         uint32_t *wc = s_wc + wave * RADIX;
 #pragma unroll
         for (int u = 0; u < (RADIX + 63) / 64; ++u)
             if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
-        if (tid < RADIX) s_toff[cur][tid] = toff;
-        l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
+        if (tid < RADIX) s_toff[b][tid] = toff;
+        l0_pack<BITS, TILE, T>(rr, s_code[b], s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         // rr and toff are consumed: the next tile's bytes fly during this whole tile (the last
         // tile re-loads itself, so every iteration issues the same loads: static wait counts)
         load(min(t + walk.step, walk.end - 1));
-        const uint32_t *ptoff = s_toff[cur ^ 1];
+        mark(0);
 #pragma unroll
-        for (int g = 0; g < PRE; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
+        for (int g = 0; g < G_TOP; ++g) store_group(g);
+        mark(1);
         lds_barrier();  // packed codes visible
+        mark(2);
         const uint64_t P0 = a.lo + (uint64_t)t * TILE;
         // a tile without stops that ends before a.hi: every position starts a k-mer (wave-uniform)
         uint32_t anystop = 0;
@@ -444,29 +438,27 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         for (int j = 0; j < (P::kGroups + 63) / 64; ++j)
             anystop |= s_dol[min((uint32_t)(j * 64 + lane), (uint32_t)P::kGroups - 1)];
         const bool clean = __ballot(anystop != 0) == 0 && P0 + TILE <= a.hi;
-        uint64_t key[I];
-        uint32_t val[I], dig[I], rank[I];
-        bool valid[I];
+        uint32_t dr[I], validm = 0;  // per item: digit | rank << 8 (rank < I * 64)
         uint32_t p0 = wave * (I * 64) + lane;
         asm volatile("" : "+v"(p0));
+        mark(3);
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = p0 + i * 64;
-            valid[i] = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
-            key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
-            val[i] = (uint32_t)(P0 + p);
-        }
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            dig[i] = dg_of(key[i], d0);
-            const uint64_t peers = match_peers<R>(dig[i], valid[i]);
+            const bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
+            validm |= (valid ? 1u : 0u) << i;
+            const uint32_t dig = dg_of(l0_key_of<BITS, CANON>(s_code[b], p, a.total_bits, a.symbols), d0);
+            const uint64_t peers = match_peers<R>(dig, valid);
             const uint32_t rank_in = lanes_below(peers);
-            const uint32_t old = wc[dig[i]];
-            if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
-            rank[i] = old + rank_in;
-            if (PRE + i < I) pipe_store<T, I, R, 0, ND>(PRE + i, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
+            const uint32_t old = wc[dig];
+            if (valid && rank_in == 0) wc[dig] = old + (uint32_t)__popcll(peers);
+            dr[i] = dig | ((old + rank_in) << 8);
+            if (i < G_RANK) store_group(G_TOP + i);
+            __builtin_amdgcn_sched_barrier(0);  // one item at a time (register pressure, see above)
         }
-        lds_barrier();  // ranks final; the previous tile's staging has been read out
+        mark(4);
+        lds_barrier();  // ranks final
+        mark(5);
         uint32_t total = 0, incl = 0;
         if (tid < RADIX) {
 #pragma unroll
@@ -483,30 +475,43 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             }
             if (lane == 63) s_wsum[wave] = incl;
         }
+#pragma unroll
+        for (int g = 0; g < G_SCAN; ++g) store_group(G_TOP + G_RANK + g);
         lds_barrier();
         if (tid < RADIX) {
             uint32_t pre = 0;
             for (int w = 0; w < wave; ++w) pre += s_wsum[w];
             const uint32_t st = pre + incl - total;
             s_start[tid] = st;
-            s_toff[cur][tid] -= st;
+            s_toff[b][tid] -= st;
             if (tid == RADIX - 1) s_start[RADIX] = pre + incl;
         }
         lds_barrier();
+        mark(6);
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            const uint32_t sl = valid[i] ? s_start[dig[i]] + wc[dig[i]] + rank[i] : (uint32_t)TILE;
-            s_keys[sl] = key[i];
-            s_vals[sl] = val[i];
+            const bool valid = (validm >> i) & 1u;
+            const uint32_t dg = dr[i] & 0xFFu;
+            const uint32_t sl = valid ? s_start[dg] + wc[dg] + (dr[i] >> 8) : (uint32_t)TILE;
+            s_pos[b][sl] = (uint16_t)(p0 + i * 64);
         }
-        pcnt = s_start[RADIX];
-        lds_barrier();  // staging complete; counters and codes read
-        cur ^= 1;
+        const uint32_t cnt = s_start[RADIX];
+#pragma unroll
+        for (int g = G_TOP + G_RANK + G_SCAN; g < I; ++g) store_group(g);
+        mark(7);
+        pcnt = cnt;
+        pP0 = P0;
+        lds_barrier();  // staging complete; counters, codes and the previous staging read
+        mark(8);
+        b ^= 1;
     }
     if (walk.first < walk.end) {
-        const uint32_t *ptoff = s_toff[cur ^ 1];
 #pragma unroll
-        for (int g = 0; g < I; ++g) pipe_store<T, I, R, 0, ND>(g, d0, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
+        for (int g = 0; g < I; ++g) store_group(g);
+    }
+    if constexpr (PROF) {
+        if (pw)
+            for (int k = 0; k < kL0Phases; ++k) atomicAdd(&a.prof[(wave != 0) * kL0Phases + k], ph[k]);
     }
 }
 
@@ -1677,6 +1682,12 @@ static bool xcd_walk_off() {
     return v;
 }
 
+// timing only: GKM_L0_PROF=1 times the phases of the 2-bit L0 partition (tools)
+static bool l0_prof() {
+    static const bool v = std::getenv("GKM_L0_PROF") != nullptr;
+    return v;
+}
+
 // tuning only (A/B runs): GKM_WAVE_OCC=4 runs the 8-key wave class at 4 waves per SIMD
 static int wave_occ() {
     static const int v = std::getenv("GKM_WAVE_OCC") ? std::atoi(std::getenv("GKM_WAVE_OCC")) : 5;
@@ -1850,11 +1861,38 @@ struct MsdDriver {
     void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
                    uint64_t sink, const NextDigits &ndg) {
         if (count)
-            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kPI, R, CANON>),
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kP0I, R, CANON>),
                                dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kPT), 0, c->stream, a, d0, tile_hist, nt0);
+        else if (BITS == 2 && R == 7 && !CANON && l0_prof())
+            l0_prof_launch<ND>(a, d0, kout, vout, nt, sink, ndg);
         else
-            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kPT, kPI, R, ND, CANON>), dim3(pgrid), dim3(kPT), 0, c->stream,
+            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kPT, kP0I, R, ND, CANON>), dim3(pgrid), dim3(kPT), 0, c->stream,
                                a, d0, tile_hist, kout, vout, nt, sink, ndg);
+    }
+
+    // timing only (GKM_L0_PROF=1): the L0 partition with per-phase clocks, printed to stderr
+    template <bool ND>
+    void l0_prof_launch(L0Args a, Dig d0, uint64_t *kout, uint32_t *vout, uint32_t nt, uint64_t sink,
+                        const NextDigits &ndg) {
+        unsigned long long *pr = nullptr;
+        if (scratch(c, "l0_prof", 2 * kL0Phases, &pr) != hipSuccess) return;
+        hipMemsetAsync(pr, 0, 16 * kL0Phases, c->stream);
+        a.prof = pr;
+        hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kP0I, 7, ND, false, true>), dim3(pgrid), dim3(kPT), 0, c->stream,
+                           a, d0, tile_hist, kout, vout, nt, sink, ndg);
+        unsigned long long h[2 * kL0Phases];
+        hipMemcpyAsync(h, pr, 16 * kL0Phases, hipMemcpyDeviceToHost, c->stream);
+        hipStreamSynchronize(c->stream);
+        static const char *names[kL0Phases] = {"pack+load", "top-stores", "bar1", "clean", "rank+stores",
+                                               "bar2", "scan+stores", "staging+stores", "bar5"};
+        for (int w = 0; w < 2; ++w) {
+            unsigned long long tot = 0;
+            for (int k = 0; k < kL0Phases; ++k) tot += h[w * kL0Phases + k];
+            std::fprintf(stderr, "[l0prof] wave %s:", w ? "last" : "first");
+            for (int k = 0; k < kL0Phases; ++k)
+                std::fprintf(stderr, " %s %.1f%%", names[k], tot ? 100.0 * h[w * kL0Phases + k] / tot : 0.0);
+            std::fprintf(stderr, " (ticks per tile: %.0f)\n", (double)tot / std::max<uint32_t>(nt, 1));
+        }
     }
 
     template <bool CANON>
@@ -1895,7 +1933,7 @@ struct MsdDriver {
     // column scan (seg_base / seg_cnt), *count = k-mers kept
     int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count) {
         const uint64_t span = hi > lo ? hi - lo : 0;
-        const uint64_t nt0 = std::max<uint64_t>((span + kPTile - 1) / kPTile, 1);
+        const uint64_t nt0 = std::max<uint64_t>((span + kP0Tile - 1) / kP0Tile, 1);
         const uint64_t nc0 = (nt0 + ctiles - 1) / ctiles;
         l0_tiles = nt0;
         int rc = tables(nt0, nc0, 1);
@@ -1946,7 +1984,7 @@ struct MsdDriver {
         timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
-        const bool with_nd = kout == c->keys[0];
+        const bool with_nd = kout == c->keys[0] && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
         if (with_nd) {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));

@@ -42,6 +42,9 @@ FERR_AMBIG_SEG = 5
 FERR_CRISPR_LEN = 6
 
 LIB_PATH = Path(__file__).with_name("libgkm.so")
+# tuning only: GKM_LIB names another build of the same library (A/B of compile-time variants)
+if os.environ.get("GKM_LIB"):
+    LIB_PATH = Path(os.environ["GKM_LIB"]).resolve()
 
 # every symbol include/gkm.h declares (checked by tests/test_native_abi.py)
 EXPORTED = (

@@ -325,6 +325,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->enum_sorted = false;
     c->pk_fresh = false;
     c->n = 0;
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
@@ -367,7 +368,7 @@ extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
     c->have_starts = true;
     c->enumerated = true;
     c->starts_materialized = false;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = c->enum_sorted = false;
     if (n_out) *n_out = n;
     return GK_OK;
 }
@@ -388,7 +389,7 @@ extern "C" int gk_set_start_indices(gk_ctx *c, const uint32_t *src, uint64_t n, 
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = c->enum_sorted = false;
     return GK_OK;
 }
 
@@ -424,7 +425,15 @@ int gkm::ensure_keys(gk_ctx *c) {
     if (int rc = ensure_elems(c, c->n, c->spec.words)) return rc;
     int slot;
     timer_begin(c, "reencode_keys", &slot);
-    GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
+    // multi-word keys of a sorted enumeration: through an enumeration-order table in the free key
+    // buffer (one aligned row per k-mer instead of a ~70-byte window at a random position)
+    static const bool no_table = std::getenv("GKM_NO_KEY_TABLE") != nullptr;  // (A/B)
+    const KeySpec &ks = c->spec;
+    if (c->enum_sorted && !no_table && ks.words >= 2 && ks.symbols == ks.min_len && ks.symbols <= 64 &&
+        (ks.bits == 2 || ks.bits == 4) && c->n >= 4096 && c->key_words_b[c->cur ^ 1] >= ks.words)
+        GK_TRY_HIP(c, launch_encode_table_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur], c->keys[c->cur ^ 1]));
+    else
+        GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
     timer_end(c, slot);
     c->keys_valid = true;
     c->keys_stale = false;
@@ -614,6 +623,8 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
         if (bad) return fail(c, GK_E_NO_BASES, "kmers compared were less than min_kmer_len");
     }
     c->unique_valid = c->heads_valid = false;
+    c->enum_sorted = false;
+    const bool from_enum = c->enumerated;
     int rc;
     if (c->n < 2) {
         rc = materialize_starts(c);
@@ -644,6 +655,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     }
     rc = direct ? sort_direct(c, ks) : sort_doubling(c, max_kmer_len);
     if (rc != GK_OK) return rc;
+    c->enum_sorted = from_enum && direct && ks.symbols == ks.min_len;
     c->starts_materialized = true;
     c->sorted = true;
     c->enumerated = false;
@@ -926,7 +938,7 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = c->enum_sorted = false;
     if (range_split(c, ks)) {  // mixed sba: ACGT-only k-mers by 2-bit digit, the rest by prefix
         const int ob = range_own_bits(acgt_spec(ks));
         SplitRange rg{digit_lo, digit_hi, range_prefix(digit_lo, true, ob), range_prefix(digit_hi, false, ob), (ob + 1) / 2};
@@ -966,7 +978,7 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     c->have_starts = true;
     c->enumerated = false;
     c->starts_materialized = true;
-    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = false;
+    c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = c->enum_sorted = false;
     if (n > 0) {
         rc = msd_shard_sort(c, ks, d_keys, d_starts, h_piece_off, h_piece_len, h_piece_bucket, npieces);
         if (rc != GK_OK) return rc;

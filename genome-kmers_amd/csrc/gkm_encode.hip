@@ -7,6 +7,7 @@
 // The encoders turn the k-mer at a start into an integer whose unsigned order equals that byte
 // order: 2-bit codes when the sba is pure ACGT, 4-bit codes ('$' = 0) otherwise.
 #include <cstdlib>
+#include <vector>
 
 #include "gkm_canon.h"
 #include "gkm_internal.h"
@@ -428,6 +429,40 @@ __device__ __forceinline__ void canon2(int k, uint64_t &hi, uint64_t &lo) {
     }
 }
 
+// the W key words of the fixed-length k-mer at st: SWAR for windows of A/C/G/T, per symbol otherwise
+template <int W, int BITS>
+__device__ __forceinline__ void fast_window_key(const uint8_t *__restrict__ sba, const KS &ks, uint32_t st,
+                                                const uint8_t *s_lut4, uint64_t (&w)[W]) {
+    const int k = ks.symbols;
+    uint64_t hi, lo;
+    if (window2_acgt(sba, st, k, hi, lo)) {
+        if (ks.canonical) canon2(k, hi, lo);
+        if (BITS == 2) {
+            w[W - 1] = lo;
+            if (W > 1) w[0] = hi;
+        } else {
+            const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
+#pragma unroll
+            for (int q = 0; q < W; ++q) {  // q: word from the least significant end
+                uint64_t e = expand4_16((uint32_t)part[q]);
+                const int left = k - 16 * q;  // symbols in this word
+                if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
+                w[W - 1 - q] = e;
+            }
+        }
+    } else {
+        const uint8_t *b = sba + st;
+        if (ks.canonical) {
+            const bool rc = canon_is_rc<BITS>(b, k, s_lut4);
+#pragma unroll
+            for (int q = 0; q < W; ++q) w[q] = 0;
+            for (int t = 0; t < k; ++t) bi_shl_or<W>(w, BITS, canon_sym<BITS>(b, k, t, rc, s_lut4));
+        } else {
+            window_key<W, BITS, false>(ks, [&](int q) { return (uint32_t)b[q]; }, s_lut4, w);
+        }
+    }
+}
+
 template <int W, int BITS>
 __global__ __launch_bounds__(256) void encode_gather_fast_kernel(const uint8_t *__restrict__ sba, KS ks,
                                                                  const uint32_t *__restrict__ starts, uint64_t n,
@@ -435,40 +470,108 @@ __global__ __launch_bounds__(256) void encode_gather_fast_kernel(const uint8_t *
     __shared__ uint8_t s_lut4[256];
     s_lut4[threadIdx.x] = c_code4[threadIdx.x];
     __syncthreads();
-    const int k = ks.symbols;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t st = starts[i];
-        uint64_t hi, lo;
         uint64_t w[W];
-        if (window2_acgt(sba, st, k, hi, lo)) {
-            if (ks.canonical) canon2(k, hi, lo);
-            if (BITS == 2) {
-                w[W - 1] = lo;
-                if (W > 1) w[0] = hi;
-            } else {
-                const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
+        fast_window_key<W, BITS>(sba, ks, starts[i], s_lut4, w);
 #pragma unroll
-                for (int q = 0; q < W; ++q) {  // q: word from the least significant end
-                    uint64_t e = expand4_16((uint32_t)part[q]);
-                    const int left = k - 16 * q;  // symbols in this word
-                    if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
-                    w[W - 1 - q] = e;
-                }
-            }
+        for (int q = 0; q < W; ++q) keys[(uint64_t)q * n + i] = w[q];
+    }
+}
+
+// Keys through an enumeration-order table (multi-word keys of a sorted enumeration, C5: 4 words).
+// The gather above reads each sorted start's window from the sequence -- 64-72 unaligned bytes at
+// a random position, about two random 64-B sectors per k-mer (236 ms at C5).  Here every key is
+// computed once in enumeration order (sequential reads, contiguous AoS writes) and each sorted
+// start then reads its W aligned words: one random row per k-mer.  Enumeration index of a start
+// p in contig s: kb[s] + (p - seg[s]), kb = exclusive prefix of the contigs' k-mer counts.
+constexpr int kSegLds = 2048;  // contig tables staged in LDS up to this many contigs
+
+// the last s with tab[s] <= x (tab ascending, tab[0] <= x)
+__device__ __forceinline__ uint32_t last_le(const uint32_t *tab, uint32_t n, uint32_t x) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int W, int BITS>
+__global__ __launch_bounds__(256) void key_table_kernel(const uint8_t *__restrict__ sba, KS ks,
+                                                        const uint32_t *__restrict__ seg, const uint32_t *__restrict__ kb,
+                                                        uint32_t nseg, uint64_t n, uint64_t *__restrict__ table) {
+    __shared__ uint8_t s_lut4[256];
+    __shared__ uint32_t s_seg[kSegLds], s_kb[kSegLds];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    const bool lds = nseg <= (uint32_t)kSegLds;
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < nseg; i += 256) {
+            s_seg[i] = seg[i];
+            s_kb[i] = kb[i];
+        }
+    __syncthreads();
+    const uint32_t *tseg = lds ? s_seg : seg, *tkb = lds ? s_kb : kb;
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = last_le(tkb, nseg, (uint32_t)j);  // contigs without k-mers share kb: the last wins
+        uint64_t w[W];
+        fast_window_key<W, BITS>(sba, ks, tseg[s] + ((uint32_t)j - tkb[s]), s_lut4, w);
+#pragma unroll
+        for (int q = 0; q < W; ++q) table[j * W + q] = w[q];
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void table_gather_kernel(const uint32_t *__restrict__ starts,
+                                                           const uint32_t *__restrict__ seg,
+                                                           const uint32_t *__restrict__ kb, uint32_t nseg, uint64_t n,
+                                                           const uint64_t *__restrict__ table,
+                                                           uint64_t *__restrict__ keys) {
+    __shared__ uint32_t s_seg[kSegLds], s_kb[kSegLds];
+    const bool lds = nseg <= (uint32_t)kSegLds;
+    if (lds)
+        for (uint32_t i = threadIdx.x; i < nseg; i += 256) {
+            s_seg[i] = seg[i];
+            s_kb[i] = kb[i];
+        }
+    __syncthreads();
+    const uint32_t *tseg = lds ? s_seg : seg, *tkb = lds ? s_kb : kb;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = starts[i];
+        const uint32_t s = last_le(tseg, nseg, p);
+        const uint64_t j = (uint64_t)tkb[s] + (p - tseg[s]);
+        uint64_t w[W];
+        if constexpr (W == 4) {
+            const uint4 *r = reinterpret_cast<const uint4 *>(table + j * 4);
+            const uint4 a = r[0], b = r[1];
+            w[0] = ((uint64_t)a.y << 32) | a.x;
+            w[1] = ((uint64_t)a.w << 32) | a.z;
+            w[2] = ((uint64_t)b.y << 32) | b.x;
+            w[3] = ((uint64_t)b.w << 32) | b.z;
+        } else if constexpr (W == 2) {
+            const uint4 a = *reinterpret_cast<const uint4 *>(table + j * 2);
+            w[0] = ((uint64_t)a.y << 32) | a.x;
+            w[1] = ((uint64_t)a.w << 32) | a.z;
         } else {
-            const uint8_t *b = sba + st;
-            if (ks.canonical) {
-                const bool rc = canon_is_rc<BITS>(b, k, s_lut4);
 #pragma unroll
-                for (int q = 0; q < W; ++q) w[q] = 0;
-                for (int t = 0; t < k; ++t) bi_shl_or<W>(w, BITS, canon_sym<BITS>(b, k, t, rc, s_lut4));
-            } else {
-                window_key<W, BITS, false>(ks, [&](int q) { return (uint32_t)b[q]; }, s_lut4, w);
-            }
+            for (int q = 0; q < W; ++q) w[q] = table[j * W + q];
         }
 #pragma unroll
         for (int q = 0; q < W; ++q) keys[(uint64_t)q * n + i] = w[q];
     }
+}
+
+template <int W, int BITS>
+static hipError_t table_gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys,
+                                 uint64_t *table, const uint32_t *kb) {
+    const int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL((key_table_kernel<W, BITS>), dim3(grid), dim3(256), 0, c->stream, c->sba, k, c->seg, kb,
+                       (uint32_t)c->nseg, n, table);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((table_gather_kernel<W>), dim3(grid), dim3(256), 0, c->stream, starts, c->seg, kb,
+                       (uint32_t)c->nseg, n, table, keys);
+    return hipGetLastError();
 }
 
 template <int W, int BITS, bool BOUNDED>
@@ -591,6 +694,42 @@ static hipError_t gather_dispatch(gk_ctx *c, const KS &k, const uint32_t *starts
     case 4: return gather_w<4, BITS, BOUNDED>(c, k, starts, n, keys);
     }
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n,
+                                      uint64_t *keys, uint64_t *table) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    // kb: exclusive prefix of the contigs' k-mer counts (kmers.py:837-861 counts)
+    std::vector<uint32_t> kb(c->nseg);
+    uint64_t acc = 0;
+    for (uint64_t s = 0; s < c->nseg; ++s) {
+        kb[s] = (uint32_t)acc;
+        const uint64_t end = (s + 1 == c->nseg) ? c->sba_len - 1 : (uint64_t)c->hseg[s + 1] - 2;
+        const uint64_t len = end - c->hseg[s] + 1;
+        if (len >= (uint64_t)ks.symbols) acc += len - ks.symbols + 1;
+    }
+    if (acc != n) return hipErrorInvalidValue;  // not the whole enumeration
+    uint32_t *d_kb = nullptr;
+    if (scratch(c, "enc_kb", std::max<uint64_t>(c->nseg, 1), &d_kb) != hipSuccess) return hipErrorOutOfMemory;
+    e = hipMemcpyAsync(d_kb, kb.data(), 4 * c->nseg, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    KS k = pod(ks);
+    if (ks.bits == 2) {
+        switch (ks.words) {
+        case 2: e = table_gather_w<2, 2>(c, k, starts, n, keys, table, d_kb); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (ks.words) {
+        case 2: e = table_gather_w<2, 4>(c, k, starts, n, keys, table, d_kb); break;
+        case 3: e = table_gather_w<3, 4>(c, k, starts, n, keys, table, d_kb); break;
+        case 4: e = table_gather_w<4, 4>(c, k, starts, n, keys, table, d_kb); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(c->stream);  // kb (host vector) was read by an async copy
 }
 
 hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys) {

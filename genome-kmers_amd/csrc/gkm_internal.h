@@ -90,6 +90,8 @@ struct gk_ctx {
     bool msd_force_keys = false;  // split_sort: the class-A MSD (acgt_only) writes its final keys too
     bool split_keys_final = false;  // the last split sort wrote the final (4-bit) keys in sorted order
     bool keys_stale = false;   // ... once re-encoded from vals[cur]: the MSD sort does not keep them (ensure_keys)
+    bool enum_sorted = false;  // vals = gk_sort's order of ALL enumerated k-mers (fixed length): ensure_keys
+                               // may gather the keys through a table in enumeration order
     bool keys_are_ranks = false;
     gkm::KeySpec spec{};
 
@@ -209,6 +211,11 @@ hipError_t launch_enumerate(gk_ctx *c, uint32_t min_k, uint32_t *out);
 hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n, uint32_t min_k, uint32_t *d_bad);
 hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist);
 hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys);
+// keys of sorted starts that are a permutation of the whole enumeration (c->enum_sorted): every
+// k-mer's key in enumeration order into `table` (AoS, W words each), then one aligned row gather
+// per sorted start (gkm_encode.hip)
+hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n,
+                                      uint64_t *keys, uint64_t *table);
 // strand of each canonical k-mer: 1 if its reverse complement is the smaller (the key), else 0
 hipError_t launch_canon_strands(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint8_t *out);
 

@@ -1860,9 +1860,25 @@ struct MsdDriver {
     template <int BITS, int R, bool ND, bool CANON>
     void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
                    uint64_t sink, const NextDigits &ndg) {
-        if (count)
+        // the count pass streams the sequence: 256-thread workgroups, eight per CU, each holding a
+        // whole tile of loads in flight (1,024-thread ones, two per CU, kept a quarter as many
+        // bytes in flight; GKM_L0_COUNT_1024=1 runs them for A/B)
+        static const bool count1024 = std::getenv("GKM_L0_COUNT_1024") != nullptr;
+        if (count && count1024)
             hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kP0I, R, CANON>),
                                dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kPT), 0, c->stream, a, d0, tile_hist, nt0);
+        else if (count) {
+            static int per_cu = 0;  // resident workgroups (the grid is persistent)
+            if (!per_cu &&
+                (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                     &per_cu, (const void *)msd0_count_kernel<BITS, kPT / 4, kP0I * 4, R, CANON>, kPT / 4, 0) !=
+                     hipSuccess ||
+                 per_cu < 1))
+                per_cu = 1;
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT / 4, kP0I * 4, R, CANON>),
+                               dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kPT / 4), 0, c->stream, a, d0,
+                               tile_hist, nt0);
+        }
         else if (BITS == 2 && R == 7 && !CANON && l0_prof())
             l0_prof_launch<ND>(a, d0, kout, vout, nt, sink, ndg);
         else

@@ -2626,6 +2626,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
             plen.push_back(kc[w]);
             found += kc[w];
         }
+        timer_units(c, slot, found);  // (stage rates: kept k-mers out, the whole sequence in)
         if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
     }
     *n_kept = found;

@@ -854,7 +854,21 @@ struct Lists {
     uint32_t *dn_start, *dn_len;                 // key bits exhausted: final as they stand
     uint8_t *dn_par;
     uint2 *loc[kLocal];                          // local entries by class
+    // per entry: the bucket's sorted key bits (its prefix), | kCompact when its elements are
+    // stored compact (a compact level's output, see level_pass); null: not recorded
+    uint64_t *nb_pref;
+    uint64_t *loc_pref[kLocal];
 };
+
+// A compact level writes per element, in the key array, the key bits below the next 8-bit digit
+// (high half) and the start (low half), and that digit in the digit bytes: 9 B instead of 12 (and
+// two stores instead of three); the bucket's prefix completes the key.
+constexpr uint64_t kCompact = 1ull << 63;
+
+__device__ __forceinline__ uint64_t compact_key(uint64_t pref, int hi, int B, uint32_t dig, uint32_t low) {
+    const int rem = B - hi;  // 9..40
+    return ((pref & ~kCompact) << rem) | ((uint64_t)dig << (rem - 8)) | (uint64_t)low;
+}
 
 // local class of a bucket of <= kBlockMax elements
 __host__ __device__ constexpr uint32_t local_cap(int cls) {
@@ -871,16 +885,18 @@ __device__ __forceinline__ int list_of(uint32_t size, int hi, int B, bool allow_
 
 // entry `at` of list l for a sub-bucket
 __device__ __forceinline__ void put_entry(const Lists &L, int l, uint32_t at, uint32_t st, uint32_t size, int hi,
-                                          int parity) {
+                                          int parity, uint64_t pref = 0) {
     if (l == kCtrBig) {
         L.nb_start[at] = st;
         L.nb_len[at] = size;
+        if (L.nb_pref) L.nb_pref[at] = pref;
     } else if (l == kCtrDone) {
         L.dn_start[at] = st;
         L.dn_len[at] = size;
         L.dn_par[at] = (uint8_t)parity;
     } else {
         L.loc[l - kCtrLoc][at] = local_entry(st, size, hi, parity);
+        if (L.loc_pref[l - kCtrLoc]) L.loc_pref[l - kCtrLoc][at] = pref;
     }
 }
 
@@ -900,10 +916,14 @@ __device__ __forceinline__ void route(uint32_t st, uint32_t size, int hi, int B,
 // sums[l] += elements routed to list l (for the profile's work counts).
 constexpr int kClassT = 1024;
 
+// Prefixes: sub-bucket i of a partition by pw-bit digits has parent i >> pw (prefix ppref[i >> pw],
+// 0 when null) and digit i & (2^pw - 1); with pw = 0 the entries are whole buckets (prefix ppref[i]).
+// compact: the level wrote compact elements (the entries get kCompact).
 __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__restrict__ seg_base,
                                                            const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
                                                            int B, int parity, Lists L, uint32_t *__restrict__ ctr,
-                                                           unsigned long long *__restrict__ sums, uint32_t min_size) {
+                                                           unsigned long long *__restrict__ sums, uint32_t min_size,
+                                                           const uint64_t *__restrict__ ppref, int pw, int compact) {
     constexpr int NW = kClassT / 64;
     __shared__ uint32_t s_cnt[kLists][NW];
     __shared__ uint32_t s_elems[kLists][NW];
@@ -947,9 +967,31 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
         for (int w = 0; w < wave; ++w) pre += s_cnt[l][w];
         at[l] = pre + below[l];
     }
+    uint64_t pref = 0;
+    if (li >= 0) {
+        if (pw > 0) pref = ((ppref ? ppref[i >> pw] & ~kCompact : 0ull) << pw) | (i & ((1ull << pw) - 1));
+        else pref = ppref ? ppref[i] & ~kCompact : 0ull;
+        if (compact) pref |= kCompact;
+    }
 #pragma unroll
     for (int l = 0; l < kLists; ++l)
-        if (li == l) put_entry(L, l, at[l], st, size, hi, parity);
+        if (li == l) put_entry(L, l, at[l], st, size, hi, parity, pref);
+}
+
+// keys of compact elements (one workgroup per bucket): prefix | digit | low bits
+__global__ __launch_bounds__(256) void expand_compact_kernel(const uint32_t *__restrict__ bst,
+                                                             const uint32_t *__restrict__ blen,
+                                                             const uint64_t *__restrict__ bpref, int hi, int B,
+                                                             const uint8_t *__restrict__ nd,
+                                                             uint64_t *__restrict__ kio, uint32_t *__restrict__ vout) {
+    const uint64_t st = bst[blockIdx.x];
+    const uint32_t len = blen[blockIdx.x];
+    const uint64_t pf = bpref[blockIdx.x];
+    for (uint32_t e = threadIdx.x; e < len; e += 256) {
+        const uint64_t x = kio[st + e];
+        kio[st + e] = compact_key(pf, hi, B, nd[st + e], (uint32_t)(x >> 32));
+        vout[st + e] = (uint32_t)x;
+    }
 }
 
 // tile + chunk tables of a bucket list (one thread per bucket)
@@ -1032,15 +1074,34 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
     return x;
 }
 
+// compact inputs (first local round after a compact level): where to find the elements' low key
+// bits and next digits, and the entries' prefixes
+struct CompactIn {
+    const uint64_t *pref;  // per list entry (null: no entry is compact)
+    const uint8_t *nd;
+};
+
 template <int T, int I>
 __device__ __forceinline__ void local_load(const uint2 e, const uint64_t *k0, const uint32_t *v0, const uint64_t *k1,
-                                           const uint32_t *v1, uint64_t (&key)[I], uint32_t (&val)[I]) {
+                                           const uint32_t *v1, uint64_t (&key)[I], uint32_t (&val)[I],
+                                           uint64_t pf = 0, const CompactIn *ci = nullptr, int B = 0) {
     const uint64_t st = e.x;
     const uint32_t len = e.y >> 8;
     const uint64_t *sk = (e.y & 1) ? k1 : k0;
     const uint32_t *sv = (e.y & 1) ? v1 : v0;
     uint32_t q0 = (threadIdx.x >> 6) * (I * 64) + (threadIdx.x & 63);
     asm volatile("" : "+v"(q0));
+    if (pf & kCompact) {  // (uniform: one bucket per wave / workgroup)
+        const int hi = (e.y >> 1) & 127;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint64_t e_ = st + min(q0 + i * 64, len - 1);
+            const uint64_t x = sk[e_];
+            key[i] = compact_key(pf, hi, B, ci->nd[e_], (uint32_t)(x >> 32));
+            val[i] = (uint32_t)x;
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         const uint64_t e_ = st + min(q0 + i * 64, len - 1);
@@ -1053,7 +1114,8 @@ template <int T, int I, int R>
 __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys,
+                                                      CompactIn ci) {
     using SM = PartSmem<T, I, R>;
     constexpr int TILE = SM::kTile;
     constexpr int RADIX = SM::kRadix;
@@ -1072,9 +1134,10 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     if (idx >= count) return;
     for (int i = tid; i < SM::kWaves * RADIX; i += T) s_mask[i] = 0;
     uint2 e = list[idx];
+    uint64_t pf = ci.pref ? ci.pref[idx] : 0;
     uint64_t key[I];
     uint32_t val[I];
-    local_load<T, I>(e, k0, v0, k1, v1, key, val);
+    local_load<T, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     for (; idx < count; idx += gridDim.x) {
         const uint2 ce = e;
@@ -1099,7 +1162,10 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         const Dig dd = dig_at(B, hi, R);
         const int nhi = hi + R;      // key bits sorted within a sub-bucket
         const bool last = nhi >= B;  // sub-bucket keys are equal
-        if (idx + gridDim.x < count) e = list[idx + gridDim.x];  // else: re-load the current one
+        if (idx + gridDim.x < count) {  // else: re-load the current one
+            e = list[idx + gridDim.x];
+            pf = ci.pref ? ci.pref[idx + gridDim.x] : 0;
+        }
 
         // 1. stable partition into LDS
         for (int i = tid; i < SM::kWaves * RADIX; i += T) s_wc[i] = 0;
@@ -1167,7 +1233,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
             s_hd[out[i]] = hd[i];  // 0 / 1: final (not) a group head; 2: re-listed
         }
         // the next bucket's loads fly while this one is written back
-        local_load<T, I>(e, k0, v0, k1, v1, key, val);  // unconditional: static load count
+        local_load<T, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);  // unconditional: static load count
         lds_barrier();
 
         // 3. in-order write-back with head flags
@@ -1193,7 +1259,8 @@ template <int I, int MINW = 1>
 __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys) {
+                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys,
+                                                      CompactIn ci) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
     // digit masks (256), and the staged starts (CAP + 1 uint32) of the write-back
@@ -1216,9 +1283,10 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
 #pragma unroll
     for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;
     uint2 e = list[idx];
+    uint64_t pf = ci.pref ? ci.pref[idx] : 0;
     uint64_t key[I];
     uint32_t val[I];
-    local_load<64, I>(e, k0, v0, k1, v1, key, val);
+    local_load<64, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     for (; idx < lend; idx += lstep) {
         const uint2 ce = e;
@@ -1236,7 +1304,10 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
         const Dig dd = dig_at(B, hi, 8);
         const int nhi = hi + 8;
         const bool last = nhi >= B;
-        if (idx + lstep < lend) e = list[idx + lstep];
+        if (idx + lstep < lend) {
+            e = list[idx + lstep];
+            pf = ci.pref ? ci.pref[idx + lstep] : 0;
+        }
         const int live = min(I, (int)((len + 63) >> 6));
 
 #pragma unroll
@@ -1356,7 +1427,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
             s_k[o] = key[i];
             s_v[o] = val[i];
         }
-        local_load<64, I>(e, k0, v0, k1, v1, key, val);  // the next bucket
+        local_load<64, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);  // the next bucket
         const bool wk = relist || wkeys;  // keys: final-key sorts, or buckets with re-listed elements
 #pragma unroll
         for (int i = 0; i < I; ++i) {
@@ -1379,7 +1450,8 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
 // starts and head flags to buffer 0.
 __global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__ list, uint32_t count,
                                                        uint64_t *k0, uint32_t *v0, const uint64_t *k1,
-                                                       const uint32_t *v1, uint8_t *__restrict__ heads, int wkeys) {
+                                                       const uint32_t *v1, uint8_t *__restrict__ heads, int wkeys,
+                                                       CompactIn ci, int B) {
     const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
     const bool live = idx < count;
     const uint2 e = live ? list[idx] : make_uint2(0, 1u << 8);
@@ -1389,11 +1461,14 @@ __global__ __launch_bounds__(256) void msd_tiny_kernel(const uint2 *__restrict__
     const uint32_t *sv = (e.y & 1) ? v1 : v0;
     uint64_t key[kTiny];
     uint32_t val[kTiny];
+    const uint64_t pf = live && ci.pref ? ci.pref[idx] : 0;
+    const int ehi = (e.y >> 1) & 127;
 #pragma unroll
     for (int j = 0; j < kTiny; ++j) {
         const uint64_t at = st + min((uint32_t)j, len - 1);
-        key[j] = live ? sk[at] : 0;
-        val[j] = live ? sv[at] : 0;
+        const uint64_t x = live ? sk[at] : 0;
+        key[j] = (pf & kCompact) ? compact_key(pf, ehi, B, ci.nd[at], (uint32_t)(x >> 32)) : x;
+        val[j] = !live ? 0 : (pf & kCompact) ? (uint32_t)x : sv[at];
     }
     uint32_t out[kTiny];
     bool hd[kTiny];
@@ -1682,6 +1757,12 @@ static bool xcd_walk_off() {
     return v;
 }
 
+// tuning only (A/B runs): GKM_NO_COMPACT=1 keeps 64-bit keys in every level's output
+static bool no_compact() {
+    static const bool v = std::getenv("GKM_NO_COMPACT") != nullptr;
+    return v;
+}
+
 // timing only: GKM_L0_PROF=1 times the phases of the 2-bit L0 partition (tools)
 static bool l0_prof() {
     static const bool v = std::getenv("GKM_L0_PROF") != nullptr;
@@ -1719,6 +1800,7 @@ static int pack_sequence(gk_ctx *c, const uint64_t **code, const uint32_t **dol)
     return GK_OK;
 }
 
+static const char *kLocPrefName[kLocal] = {"locp0", "locp1", "locp2", "locp3", "locp4"};
 static const char *kLocName[kLocal][2] = {{"loc0a", "loc0b"}, {"loc1a", "loc1b"}, {"loc2a", "loc2b"},
                                           {"loc3a", "loc3b"}, {"loc4a", "loc4b"}};
 static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_r"},
@@ -1742,6 +1824,8 @@ struct MsdDriver {
     uint32_t *ctr = nullptr, h[kCtrN] = {0};
     unsigned long long *sums = nullptr, hs[kLists] = {0};
     uint32_t *big_start[2], *big_len[2];
+    uint64_t *big_pref[2];         // prefixes of the big-list buckets (Lists::nb_pref)
+    uint64_t *loc_pref[kLocal];    // prefixes of generation 0's local entries (Lists::loc_pref)
     uint32_t *dn_start, *dn_len;
     uint8_t *dn_par;
     uint2 *loc[kLocal][2];
@@ -1749,6 +1833,10 @@ struct MsdDriver {
     int width(int level) const { return wsched[std::min(level, kMaxLevels - 1)]; }
     uint8_t *heads = nullptr;
     uint8_t *nd = nullptr;  // next-level digit per element of the last pass's output
+    // compact level (see classify_kernel): the last pass wrote (low key bits, start) pairs and the
+    // next digit instead of keys and starts
+    bool compact_now = false;
+    int compact_hi = 0;
     bool nd_ready = false, nd_next = true;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
     uint64_t nloc[kLocal] = {0}, loc_elems[kLocal] = {0}, ndone = 0, big_elems = 0;
@@ -1791,8 +1879,11 @@ struct MsdDriver {
     }
 
     Lists lists(int g, int bigsel) {
+        // prefixes are recorded by classify (generation 0); re-listed entries carry full keys
         return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par,
-                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g], loc[4][g]}};
+                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g], loc[4][g]}, big_pref[bigsel],
+                     {g ? nullptr : loc_pref[0], g ? nullptr : loc_pref[1], g ? nullptr : loc_pref[2],
+                      g ? nullptr : loc_pref[3], g ? nullptr : loc_pref[4]}};
     }
 
     int init(uint64_t n_) {
@@ -1806,10 +1897,13 @@ struct MsdDriver {
         GK_TRY_HIP(c, scratch(c, "big_len0", max_big, &big_len[0]));
         GK_TRY_HIP(c, scratch(c, "big_start1", max_big, &big_start[1]));
         GK_TRY_HIP(c, scratch(c, "big_len1", max_big, &big_len[1]));
+        GK_TRY_HIP(c, scratch(c, "big_pref0", max_big, &big_pref[0]));
+        GK_TRY_HIP(c, scratch(c, "big_pref1", max_big, &big_pref[1]));
         GK_TRY_HIP(c, grow_keep(c, "dn_start", 1024, 0, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", 1024, 0, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", 1024, 0, &dn_par));
         for (int k = 0; k < kLocal; ++k) GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], 1024, 0, &loc[k][0]));
+        for (int k = 0; k < kLocal; ++k) GK_TRY_HIP(c, grow_keep(c, kLocPrefName[k], 1024, 0, &loc_pref[k]));
         GK_TRY_HIP(c, scratch(c, "msd_heads", n + 64, &heads));
         return GK_OK;
     }
@@ -2013,14 +2107,28 @@ struct MsdDriver {
         return GK_OK;
     }
 
+    // after a compact level: the (rare) sub-buckets that go to another global level get their keys
+    // back in keys[out], so that level reads keys as usual (the digit bytes stay valid for it)
+    int expand_big(int out) {
+        if (!compact_now || nbig == 0) return GK_OK;
+        hipLaunchKernelGGL(expand_compact_kernel, dim3(nbig), dim3(256), 0, c->stream, big_start[cur_big],
+                           big_len[cur_big], big_pref[cur_big], compact_hi, B, nd, c->keys[out], c->vals[out]);
+        GK_TRY_HIP(c, hipGetLastError());
+        return GK_OK;
+    }
+
     // route nsub sub-buckets (seg_base / seg_cnt, or base / cnt) of a level; hi = key bits sorted
     // after it; sub-buckets under min_size elements are dropped (final as they stand)
+    // ppref / pw / compact: see classify_kernel
     int classify(uint64_t nsub, int hi, int parity, int bigsel, const uint32_t *base = nullptr,
-                 const uint32_t *cnt = nullptr, uint32_t min_size = 1) {
+                 const uint32_t *cnt = nullptr, uint32_t min_size = 1, const uint64_t *ppref = nullptr, int pw = 0,
+                 int compact = 0) {
         if (!base) base = seg_base;
         if (!cnt) cnt = seg_cnt;
         for (int k = 0; k < kLocal; ++k)
             GK_TRY_HIP(c, grow_keep(c, kLocName[k][0], nloc[k] + nsub, nloc[k], &loc[k][0]));
+        for (int k = 0; k < kLocal; ++k)
+            GK_TRY_HIP(c, grow_keep(c, kLocPrefName[k], nloc[k] + nsub, nloc[k], &loc_pref[k]));
         GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nsub, ndone, &dn_start));
         GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nsub, ndone, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nsub, ndone, &dn_par));
@@ -2028,7 +2136,8 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * kLists, c->stream));
         timer_begin(c, "msd_classify", &slot);
         hipLaunchKernelGGL(classify_kernel, dim3((unsigned)((nsub + kClassT - 1) / kClassT)), dim3(kClassT), 0,
-                           c->stream, base, cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums, min_size);
+                           c->stream, base, cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums, min_size, ppref, pw,
+                           compact);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         int r = read_ctr();
@@ -2056,6 +2165,15 @@ struct MsdDriver {
             else
                 hipLaunchKernelGGL(msd_count_kernel<R>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start, t_count,
                                    dig_at(B, hi, R), kin, tile_hist);
+            return;
+        }
+        if (compact_now) {
+            const int rem = B - hi - R;  // 9..40: key bits below this level's digit
+            NextDigits ndg{dig_at(B, hi + R, 8), nd};
+            ndg.lowmask = (uint32_t)((1ull << (rem - 8)) - 1);
+            hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 4, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
+                               t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
+                               (uint32_t)T, n, ndg);
             return;
         }
         const NextDigits ndg{dig_at(B, hi + R, nw), nd};
@@ -2093,10 +2211,16 @@ struct MsdDriver {
         // the next level's digit bytes, unless this level's sub-buckets will most likely all be
         // local (mean under kBlockMax / 8); a next level then counts from the keys
         nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax / 8;
+        // compact output when this level's sub-buckets will most likely all be finished locally
+        // and the key bits below the next 8-bit digit fit a u32: 9 B per element out instead of 12
+        // (4 start + 4 low bits + 1 digit byte), and the finishing kernels read 9 B instead of 12
+        const int rem = B - hi - width(level);
+        compact_now = phase == 0 && !nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
+        compact_hi = hi + width(level);
         level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, false);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        nd_ready = nd_next;
+        nd_ready = nd_next || compact_now;  // a compact level wrote the next 8-bit digit
         return GK_OK;
     }
 
@@ -2107,6 +2231,7 @@ struct MsdDriver {
     int first_level_from_pieces(const uint64_t *kin, const uint32_t *vin, const uint64_t *poff, const uint64_t *plen,
                                 const uint32_t *pbucket, uint32_t np, int level = 1, int hi = kGR) {
         std::vector<uint32_t> ts, tc, cf, cn, scf, snc, sst;
+        std::vector<uint64_t> spf;  // the buckets' prefixes: their top-hi-bit values
         uint64_t out_base = 0;
         for (uint32_t i = 0; i < np;) {
             uint32_t j = i;
@@ -2129,6 +2254,7 @@ struct MsdDriver {
                 }
                 snc.push_back((uint32_t)(cf.size() - scf.back()));
                 sst.push_back((uint32_t)out_base);
+                spf.push_back(pbucket[i]);
                 out_base += tot;
             }
             i = j;
@@ -2151,12 +2277,17 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemcpyAsync(s_cfirst, scf.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipMemcpyAsync(s_nchunks, snc.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipMemcpyAsync(s_st, sst.data(), 4 * nseg, hipMemcpyHostToDevice, c->stream));
+        uint64_t *s_pref;
+        GK_TRY_HIP(c, scratch(c, "s_ppref", nseg, &s_pref));
+        GK_TRY_HIP(c, hipMemcpyAsync(s_pref, spf.data(), 8 * nseg, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         big_elems = n;
         rc = level_pass(level, hi, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
         if (rc != GK_OK) return rc;
         cur_big = 0;
-        return classify(nseg << width(level), hi + width(level), 0, cur_big);
+        rc = classify(nseg << width(level), hi + width(level), 0, cur_big, nullptr, nullptr, 1, s_pref, width(level),
+                      compact_now ? 1 : 0);
+        return rc == GK_OK ? expand_big(0) : rc;
     }
 
     // Multi-word keys, phase > 0: the head flags of the order so far (buffer 0) mark the groups of
@@ -2255,7 +2386,9 @@ struct MsdDriver {
                             c->vals[in], out);
             if (rc != GK_OK) return rc;
             cur_big ^= 1;
-            rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big);
+            rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big, nullptr, nullptr, 1,
+                          big_pref[cur_big ^ 1], width(level), compact_now ? 1 : 0);
+            if (rc == GK_OK) rc = expand_big(out);
             if (rc != GK_OK) return rc;
             ++level;
             hi += width(level - 1);
@@ -2271,6 +2404,8 @@ struct MsdDriver {
         // the first wave round of phase 0, where random keys differ right below the sorted bits
         const int skip = (round > 0 || phase > 0 || k == 3) ? 1 : 0;
         const uint32_t small = (round > 0 || phase > 0) ? kSmallLate : kSmall;
+        // round 0 reads classify's entries, some of which may hold compact elements
+        const CompactIn ci{round == 0 ? loc_pref[k] : nullptr, nd};
         // persistent grids of the workgroups that fit at once (occupancy API, per kernel)
         auto grid = [&](const void *fn, int threads) {
             int per_cu = 0;
@@ -2283,31 +2418,31 @@ struct MsdDriver {
         switch (k) {
         case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)
             hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
             break;
         case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
                  // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
             if (wave_occ() == 4)
                 hipLaunchKernelGGL((msd_wave_kernel<8, 4>), grid((const void *)msd_wave_kernel<8, 4>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
             else
                 hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
             break;
         case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
                  // on C5 (A/B, one box)
             hipLaunchKernelGGL((msd_wave_kernel<16, 3>), grid((const void *)msd_wave_kernel<16, 3>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
                                grid((const void *)msd_local_kernel<kBT, kBI, kBR>, kBT), dim3(kBT), 0, c->stream, lst,
                                cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
-                               (uint32_t)kSmall, wkeys);  // the block class keeps kSmall: 96 measured slower (A/B)
+                               (uint32_t)kSmall, wkeys, ci);  // the block class keeps kSmall: 96 measured slower (A/B)
             break;
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
-                               v1, heads, wkeys);
+                               v1, heads, wkeys, ci, B);
         }
     }
 
@@ -2403,7 +2538,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     rc = d.run_l0(0, c->sba_len, c->keys[0], c->vals[0], c->elem_cap + 64, &found);
     if (rc != GK_OK) return rc;
     if (found != c->n) return fail(c, GK_E_HIP, "msd: k-mer count differs from the enumeration");
-    rc = d.classify(1u << d.width(0), d.width(0), 0, 0);
+    rc = d.classify(1u << d.width(0), d.width(0), 0, 0, nullptr, nullptr, 1, nullptr, d.width(0));
     if (rc != GK_OK) return rc;
     rc = d.levels(1, d.width(0), 0);
     if (rc != GK_OK) return rc;

@@ -430,6 +430,9 @@ struct PipeSmem {
 struct NextDigits {
     Dig d;
     uint8_t *out;
+    // MODE 4 (a compact level, gkm_msd.hip): kout[] gets the key bits below the next digit
+    // (lowmask) in the high half and the start in the low half; vout[] is not written
+    uint32_t lowmask = 0;
 };
 
 template <int T, int I, int R, int MODE, bool ND>
@@ -441,7 +444,10 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     const uint64_t k = s_keys[s];
     const uint32_t v = s_vals[s];
     const uint64_t o = cnt ? (uint64_t)(toff[dg_of(k, d)] + base + s) : sink;
-    if (MODE != 1 || o == 0xFFFFFFFFu) {
+    if (MODE == 4) {  // compact: (low key bits << 32 | start) in the key array, the next digit byte
+        kout[o] = ((uint64_t)((uint32_t)k & nd.lowmask) << 32) | v;
+        nd.out[o] = (uint8_t)dg_of(k, nd.d);
+    } else if (MODE != 1 || o == 0xFFFFFFFFu) {
         kout[o] = k;
         vout[o] = v;
         if (ND) nd.out[o] = (uint8_t)dg_of(k, nd.d);

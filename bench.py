@@ -209,12 +209,18 @@ def pipelined_e2e(torch, eng, sba, step, log, reps: int = 3) -> dict:
 
 
 def load_traffic(path: str, kernel: str):
+    """HBM bytes per launch of `kernel` (an instantiation prefix such as
+    "msd_pipe_kernel<1024,11,8,4") from a tools/pmc_traffic.py summary, or None."""
     try:
         with open(path) as fh:
             t = json.load(fh)
-        return t.get(kernel, {}).get("hbm_bytes_max_launch")
     except (OSError, ValueError):
         return None
+    want = kernel.replace(" ", "").rstrip(">")
+    for name, rec in t.items():
+        if not name.startswith("_") and "<" in name and name.startswith(want):
+            return rec.get("hbm_bytes_max_launch")
+    return None
 
 
 def main():
@@ -347,7 +353,9 @@ def main():
         if name == "msd_select":
             return L * v["count"] + 13 * u  # the whole sequence in; kept (key, start, digit) out (units: kept)
         if name == "msd_pass_l0" and not range_mode:
-            return seq_bytes * v["count"] + 12 * u  # sequence bytes in, (key, start) out
+            return seq_bytes * v["count"] + 13 * u  # sequence bytes in, (key, start, next digit) out
+        if name.startswith("msd_pass_l") and name.endswith("c"):
+            return 21 * u  # compact level: (key, start) in, (low bits | start) + next digit out
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out
         if name.startswith("msd_local"):
@@ -364,28 +372,32 @@ def main():
         if b and v["total_ms"] > 0:
             kernels[name] = {"ms_per_launch": round(v["total_ms"] / v["count"], 4),
                              "gbs": round(b / (v["total_ms"] * 1e-3) / 1e9, 1)}
-    # dominant kernel: msd_pipe_kernel, the partition pass of every level >= 1 (averaged over
-    # its launches, as rocprofv3 --stats averages it); the L0 pass when a genome needs none
-    cands = [n for n in report if n.startswith("msd_pass_l") and n != "msd_pass_l0" and report[n]["units"]]
-    if cands:
-        dom = "msd_pass_l1.."
-        rp = {k: sum(report[n][k] for n in cands) for k in ("count", "total_ms", "units")}
-        dom_bytes = 24 * rp["units"]
+    # dominant kernel: the stage with the most time among the device kernels with a byte model
+    # (the level partitions, the compact level, the L0 partition, the wave-local finishing kernel)
+    kinds = {"msd_pass_l0": ("msd0_pipe_kernel<2,1024,18,7,true>", "the L0 partition, straight from the sequence"),
+             "msd_local_wave8": ("msd_wave_kernel<8,5>", "wave-local finishing of buckets <= 512")}
+    timed = {n: v for n, v in report.items() if stage_bytes(n, v) and v["total_ms"] > 0 and
+             (n in kinds or n.startswith("msd_pass_l"))}
+    dom = max(timed, key=lambda n: timed[n]["total_ms"]) if timed else None
+    rp = timed.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
+    dom_bytes = stage_bytes(dom, rp) if dom else 0
+    if dom in kinds:
+        kdesc, what = kinds[dom]
+    elif dom and dom.endswith("c"):
+        kdesc, what = "msd_pipe_kernel<1024,11,8,4>", "the compact last level's stable 8-bit partition"
     else:
-        dom = "msd_pass_l0"
-        rp = report.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
-        dom_bytes = stage_bytes(dom, rp)
+        kdesc, what = "msd_pipe_kernel<1024,11,8,0>", "one stable 8-bit MSD partition pass"
     avg_ms = rp["total_ms"] / max(rp["count"], 1)
     bytes_per_launch = dom_bytes / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
-    kname = "msd_pipe_kernel" if dom != "msd_pass_l0" else "msd0_pipe_kernel"
-    traffic = load_traffic(args.traffic, kname)
+    traffic = load_traffic(args.traffic, kdesc)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"{kname}<1024,11,8> ({dom}: one stable 8-bit MSD partition pass)",
+                "kernel": f"{kdesc} ({dom}: {what})",
                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "units_per_launch": int(rp["units"] / max(rp["count"], 1)), "bytes_per_unit": 24,
+                "units_per_launch": int(rp["units"] / max(rp["count"], 1)),
+                "bytes_per_unit": round(bytes_per_launch / max(rp["units"] / max(rp["count"], 1), 1), 2),
                 "stages": kernels}
 
     if rank == 0:

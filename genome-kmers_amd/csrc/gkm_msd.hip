@@ -1810,6 +1810,8 @@ static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_
                                            {"msd_local_tiny", "msd_local_tiny_r"}};
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
+static const char *kPassNamesC[] = {"msd_pass_l0c", "msd_pass_l1c", "msd_pass_l2c", "msd_pass_l3c",
+                                    "msd_pass_l4c", "msd_pass_l5c", "msd_pass_l6c", "msd_pass_l7c"};  // compact
 
 // One MSD sort of one-word keys into keys[0] / vals[0] (+ group heads).  The first partition
 // comes from the sequence (run_l0) or from received buckets (first_level_from_pieces); the rest
@@ -2205,18 +2207,18 @@ struct MsdDriver {
         timer_end(c, slot);
         int rc = scan_offsets(width(level), C, s_cfirst, s_nchunks, s_start, nseg);
         if (rc != GK_OK) return rc;
-        timer_begin(c, kPassNames[level & 7], &slot);
-        timer_units(c, slot, big_elems);
         GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
         // the next level's digit bytes, unless this level's sub-buckets will most likely all be
         // local (mean under kBlockMax / 8); a next level then counts from the keys
         nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax / 8;
         // compact output when this level's sub-buckets will most likely all be finished locally
-        // and the key bits below the next 8-bit digit fit a u32: 9 B per element out instead of 12
-        // (4 start + 4 low bits + 1 digit byte), and the finishing kernels read 9 B instead of 12
+        // and the key bits below the next 8-bit digit fit a u32: (low bits, start) as one u64 and
+        // the digit byte -- 9 B per element out instead of 12 -- and the finishing kernels read 9 B
         const int rem = B - hi - width(level);
         compact_now = phase == 0 && !nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
         compact_hi = hi + width(level);
+        timer_begin(c, compact_now ? kPassNamesC[level & 7] : kPassNames[level & 7], &slot);
+        timer_units(c, slot, big_elems);
         level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, false);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);

@@ -34,15 +34,18 @@ def main():
         wk = sum(wl) / max(len(wl), 1)
         # the largest launch (launches pair up in order: same command, same dispatch sequence)
         per = [a * 1024 * 2 + b * 1024 for a, b in zip(fl, wl)]
-        short = k.split("::")[-1].split("<")[0]
-        res[short] = {"kernel": k, "launches": max(len(fl), len(wl)),
-                      "fetch_bytes_per_launch": fk * 1024 * 2, "write_bytes_per_launch": wk * 1024,
-                      "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024,
-                      "hbm_bytes_max_launch": max(per) if per else None}
+        rec = {"kernel": k, "launches": max(len(fl), len(wl)),
+               "fetch_bytes_per_launch": fk * 1024 * 2, "write_bytes_per_launch": wk * 1024,
+               "hbm_bytes_per_launch": fk * 1024 * 2 + wk * 1024,
+               "hbm_bytes_max_launch": max(per) if per else None}
+        # keyed by the instantiation (template arguments, no spaces) and, for the first one of a
+        # name, by the bare name
+        res[k.split("::")[-1].replace(" ", "")] = rec
+        res.setdefault(k.split("::")[-1].split("<")[0], rec)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for k, v in res.items():
-        if not k.startswith("_"):
+        if not k.startswith("_") and "<" not in k:
             print(f"{k:28s} x{v['launches']:3d}  read {v['fetch_bytes_per_launch'] / 1e9:8.2f} GB  "
                   f"write {v['write_bytes_per_launch'] / 1e9:8.2f} GB")
 

@@ -1758,10 +1758,7 @@ static bool xcd_walk_off() {
 }
 
 // tuning only (A/B runs): GKM_NO_COMPACT=1 keeps 64-bit keys in every level's output
-static bool no_compact() {
-    static const bool v = std::getenv("GKM_NO_COMPACT") != nullptr;
-    return v;
-}
+static bool no_compact() { return std::getenv("GKM_NO_COMPACT") != nullptr; }  // (read per level: tests flip it)
 
 // timing only: GKM_L0_PROF=1 times the phases of the 2-bit L0 partition (tools)
 static bool l0_prof() {

@@ -215,6 +215,37 @@ def test_sparse_variation_all_levels_vs_oracle(level_bits, monkeypatch):
     oracle_check([("a", s[:450_000].tobytes().decode()), ("b", s[450_000:].tobytes().decode())], 31, 31)
 
 
+# Compact last level (gkm_msd.hip level_pass): k = 21 leaves 27 key bits below L1, so L1 stores
+# (low bits, start) pairs + digit bytes and the finishing kernels rebuild the keys from the bucket
+# prefixes; the periodic run makes sub-buckets above the local limit, which are expanded back for
+# another global level.  GKM_NO_COMPACT=1 runs the same input with full keys everywhere.
+@pytest.mark.parametrize("compact", [True, False])
+def test_compact_level_with_big_sub_buckets_vs_oracle(compact, monkeypatch):
+    if not compact:
+        monkeypatch.setenv("GKM_NO_COMPACT", "1")
+    rng = np.random.default_rng(21)
+    seqs = random_genome(rng, [1_500_000, 400_000])
+    seqs.append(("periodic", "ACGT" * 30_000 + "AACCGGTT" * 8_000))
+    k = 21
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    eng = km._get_engine()
+    eng.profile_enable(True)
+    km.sort()
+    assert ("msd_pass_l1c" in str(eng.profile_report())) == compact
+    eng.profile_enable(False)
+    unsorted = oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k)
+    want = oracle.quicksort(sc.forward_sba, unsorted, k, k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    # the keys the finishing kernels rebuilt (one-word keys: the sort's own, not a re-encode)
+    spec = oracle.key_spec(True, k, k)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+    h, t = km.get_kmer_group_counts(k, max_counts_bin=64)
+    oh, ot = oracle.group_scan(sc.forward_sba, want, k, max_counts_bin=64)
+    np.testing.assert_array_equal(h, oh)
+    assert t == ot
+
+
 def test_iupac_k31_vs_oracle():
     rng = np.random.default_rng(4)
     oracle_check(random_genome(rng, [120_000, 60_000], alphabet=b"ACGTACGTACGTNRY"), 31, 31)

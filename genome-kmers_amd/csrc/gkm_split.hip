@@ -23,6 +23,8 @@
 namespace gkm {
 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
+hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
+                                   uint32_t *out2, uint64_t n, uint64_t *total1, uint64_t *total2);
 
 __constant__ uint8_t c_code4_split[256];
 __constant__ uint8_t c_comp_split[256];  // the reference's complement (sequence_collection.py:402-433)
@@ -99,14 +101,36 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
     __shared__ uint32_t s_dol[kFlagGroups], s_bad[kFlagGroups], s_diff[kFlagGroups];
     __shared__ uint8_t s_lut4[256], s_comp[256];
     __shared__ uint32_t s_w[2][4];
+    // the store pass has nothing to do for a tile whose counts are zero: away from N runs and IUPAC
+    // letters, that is almost every tile of a genome
+    if (STORE && cnt_r[blockIdx.x] == 0 && cnt_h[blockIdx.x] == 0) return;
     s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
     s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
     const bool ranged = p4_lo != 0 || p4_hi != (1u << (4 * pns));
     const uint64_t P0 = (uint64_t)blockIdx.x * kFlagTile;
-    for (int g = threadIdx.x; g < kFlagGroups; g += 256) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * g);  // '$' pad after L
-        const uint4 ra = src[0], rb = src[1];
-        const uint32_t nxt = sba[P0 + 32ull * (g + 1)];
+    // the tile's 256 groups and the 3 halo groups: every load issued before any flag work (a second
+    // loop trip for the halo would double the load latency of the tile)
+    static_assert(kFlagGroups - 256 <= 256, "one halo group per thread at most");
+    const bool halo = threadIdx.x < kFlagGroups - 256;
+    uint4 ld[2][2];
+    uint32_t ldn[2];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0 + 32ull * threadIdx.x);  // '$' pad after L
+        ld[0][0] = src[0];
+        ld[0][1] = src[1];
+        ldn[0] = sba[P0 + 32ull * (threadIdx.x + 1)];
+        if (halo) {
+            ld[1][0] = src[512];  // group threadIdx.x + 256
+            ld[1][1] = src[513];
+            ldn[1] = sba[P0 + 32ull * (threadIdx.x + 257)];
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !halo) break;
+        const int g = threadIdx.x + 256 * h;
+        const uint4 ra = ld[h][0], rb = ld[h][1];
+        const uint32_t nxt = ldn[h];
         // SWAR, 8 positions per step: '$' flags, non-ACGT flags, and "differs from the next byte"
         // flags (each byte against its successor: the unit shifted down one byte, the next unit's
         // first byte on top)
@@ -200,8 +224,18 @@ __global__ __launch_bounds__(256) void homo_count_kernel(const uint8_t *__restri
     s_c[threadIdx.x] = 0;
     s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
     __syncthreads();
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-        atomicAdd(&s_c[homo_letter(sba, hs[i], canonical, s_comp)], 1u);
+    // the starts come in start order, so a wave mostly sees one letter (an N run): one LDS add per
+    // wave then, not 64 to the same address
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t l = homo_letter(sba, hs[i], canonical, s_comp);
+        const uint32_t l0 = __builtin_amdgcn_readfirstlane(l);
+        const uint64_t act = __ballot(1), same = __ballot(l == l0);
+        if (same == act) {
+            if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)act) - 1)) atomicAdd(&s_c[l0], (uint32_t)__popcll(act));
+        } else {
+            atomicAdd(&s_c[l], 1u);
+        }
+    }
     __syncthreads();
     if (s_c[threadIdx.x]) atomicAdd(&counts[threadIdx.x], s_c[threadIdx.x]);
 }
@@ -411,12 +445,11 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
                        ks.canonical, p4_lo, p4_hi, pns, cr, chh, nullptr, nullptr, nullptr, nullptr);
     GK_TRY_HIP(c, hipGetLastError());
     uint64_t nR = 0, nH = 0;
-    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cr, ftiles, orr, &nR));
-    GK_TRY_HIP(c, scan_u32_exclusive_pub(c, chh, ftiles, ohh, &nH));
+    GK_TRY_HIP(c, scan_u32_exclusive_pair(c, cr, orr, chh, ohh, ftiles, &nR, &nH));
     GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &b_st[0]));
     GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &h_st));
     hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
-                       ks.canonical, p4_lo, p4_hi, pns, nullptr, nullptr, orr, ohh, b_st[0], h_st);
+                       ks.canonical, p4_lo, p4_hi, pns, cr, chh, orr, ohh, b_st[0], h_st);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     const uint64_t nB = nR + nH;

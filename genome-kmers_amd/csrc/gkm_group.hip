@@ -413,6 +413,47 @@ __global__ __launch_bounds__(256) void filter_flags_kernel(const uint8_t *__rest
     }
 }
 
+// The built-in filters depend on the sba window at a start only, so they are evaluated once per
+// POSITION, streaming the sba (neighbouring threads read overlapping windows from the caches), into
+// 2 bits per position: word w covers positions 32 w .. 32 w + 31, bit j = passes, bit 32 + j =
+// raises.  The sorted-order flags then gather one bit pair per k-mer from L / 4 bytes (a GRCh38-size
+// table mostly held by the Infinity Cache) instead of a random ~31-byte window per k-mer: ~100x
+// fewer HBM line fetches.  A raising k-mer re-runs dev_filter for its code, so the error (the
+// lowest raising sorted index) is the one filter_flags_kernel reports.
+__global__ __launch_bounds__(256) void filter_pos_kernel(const uint8_t *__restrict__ sba, uint64_t L, int kind,
+                                                         int64_t p0, int64_t p1, int64_t p2,
+                                                         uint64_t *__restrict__ words) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = blockIdx.x * 256ull + (threadIdx.x & ~63u); base < L; base += step) {  // wave-uniform
+        const uint64_t p = base + lane;
+        const int r = p < L ? dev_filter(sba, L, kind, p0, p1, p2, p, nullptr, 0) : 0;
+        const uint64_t pass = __ballot(r > 0), raise = __ballot(r < 0);
+        if (lane < 2) {
+            const uint32_t sh = 32 * lane;
+            words[(base >> 5) + lane] = ((pass >> sh) & 0xFFFFFFFFull) | (((raise >> sh) & 0xFFFFFFFFull) << 32);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void filter_gather_kernel(const uint64_t *__restrict__ words,
+                                                            const uint32_t *__restrict__ starts, uint64_t n,
+                                                            const uint8_t *__restrict__ sba, uint64_t L, int kind,
+                                                            int64_t p0, int64_t p1, int64_t p2,
+                                                            uint8_t *__restrict__ flags,
+                                                            unsigned long long *__restrict__ err) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = starts[i];
+        const uint64_t w = words[s >> 5];
+        const uint32_t b = s & 31;
+        flags[i] = (uint8_t)((w >> b) & 1);
+        if ((w >> (32 + b)) & 1) {
+            const int r = dev_filter(sba, L, kind, p0, p1, p2, s, nullptr, i);
+            atomicMin(err, ((unsigned long long)i << 8) | (unsigned long long)(-r));
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // group heads: q == 0 || k-mer(q-1) != k-mer(q) under compare_sba_kmers_lexicographically(kmer_len)
 // ---------------------------------------------------------------------------------------------
@@ -569,9 +610,22 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
         GK_TRY_HIP(c, hipMemcpyAsync(c->scalars + 1, &init, 8, hipMemcpyHostToDevice, c->stream));
         int slot;
         timer_begin(c, "filter", &slot);
-        hipLaunchKernelGGL(filter_flags_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, c->sba, c->sba_len, starts,
-                           n, kind, filter->p0, filter->p1, filter->p2, c->mask, c->flags,
-                           reinterpret_cast<unsigned long long *>(c->scalars + 1));
+        // per position, then gathered (filter_pos_kernel); a mask is per sorted index, and
+        // GKM_FILTER_PER_KMER=1 (A/B) evaluates every k-mer's window in sorted order
+        static const bool per_kmer = std::getenv("GKM_FILTER_PER_KMER") != nullptr;
+        if (kind != GK_FILTER_MASK && !per_kmer && c->sba_len > 0) {
+            uint64_t *words;
+            GK_TRY_HIP(c, scratch(c, "filter_pos", (c->sba_len + 63) / 64 * 2, &words));
+            hipLaunchKernelGGL(filter_pos_kernel, dim3(grid_for((c->sba_len + 255) / 256 * 256, 16384)), dim3(256), 0,
+                               c->stream, c->sba, c->sba_len, kind, filter->p0, filter->p1, filter->p2, words);
+            hipLaunchKernelGGL(filter_gather_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, words, starts, n,
+                               c->sba, c->sba_len, kind, filter->p0, filter->p1, filter->p2, c->flags,
+                               reinterpret_cast<unsigned long long *>(c->scalars + 1));
+        } else {
+            hipLaunchKernelGGL(filter_flags_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream, c->sba, c->sba_len,
+                               starts, n, kind, filter->p0, filter->p1, filter->p2, c->mask, c->flags,
+                               reinterpret_cast<unsigned long long *>(c->scalars + 1));
+        }
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         unsigned long long err = 0;

@@ -344,6 +344,48 @@ def test_custom_python_filter_is_honoured():
     assert got == want
 
 
+FILTER_SPECS = [
+    {"kind": "homopolymer", "max_homopolymer_size": 3, "kmer_len": 31},
+    {"kind": "homopolymer", "max_homopolymer_size": 4, "kmer_len": 40},  # past some '$': raises
+    {"kind": "gc", "min_gc": 0.35, "max_gc": 0.6, "kmer_len": 31},
+    {"kind": "gc", "min_gc": 0.3, "max_gc": 0.7, "kmer_len": 36},  # raises (segment end)
+    {"kind": "no_ambiguous", "kmer_len": 31},
+    {"kind": "no_ambiguous", "kmer_len": 33},  # raises (segment end)
+    {"kind": "length", "min_kmer_len": 31},
+    {"kind": "crispr_ngg"},
+]
+
+
+@pytest.mark.parametrize("spec", FILTER_SPECS, ids=lambda s: "-".join(str(v) for v in s.values()))
+def test_builtin_filters_per_position_vs_oracle(spec):
+    """The built-in filters are evaluated once per sba position and gathered into sorted order
+    (gkm_group.hip filter_pos_kernel): histograms, totals, yields and the raised error (its type
+    and sba index: the first raising k-mer in sorted order) against the oracle's group scan over
+    the same sorted starts, on an IUPAC sequence with N runs, several contigs and ragged ends."""
+    rng = np.random.default_rng(21)
+    rep = rng.choice(np.frombuffer(b"ACGTACGTGCCGGS", dtype=np.uint8), 900).astype(np.uint8)
+    seqs = random_genome(rng, [60_000, 41_003, 25_017], alphabet=b"ACGTACGTACGTACGTNRY", repeat=rep, copies=6)
+    seqs = [(n, s[:5000] + "N" * 700 + s[5000:]) for n, s in seqs]
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=31, max_kmer_len=31)
+    km.sort()
+    sba, st = sc.forward_sba, km.kmer_sba_start_indices
+    filt, params = filter_of(spec), oracle.filter_params(spec)
+    try:
+        want = oracle.group_scan(sba, st, 31, params, max_counts_bin=100)
+    except oracle.OracleError as e:
+        with pytest.raises((ValueError, IndexError)) as got:
+            km.get_kmer_group_counts(31, filt, max_counts_bin=100)
+        if "kmer_sba_start_idx" in str(got.value) or "sba index" in str(got.value):
+            assert str(e.idx) in str(got.value)
+        return
+    h, t = km.get_kmer_group_counts(31, filt, max_counts_bin=100)
+    assert h.tolist() == want[0].tolist() and int(t) == want[1]
+    ys = oracle.group_scan(sba, st, 31, params, min_group_size=2, yield_first_n=2)
+    got = list(km.get_kmers(31, kmer_filter_func=filt, min_group_size=2, yield_first_n=2))
+    assert got == ys
+
+
 def test_unique_counts_match_groups():
     rng = np.random.default_rng(13)
     rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 700).astype(np.uint8)

@@ -246,6 +246,34 @@ def test_compact_level_with_big_sub_buckets_vs_oracle(compact, monkeypatch):
     assert t == ot
 
 
+# Compact buckets of C3's wave class (257..512 k-mers): with a 6-bit L1 the compact level leaves
+# buckets of ~490 k-mers for msd_wave_kernel<8> (C3's ~370 are in the same class), plus a periodic
+# run whose sub-buckets outgrow the rank-by-count limit and are re-listed with rebuilt keys.
+def test_compact_wave_class_vs_oracle(monkeypatch):
+    monkeypatch.setenv("GKM_LEVEL_BITS", "7,6,8")
+    rng = np.random.default_rng(22)
+    seqs = random_genome(rng, [3_000_000, 1_000_000])
+    seqs.append(("periodic", "ACGTTGCA" * 5_000 + "AACCGGTTAC" * 3_000))
+    k = 21
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    eng = km._get_engine()
+    eng.profile_enable(True)
+    km.sort()
+    rep = str(eng.profile_report())
+    eng.profile_enable(False)
+    assert "msd_pass_l1c" in rep and "msd_local_wave8" in rep
+    unsorted = oracle.enumerate_starts(sc.forward_sba, sc._forward_sba_seg_starts, k)
+    want = oracle.quicksort(sc.forward_sba, unsorted, k, k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    spec = oracle.key_spec(True, k, k)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+    h, t = km.get_kmer_group_counts(k, max_counts_bin=64)
+    oh, ot = oracle.group_scan(sc.forward_sba, want, k, max_counts_bin=64)
+    np.testing.assert_array_equal(h, oh)
+    assert t == ot
+
+
 def test_iupac_k31_vs_oracle():
     rng = np.random.default_rng(4)
     oracle_check(random_genome(rng, [120_000, 60_000], alphabet=b"ACGTACGTACGTNRY"), 31, 31)

@@ -345,6 +345,8 @@ def main():
     seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
 
     range_mode = dist is not None and args.exchange == "range"
+    # the last global level was compact: the wave-local round reads 9 B per element, not 12
+    compact_in = any(n.startswith("msd_pass_l") and n.endswith("c") for n in report)
 
     def stage_bytes(name, v):
         u = v.get("units", 0)
@@ -359,7 +361,9 @@ def main():
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out
         if name.startswith("msd_local"):
-            return 25 * u  # (key, start) in; key, start and 1 head flag out
+            # (key 8 B, start 4 B) in -- or, behind a compact level, (low bits | start) 8 B + digit
+            # byte 1 B; key, start and 1 head flag out
+            return (22 if compact_in else 25) * u
         if name == "msd_count":
             return 8 * u
         if name == "unique_counts":

@@ -1255,12 +1255,15 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
 // counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
 // in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
 // -- the ranks are stable.  About 12 VALU per item instead of about 50.
+// The re-list lists are read through a pointer (lists_store_kernel's device copy), only on the rare
+// re-list path: 16 list pointers held as kernel arguments kept ~50 SGPRs live over the bucket loop
+// (<8,5>: 69 -> 22 SGPR spills to VGPR lanes, each a v_writelane / v_readlane).
 template <int I, int MINW = 1>
 __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
-                                                      const uint32_t *v1, uint8_t *__restrict__ heads, Lists L,
-                                                      uint32_t *__restrict__ ctr, int skip, uint32_t small, int wkeys,
-                                                      CompactIn ci) {
+                                                      const uint32_t *v1, uint8_t *__restrict__ heads,
+                                                      const Lists *__restrict__ Lp, uint32_t *__restrict__ ctr,
+                                                      int skip, uint32_t small, int wkeys, CompactIn ci) {
     constexpr int CAP = 64 * I;
     __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
     // digit masks (256), and the staged starts (CAP + 1 uint32) of the write-back
@@ -1411,7 +1414,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
             for (int i = 0; i < I; ++i) {
                 const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
                 const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : 0;
-                route((uint32_t)st + slot[i], size, nhi, B, 0, false, L, ctr, lane);
+                route((uint32_t)st + slot[i], size, nhi, B, 0, false, *Lp, ctr, lane);
             }
         }
         // write-back staged through LDS: every element goes to its final slot (the keys' slots are
@@ -1444,6 +1447,9 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
         for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;  // the digit masks of the next bucket
     }
 }
+
+// one round's lists, copied to device memory for the wave kernels
+__global__ void lists_store_kernel(Lists L, Lists *__restrict__ dst) { *dst = L; }
 
 // Buckets of <= kTiny elements (mostly from the tie groups of multi-word keys): one thread per
 // bucket, stable rank-by-count over the full word (ties: load order = start order), write-back of
@@ -2398,7 +2404,7 @@ struct MsdDriver {
 
     // one local class's kernel over a list of cnt buckets
     void local_launch(int k, uint32_t cnt, const uint2 *lst, uint64_t *k0, uint32_t *v0, const uint64_t *k1,
-                      const uint32_t *v1, const Lists &nl, int round) {
+                      const uint32_t *v1, const Lists &nl, const Lists *d_nl, int round) {
         // common-prefix skip: re-listed buckets, later phases (repeats) and the block class; not
         // the first wave round of phase 0, where random keys differ right below the sorted bits
         const int skip = (round > 0 || phase > 0 || k == 3) ? 1 : 0;
@@ -2417,21 +2423,21 @@ struct MsdDriver {
         switch (k) {
         case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)
             hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
             break;
         case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
                  // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
             if (wave_occ() == 4)
                 hipLaunchKernelGGL((msd_wave_kernel<8, 4>), grid((const void *)msd_wave_kernel<8, 4>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
             else
                 hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
             break;
         case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
                  // on C5 (A/B, one box)
             hipLaunchKernelGGL((msd_wave_kernel<16, 3>), grid((const void *)msd_wave_kernel<16, 3>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, small, wkeys, ci);
+                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),
@@ -2463,6 +2469,10 @@ struct MsdDriver {
             // the re-list counters of this round start from 0 (the done count carries on)
             GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrLoc, 0, 4 * kLocal, c->stream));
             const Lists nl = lists(ng, 0);
+            Lists *d_nl = nullptr;
+            GK_TRY_HIP(c, scratch(c, "lists_dev", 1, &d_nl));
+            hipLaunchKernelGGL(lists_store_kernel, dim3(1), dim3(1), 0, c->stream, nl, d_nl);
+            GK_TRY_HIP(c, hipGetLastError());
             for (int k = 0; k < kLocal; ++k) {
                 if (!nloc[k]) continue;
                 timer_begin(c, round == 0 ? kLocTimer[k][0] : kLocTimer[k][1], &slot);
@@ -2478,7 +2488,7 @@ struct MsdDriver {
                     hipEventCreate(&t1);
                     hipEventRecord(t0, c->stream);
                 }
-                local_launch(k, cnt, lst, k0, v0, k1, v1, nl, round);
+                local_launch(k, cnt, lst, k0, v0, k1, v1, nl, d_nl, round);
                 GK_TRY_HIP(c, hipGetLastError());
                 timer_end(c, slot);
                 if (trace) {  // diagnostics: one line per local launch

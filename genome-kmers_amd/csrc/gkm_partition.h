@@ -315,19 +315,33 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
     lds_barrier();
     const uint64_t b = t_start[blockIdx.x];
     const uint32_t m = t_count[blockIdx.x];
-    // 4 digits per load where the run is 4-byte aligned, bytes at the ragged ends
-    const uint32_t head = min<uint32_t>((uint32_t)((4 - (b & 3)) & 3), m);
-    const uint32_t words = (m - head) >> 2;
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(nd + b + head);
+    // 16 digits per load where the run is 16-byte aligned (a tile's ~11 K digits: <= 3 loads per
+    // thread, all in flight together), bytes at the ragged ends
+    const uint32_t head = min<uint32_t>((uint32_t)((16 - ((uintptr_t)(nd + b) & 15)) & 15), m);
+    const uint32_t quads = (m - head) >> 4;
+    const uint4 *w = reinterpret_cast<const uint4 *>(nd + b + head);
     if (t < (int)head) atomicAdd(&s_hist[nd[b + t]], 1u);
-    for (uint32_t i = t; i < words; i += 256) {
-        const uint32_t x = w[i];
-        atomicAdd(&s_hist[x & 0xFF], 1u);
-        atomicAdd(&s_hist[(x >> 8) & 0xFF], 1u);
-        atomicAdd(&s_hist[(x >> 16) & 0xFF], 1u);
-        atomicAdd(&s_hist[x >> 24], 1u);
+    for (uint32_t i0 = 0; i0 < quads; i0 += 3 * 256) {
+        uint4 x4[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const uint32_t i = i0 + r * 256 + t;
+            x4[r] = i < quads ? w[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            if (i0 + r * 256 + t >= quads) continue;
+            const uint32_t xs[4] = {x4[r].x, x4[r].y, x4[r].z, x4[r].w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                atomicAdd(&s_hist[xs[u] & 0xFF], 1u);
+                atomicAdd(&s_hist[(xs[u] >> 8) & 0xFF], 1u);
+                atomicAdd(&s_hist[(xs[u] >> 16) & 0xFF], 1u);
+                atomicAdd(&s_hist[xs[u] >> 24], 1u);
+            }
+        }
     }
-    const uint32_t tail0 = head + 4 * words;
+    const uint32_t tail0 = head + 16 * quads;  // < 16 bytes left
     if (tail0 + t < m) atomicAdd(&s_hist[nd[b + tail0 + t]], 1u);
     lds_barrier();
     for (int i = t; i < RADIX; i += 256) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];

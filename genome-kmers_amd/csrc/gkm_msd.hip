@@ -372,8 +372,10 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     __shared__ uint32_t s_start[RADIX + 1];
     __shared__ uint32_t s_wsum[RADIX / 64 > 0 ? RADIX / 64 : 1];
     __shared__ uint8_t s_lut4[256];
+    __shared__ uint64_t s_mask[NW * RADIX];  // per-wave digit masks of the ranking (zero between uses)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
+    for (int i = tid; i < NW * RADIX; i += T) s_mask[i] = 0;
     // the first iteration's stores read buffer 1 before anything was staged (they go to the
     // sink): keep their positions inside the tile
     for (int i = tid; i < TILE + 2; i += T) s_pos[1][i] = 0;
@@ -448,7 +450,13 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             const bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
             validm |= (valid ? 1u : 0u) << i;
             const uint32_t dig = dg_of(l0_key_of<BITS, CANON>(s_code[b], p, a.total_bits, a.symbols), d0);
-            const uint64_t peers = match_peers<R>(dig, valid);
+            // peers by LDS mask (msd_wave_kernel's scheme): each valid lane ORs its bit into its
+            // digit's mask, reads it back and every lane zeroes it -- one wave's LDS operations
+            // complete in order.  Against R + 1 ballots per item: C3 L0 14.0 -> 12.9 ms (A/B)
+            uint64_t *mk = s_mask + wave * RADIX;
+            if (valid) atomicOr((unsigned long long *)&mk[dig], 1ull << lane);
+            const uint64_t peers = valid ? mk[dig] : 0ull;
+            mk[dig] = 0;
             const uint32_t rank_in = lanes_below(peers);
             const uint32_t old = wc[dig];
             if (valid && rank_in == 0) wc[dig] = old + (uint32_t)__popcll(peers);

@@ -272,7 +272,10 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     using P = L0Pack<BITS, TILE>;
     __shared__ uint64_t s_code[P::kCodeWords];
     __shared__ uint32_t s_dol[P::kGroups];
-    __shared__ uint32_t s_hist[RADIX];
+    // 4 interleaved histogram copies (digit d, copy c at 4 d + c; copy = thread & 3): the lanes of
+    // one atomic that share a digit land on 4 different words in 4 banks (C3: 1.845 -> 1.797 ms, A/B)
+    constexpr int NC = 4;
+    __shared__ uint32_t s_hist[RADIX * NC];
     __shared__ uint8_t s_lut4[256];
     const int t = threadIdx.x;
     if (t < 256) s_lut4[t] = c_code4_msd[t];
@@ -281,7 +284,10 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
     if (blockIdx.x < ntiles) l0_load<BITS, TILE, T>(a, a.lo + (uint64_t)blockIdx.x * TILE, rr);
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t P0 = a.lo + (uint64_t)tile * TILE;
-        for (int i = t; i < RADIX; i += T) s_hist[i] = 0;
+        // each thread zeroes the copies it summed for the previous tile (no barrier between)
+        for (int i = t; i < RADIX; i += T)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) s_hist[i * NC + c] = 0;
         lds_barrier();  // the LUT; the previous tile's histogram and codes have been read
         l0_pack<BITS, TILE, T>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
         lds_barrier();
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                 const uint32_t keepm = win8_keep(w, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i]], 1u);
+                    if ((keepm >> i) & 1u) atomicAdd(&s_hist[dig[i] * NC + (t & (NC - 1))], 1u);
             }
         } else {
             // canonical 2-bit keys in a tile without stops: the digit is the smaller of the forward
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                             const uint32_t v = (uint32_t)(tr >> (56 - 2 * i)) & 0xFFu;  // symbols q0+k-4+i ..
                             const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
                             const uint32_t d = min(f7, (~rv & 0xFFu) >> 1);
-                            if (l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+                            if (l0_owned(d, a)) atomicAdd(&s_hist[d * NC], 1u);
                         }
                     }
                 }
@@ -327,12 +333,17 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                 for (int i = 0; i < I; ++i) {
                     const uint32_t p = i * T + t;
                     const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
-                    if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d], 1u);
+                    if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d * NC], 1u);
                 }
             }
         }
         lds_barrier();
-        for (int i = t; i < RADIX; i += T) tile_hist[(uint64_t)tile * RADIX + i] = s_hist[i];
+        for (int i = t; i < RADIX; i += T) {
+            uint32_t h = 0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) h += s_hist[i * NC + c];
+            tile_hist[(uint64_t)tile * RADIX + i] = h;
+        }
     }
 }
 

@@ -369,9 +369,16 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     static_assert(TILE < 65536, "tile positions are staged as u16");
     constexpr int RADIX = 1 << R;
     constexpr int NW = T / 64;
-    // store groups of the previous tile: 2 after the packing, one per ranked item, 2 during the
-    // scan, the rest after the staging
-    constexpr int G_TOP = 2, G_SCAN = 2;
+    // store groups of the previous tile: G_TOP after the packing, one per ranked item, G_SCAN
+    // during the scan, the rest after the staging
+#ifndef GKM_L0_GTOP
+#define GKM_L0_GTOP 1
+#endif
+#ifndef GKM_L0_GSCAN
+#define GKM_L0_GSCAN 2
+#endif
+    // (tuning overrides, tools/gpu_ab_l0_groups.sh: G_TOP 1 beat 0, 2 and 4 by 0.2-0.6 ms at C3)
+    constexpr int G_TOP = GKM_L0_GTOP, G_SCAN = GKM_L0_GSCAN;
     constexpr int G_RANK = I - G_TOP - G_SCAN - 2 > 0 ? I - G_TOP - G_SCAN - 2 : 0;
     using P = L0Pack<BITS, TILE>;
     static_assert(T >= RADIX, "one thread per digit");

@@ -13,6 +13,7 @@
 #include <map>
 
 #include "gkm_internal.h"
+#include "gkm_partition.h"
 
 namespace gkm {
 
@@ -239,6 +240,75 @@ extern "C" int gk_device_count(int *count) {
     return e == hipSuccess ? GK_OK : GK_E_HIP;
 }
 
+// Every partition of the sort ranks an item by one returning LDS atomic (rank_atomic,
+// gkm_partition.h): it relies on the LDS applying the same-address lanes of one wave instruction in
+// increasing lane order.  That is how gfx950 behaves (tools/lds_rank_probe.hip: no exception in
+// 4e10 lane-ranks), not an ISA guarantee, so it is checked once per device and process against a
+// ballot-match ground truth -- 256, 64, 16, 4 and 1 random digits, 4 items per trial,
+// every CU busy -- and a device where it does not hold is refused (a wrong order would otherwise
+// be silent).
+__global__ __launch_bounds__(256) void lds_rank_check_kernel(uint32_t trials, unsigned long long *bad) {
+    __shared__ uint32_t s_cnt[4][256];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t *cnt = s_cnt[wave];
+    unsigned long long nb = 0;
+    for (uint32_t t = 0; t < trials; ++t) {
+        const uint32_t dmask = 0xFFu >> (2 * (t % 5));  // 256, 64, 16, 4 and 1 digits
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cnt[u * 64 + lane] = 0;
+        uint32_t dd[4], got[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t x = (blockIdx.x * 0x9E3779B9u) ^ (t * 0x85EBCA6Bu) ^ ((uint32_t)(i * 64 + lane) * 0xC2B2AE35u);
+            x ^= x >> 15;
+            x *= 0x2C1B3C6Du;
+            x ^= x >> 12;
+            dd[i] = x & dmask;
+            got[i] = rank_atomic(cnt, dd[i], ((x >> 20) & 7u) != 0);  // some lanes sit out
+            if (((x >> 20) & 7u) == 0) got[i] = ~0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool valid = got[i] != ~0u;
+            // ground truth: valid lanes with the same digit below this lane, and in earlier items
+            uint32_t want = 0;
+            for (int j = 0; j <= i; ++j) {
+                uint64_t m = __ballot(got[j] != ~0u);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const uint64_t x = __ballot((dd[j] >> b) & 1u);
+                    m &= ((dd[i] >> b) & 1u) ? x : ~x;
+                }
+                want += (uint32_t)__popcll(j < i ? m : (m & ((1ull << lane) - 1ull)));
+            }
+            nb += valid && got[i] != want;
+        }
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+
+static int lds_rank_check(int device) {
+    static int state[64] = {0};  // per device: 0 unchecked, 1 holds, -1 does not
+    if (device < 0 || device >= 64) return GK_E_ARG;
+    if (state[device] != 0) return state[device] > 0 ? GK_OK : GK_E_UNSUPPORTED;
+    unsigned long long *d = nullptr, h = 0;
+    if (hipMalloc(&d, 8) != hipSuccess) return GK_E_HIP;
+    hipError_t e = hipMemset(d, 0, 8);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(lds_rank_check_kernel, dim3(2048), dim3(256), 0, 0, 40u, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return GK_E_HIP;
+    state[device] = h == 0 ? 1 : -1;
+    if (h)
+        std::fprintf(stderr, "libgkm: device %d: a returning LDS atomic did not apply same-address lanes in lane "
+                             "order (%llu of ~1e8 ranks differ); the stable partitions need it -- device refused\n",
+                     device, h);
+    return h == 0 ? GK_OK : GK_E_UNSUPPORTED;
+}
+
 extern "C" int gk_create(gk_ctx **out, int device) {
     if (!out) return GK_E_ARG;
     *out = nullptr;
@@ -246,6 +316,7 @@ extern "C" int gk_create(gk_ctx **out, int device) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GK_E_HIP;
     if (device < 0 || device >= ndev) return GK_E_ARG;
     if (hipSetDevice(device) != hipSuccess) return GK_E_HIP;
+    if (int rc = lds_rank_check(device)) return rc;
     gk_ctx *c = new gk_ctx();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -264,7 +335,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
-                    c->dhist, c->mask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
+                    c->dhist, c->mask, c->hmask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
         if (b) hipFree(b);
     for (auto &e : c->scratch)
@@ -781,6 +852,15 @@ extern "C" int gk_set_filter_mask(gk_ctx *c, const uint8_t *mask, uint64_t n) {
     if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->mask, mask, n, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     c->mask_n = n;
+    return GK_OK;
+}
+
+extern "C" int gk_set_group_heads(gk_ctx *c, const uint8_t *heads, uint64_t n) {
+    if (!c) return GK_E_ARG;
+    GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->hmask), &c->hmask_cap, n + 64));
+    if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->hmask, heads, n, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    c->hmask_n = n;
     return GK_OK;
 }
 

@@ -566,6 +566,15 @@ __global__ __launch_bounds__(256) void group_yield_write_kernel(const uint32_t *
     }
 }
 
+// group heads of the valid k-mers from a host head mask (GK_GROUPS_FROM_HEADS): head of valid
+// k-mer q = the mask at its position; the first valid k-mer starts group 0
+__global__ __launch_bounds__(256) void heads_from_mask_kernel(const uint8_t *__restrict__ hmask,
+                                                              const uint32_t *__restrict__ cidx, uint64_t cnt,
+                                                              uint8_t *__restrict__ out) {
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < cnt; q += (uint64_t)gridDim.x * blockDim.x)
+        out[q] = q == 0 ? 1 : (hmask[cidx ? cidx[q] : q] != 0);
+}
+
 __global__ __launch_bounds__(256) void unique_counts_kernel(const uint32_t *__restrict__ gstart, uint64_t G,
                                                             uint64_t count, uint32_t *__restrict__ counts) {
     for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x)
@@ -649,6 +658,17 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
         return GK_OK;
     }
 
+    // groups a caller's comparison decided (a custom kmer_comparison_func)
+    if (is_sorted == GK_GROUPS_FROM_HEADS) {
+        if (c->hmask_n != n) return fail(c, GK_E_ARG, "group head mask length differs from the k-mer count");
+        hipLaunchKernelGGL(heads_from_mask_kernel, dim3(grid_for(cnt)), dim3(256), 0, c->stream, c->hmask, cidx, cnt,
+                           c->flags);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t g = 0;
+        GK_TRY_HIP(c, select_flags(c, c->flags, cnt, c->idx_b, &g));
+        *G = g;
+        return GK_OK;
+    }
     // canonical k-mers have no prefixes: groups exist at the sort length only
     if (is_sorted && c->canonical && (kmer_len < 0 || (uint64_t)kmer_len != c->sort_len))
         return fail(c, GK_E_UNSUPPORTED, "canonical k-mers are grouped at kmer_len == the sort length only");

@@ -128,6 +128,8 @@ struct gk_ctx {
     uint64_t dhist_cap = 0;
     uint8_t *mask = nullptr;
     uint64_t mask_cap = 0, mask_n = 0;
+    uint8_t *hmask = nullptr;  // gk_set_group_heads
+    uint64_t hmask_cap = 0, hmask_n = 0;
     uint32_t *ranks = nullptr;      // doubling: rank per sba position
     uint64_t ranks_cap = 0;
     uint32_t *ym = nullptr, *yoff = nullptr, *oy = nullptr, *ot = nullptr;  // generator yields

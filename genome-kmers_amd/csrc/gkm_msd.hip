@@ -39,6 +39,12 @@ constexpr int kBlockMax = kBT * kBI;    // 4096
 constexpr int kLocal = 5;                // 4 = tiny (<= kTiny elements: one thread per bucket)
 constexpr int kTiny = 8;
 constexpr int kSmall = 24;
+// waves per SIMD the wave-local kernels' registers are capped for (msd_wave_kernel<I, W, .>); the
+// LDS (7.2 KB per wave at I = 8) admits 5 per SIMD
+#ifndef GKM_WAVE_OCC8
+#define GKM_WAVE_OCC8 5
+#endif
+constexpr int kWaveOcc4 = 6, kWaveOcc8 = GKM_WAVE_OCC8, kWaveOcc16 = 3;
 // later local rounds (buckets re-listed because a sub-bucket outgrew kSmall: repeat families) and
 // later phases finish sub-buckets of up to kSmallLate by rank-by-count instead of re-listing them
 // for another round -- a round costs a bucket load, ranking and write-back per bucket
@@ -390,10 +396,8 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     __shared__ uint32_t s_start[RADIX + 1];
     __shared__ uint32_t s_wsum[RADIX / 64 > 0 ? RADIX / 64 : 1];
     __shared__ uint8_t s_lut4[256];
-    __shared__ uint64_t s_mask[NW * RADIX];  // per-wave digit masks of the ranking (zero between uses)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
-    for (int i = tid; i < NW * RADIX; i += T) s_mask[i] = 0;
     // the first iteration's stores read buffer 1 before anything was staged (they go to the
     // sink): keep their positions inside the tile
     for (int i = tid; i < TILE + 2; i += T) s_pos[1][i] = 0;
@@ -468,17 +472,9 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             const bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
             validm |= (valid ? 1u : 0u) << i;
             const uint32_t dig = dg_of(l0_key_of<BITS, CANON>(s_code[b], p, a.total_bits, a.symbols), d0);
-            // peers by LDS mask (msd_wave_kernel's scheme): each valid lane ORs its bit into its
-            // digit's mask, reads it back and every lane zeroes it -- one wave's LDS operations
-            // complete in order.  Against R + 1 ballots per item: C3 L0 14.0 -> 12.9 ms (A/B)
-            uint64_t *mk = s_mask + wave * RADIX;
-            if (valid) atomicOr((unsigned long long *)&mk[dig], 1ull << lane);
-            const uint64_t peers = valid ? mk[dig] : 0ull;
-            mk[dig] = 0;
-            const uint32_t rank_in = lanes_below(peers);
-            const uint32_t old = wc[dig];
-            if (valid && rank_in == 0) wc[dig] = old + (uint32_t)__popcll(peers);
-            dr[i] = dig | ((old + rank_in) << 8);
+            // stable rank by one returning LDS atomic (rank_atomic, gkm_partition.h); the LDS-mask
+            // round trip it replaces took C3 L0 14.0 -> 12.9 ms against R + 1 ballots per item
+            dr[i] = dig | (rank_atomic(wc, dig, valid) << 8);
             if (i < G_RANK) store_group(G_TOP + i);
             __builtin_amdgcn_sched_barrier(0);  // one item at a time (register pressure, see above)
         }
@@ -493,12 +489,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
                 s_wc[w * RADIX + tid] = total;
                 total += v;
             }
-            incl = total;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off);
-                if (lane >= off) incl += y;
-            }
+            incl = wave_incl_scan(total);
             if (lane == 63) s_wsum[wave] = incl;
         }
 #pragma unroll
@@ -912,17 +903,20 @@ __device__ __forceinline__ int list_of(uint32_t size, int hi, int B, bool allow_
 // entry `at` of list l for a sub-bucket
 __device__ __forceinline__ void put_entry(const Lists &L, int l, uint32_t at, uint32_t st, uint32_t size, int hi,
                                           int parity, uint64_t pref = 0) {
+    // (global stores: flat ones, through pointers read from memory, would make every later
+    // memory wait of the kernel a full drain)
     if (l == kCtrBig) {
-        L.nb_start[at] = st;
-        L.nb_len[at] = size;
-        if (L.nb_pref) L.nb_pref[at] = pref;
+        gmem(L.nb_start)[at] = st;
+        gmem(L.nb_len)[at] = size;
+        if (L.nb_pref) gmem(L.nb_pref)[at] = pref;
     } else if (l == kCtrDone) {
-        L.dn_start[at] = st;
-        L.dn_len[at] = size;
-        L.dn_par[at] = (uint8_t)parity;
+        gmem(L.dn_start)[at] = st;
+        gmem(L.dn_len)[at] = size;
+        gmem(L.dn_par)[at] = (uint8_t)parity;
     } else {
-        L.loc[l - kCtrLoc][at] = local_entry(st, size, hi, parity);
-        if (L.loc_pref[l - kCtrLoc]) L.loc_pref[l - kCtrLoc][at] = pref;
+        const uint2 le = local_entry(st, size, hi, parity);
+        gmem(reinterpret_cast<uint64_t *>(L.loc[l - kCtrLoc]))[at] = ((uint64_t)le.y << 32) | le.x;
+        if (L.loc_pref[l - kCtrLoc]) gmem(L.loc_pref[l - kCtrLoc])[at] = pref;
     }
 }
 
@@ -1151,14 +1145,12 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     __shared__ uint8_t s_hd[TILE + 1];
     __shared__ uint32_t s_any;
     __shared__ uint64_t s_kf, s_or;                  // common-prefix skip: first key, OR of differences
-    __shared__ uint64_t s_mask[SM::kWaves * RADIX];  // ranking masks (zero between uses)
     uint64_t *s_k = reinterpret_cast<uint64_t *>(s_raw);
     uint32_t *s_v = reinterpret_cast<uint32_t *>(s_raw + SM::kValOff);
     uint32_t *s_wc = reinterpret_cast<uint32_t *>(s_raw);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t idx = blockIdx.x;
     if (idx >= count) return;
-    for (int i = tid; i < SM::kWaves * RADIX; i += T) s_mask[i] = 0;
     uint2 e = list[idx];
     uint64_t pf = ci.pref ? ci.pref[idx] : 0;
     uint64_t key[I];
@@ -1204,7 +1196,7 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
         // items of this wave holding elements (wave-uniform)
         const int wbase = wave * (I * 64);
         const int live = (int)len > wbase ? min(I, ((int)len - wbase + 63) >> 6) : 0;
-        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live, s_mask);
+        partition_stage<T, I, R>(key, val, valid, dd, s_raw, nullptr, s_wsum, s_start, slot, nullptr, live);
 
         // 2. final position and head flag of every element
         uint32_t out[I];
@@ -1274,29 +1266,70 @@ __global__ __launch_bounds__(T) void msd_local_kernel(const uint2 *__restrict__ 
     }
 }
 
-// Single-wave finishing kernel for buckets of <= 256 elements (the common case: ~185 at C3).
-// Same contract as msd_local_kernel<64, 4, 8>, with a cheaper stable ranking: instead of 8
-// ballots per item, each lane ORs its bit into an LDS mask of its digit, reads the mask back
-// (its peers) and zeroes it; the first peer of each item adds the item's count to the digit's
-// counter with a returning LDS atomic, and broadcasts the old value.  LDS ops of one wave complete
-// in order, so item i's mask holds item i's lanes only and the counters accumulate in item order
-// -- the ranks are stable.  About 12 VALU per item instead of about 50.
-// The re-list lists are read through a pointer (lists_store_kernel's device copy), only on the rare
-// re-list path: 16 list pointers held as kernel arguments kept ~50 SGPRs live over the bucket loop
-// (<8,5>: 69 -> 22 SGPR spills to VGPR lanes, each a v_writelane / v_readlane).
-template <int I, int MINW = 1>
+// list entry j of a wave class (scalar loads) and its prefix (0: not recorded)
+__device__ __forceinline__ void wave_entry(const uint2 *__restrict__ list, const uint64_t *__restrict__ cpref,
+                                           uint32_t j, uint2 &e, uint64_t &pf) {
+    e = list[j];
+    pf = cpref ? cpref[j] : 0ull;
+}
+
+// raw elements of a wave-class bucket: compact (x = low << 32 | start, next-digit byte) or full
+// (key, start).  Branch-free, one instruction per word, so the compiler's count of loads and
+// stores in flight stays static and the bucket loop never drains its stores: the second word is a
+// 4-byte load either way -- of the start, or unaligned at the digit byte (its low byte; the digit
+// array is padded past n).  Buffers chosen by integer selects (pointer selects between kernel
+// arguments went through the stack as flat loads).  Loads clamped to the bucket.
+template <int I>
+__device__ __forceinline__ void wave_load(const uint2 e, uint64_t pf, int lane, const uint64_t *k0, const uint64_t *k1,
+                                          const uint32_t *v0, const uint32_t *v1, const uint8_t *cnd,
+                                          uint64_t (&a)[I], uint32_t (&b)[I]) {
+    const uint64_t st = e.x;
+    const uint32_t len = e.y >> 8;
+    const bool p1 = (e.y & 1) != 0, cmp = (pf & kCompact) != 0;
+    const uint64_t kb = p1 ? (uint64_t)k1 : (uint64_t)k0;
+    const uint64_t bb = cmp ? (uint64_t)cnd : (p1 ? (uint64_t)v1 : (uint64_t)v0);
+    const int sh = cmp ? 0 : 2;
+    uint32_t q = lane;
+    asm volatile("" : "+v"(q));
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+        const uint64_t at = st + min(q + i * 64, len - 1);
+        a[i] = *reinterpret_cast<gu64 *>(kb + 8 * at);
+        b[i] = *reinterpret_cast<gu32u *>(bb + (at << sh));
+    }
+}
+
+// Single-wave finishing kernel for buckets of <= 64 I elements (C3: ~370 keys behind the compact
+// level, class 1).  Per bucket, one wave:
+//   keys   compact entries (a compact level's output): key = prefix | next-digit byte | low bits
+//          (compact_key); full entries: (key, start) as stored
+//   rank   the next 8-bit digit of every element, ranked by ONE returning LDS atomic per item
+//          (rank_atomic: stable); the 256 digit counts are scanned 4 per lane (wave_incl_scan)
+//   order  each digit's elements take its slots in stable order; the key bits below the digit are
+//          staged at those slots, and a sub-bucket of 2..small elements is ordered by
+//          rank-by-count over them (ties: staging order = start order); larger sub-buckets are
+//          re-listed for another round; a sub-bucket whose key bits are exhausted is final
+//   write  keys (the group-head flag in bit 63 when B < 64) and starts staged at their final slots,
+//          then stored contiguously: keys, starts and head flags of the whole bucket
+// The NEXT bucket's elements are loaded at the top of the current one, so they fly during its
+// whole ranking and write-back (round 2 issued them just before the write-back); the write-back is
+// branch-free with a static store count (slots clamped to the bucket), so the next iteration waits
+// for those loads without draining the stores.  The list entries and prefixes are scalar loads two
+// buckets ahead.  LDS per wave: staged keys (aliased by the low bits of the ranking: one wave's LDS
+// operations complete in order), staged starts, digit counts -- 7.2 KB at I = 8.
+// WK: keys are written back (one-word sorts); otherwise only for buckets with re-listed elements.
+template <int I, int MINW, bool WK>
 __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads,
                                                       const Lists *__restrict__ Lp, uint32_t *__restrict__ ctr,
-                                                      int skip, uint32_t small, int wkeys, CompactIn ci) {
+                                                      int skip, uint32_t small, const uint64_t *__restrict__ cpref,
+                                                      const uint8_t *__restrict__ cnd) {
     constexpr int CAP = 64 * I;
-    __shared__ uint64_t s_k[CAP + 1];  // slot CAP: sink
-    // digit masks (256), and the staged starts (CAP + 1 uint32) of the write-back
-    __shared__ uint64_t s_mask[(CAP + 2) / 2 > 256 ? (CAP + 2) / 2 : 256];
-    __shared__ uint32_t s_cnt[257];  // digit counts, then exclusive starts (s_cnt[256] = total)
+    __shared__ uint64_t s_k[CAP + 1];  // staged keys (slot CAP: sink); the low bits while ranking
+    __shared__ uint32_t s_v[CAP + 1];  // staged starts
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[260];  // digit counts -> starts; [256] = len
     const int lane = threadIdx.x;
-    const uint64_t me_bit = 1ull << lane;
     // XCD-aware walk (grid a multiple of 8): workgroup b takes the (b % 8)-th eighth of the list,
     // so the list's neighbouring buckets -- neighbours in memory, since classify appends a level's
     // sub-buckets in runs of address order -- are finished at about the same time on one XCD and
@@ -1309,21 +1342,43 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
         lstep = gridDim.x >> 3;
     }
     if (idx >= lend) return;
+    // keys and starts of a bucket from its raw elements
+    auto unpack = [B](const uint2 e, uint64_t pf, const uint64_t (&a)[I], const uint32_t (&b)[I], uint64_t (&key)[I],
+                      uint32_t (&val)[I]) {
+        const int hi0 = (e.y >> 1) & 127;
+        const bool cmp = (pf & kCompact) != 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;
-    uint2 e = list[idx];
-    uint64_t pf = ci.pref ? ci.pref[idx] : 0;
-    uint64_t key[I];
-    uint32_t val[I];
-    local_load<64, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);
+        for (int i = 0; i < I; ++i) {
+            key[i] = cmp ? compact_key(pf, hi0, B, b[i] & 0xFFu, (uint32_t)(a[i] >> 32)) : a[i];
+            val[i] = cmp ? (uint32_t)a[i] : b[i];
+        }
+    };
+    uint2 e, en;
+    uint64_t pf, pfn;
+    uint64_t key[I], a[I];
+    uint32_t val[I], b[I];
+    wave_entry(list, cpref, idx, e, pf);
+    wave_load<I>(e, pf, lane, k0, k1, v0, v1, cnd, a, b);
+    en = e;
+    pfn = pf;
+    if (idx + lstep < lend) wave_entry(list, cpref, idx + lstep, en, pfn);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    for (; idx < lend; idx += lstep) {
-        const uint2 ce = e;
-        const uint64_t st = ce.x;
-        const uint32_t len = ce.y >> 8;
-        int hi = (ce.y >> 1) & 127;
-        if (skip) {
-            const uint64_t kf = __shfl(key[0], 0);
+    unpack(e, pf, a, b, key, val);
+    for (;;) {
+        const uint64_t st = e.x;
+        const uint32_t len = e.y >> 8;
+        const int hi0 = (e.y >> 1) & 127;
+        // the next bucket's raw elements fly during this whole bucket; they are unpacked after its
+        // write-back (so the loop carries keys, not loads: no register copy waits for memory)
+        wave_load<I>(en, pfn, lane, k0, k1, v0, v1, cnd, a, b);  // after the last: itself again
+        uint2 enn = en;
+        uint64_t pfnn = pfn;
+        if (idx + 2 * lstep < lend) wave_entry(list, cpref, idx + 2 * lstep, enn, pfnn);
+
+        int hi = hi0;
+        if (skip) {  // common-prefix skip (later rounds and phases: repeats)
+            const uint64_t kf = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(key[0] >> 32), 0) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key[0], 0);
             uint64_t x = 0;
 #pragma unroll
             for (int i = 0; i < I; ++i)
@@ -1331,146 +1386,123 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
             hi = skip_hi(wave_or64(x), B, hi);
         }
         const Dig dd = dig_at(B, hi, 8);
-        const int nhi = hi + 8;
-        const bool last = nhi >= B;
-        if (idx + lstep < lend) {
-            e = list[idx + lstep];
-            pf = ci.pref ? ci.pref[idx + lstep] : 0;
-        }
-        const int live = min(I, (int)((len + 63) >> 6));
+        const bool last = hi + 8 >= B;                      // a sub-bucket's keys are equal
+        const uint64_t lowm = (1ull << dd.shift) - 1ull;    // key bits below the digit
+        const int live = min(I, (int)((len + 63) >> 6));    // items holding elements (wave-uniform)
 
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s_cnt[u * 64 + lane] = 0;
-        bool valid[I];
-        uint32_t dig[I];
-        uint64_t peers[I];
+        // 1. stable rank inside the digit
+        reinterpret_cast<uint4 *>(s_cnt)[lane] = make_uint4(0, 0, 0, 0);
+        uint32_t pk[I];  // rank | digit << 16, then rank << 21 | size << 10 | sub-bucket start
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            valid[i] = (uint32_t)(i * 64 + lane) < len;
-            dig[i] = dg_of(key[i], dd);
-            peers[i] = 0;
+            pk[i] = 0;
             if (i >= live) continue;
-            if (valid[i]) atomicOr((unsigned long long *)&s_mask[dig[i]], (unsigned long long)me_bit);
-            peers[i] = s_mask[dig[i]];
-            s_mask[dig[i]] = 0;  // every lane of the digit writes 0 after the wave's read
+            const uint32_t d = dg_of(key[i], dd);
+            pk[i] = rank_atomic(s_cnt, d, (uint32_t)(i * 64 + lane) < len) | (d << 16);
         }
-        uint32_t rank_in[I], old[I];
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            old[i] = 0;
-            rank_in[i] = lanes_below(peers[i]);
-            if (i < live && valid[i] && rank_in[i] == 0) old[i] = atomicAdd(&s_cnt[dig[i]], (uint32_t)__popcll(peers[i]));
-        }
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            if (i >= live) continue;
-            const int leader = valid[i] ? __ffsll((unsigned long long)peers[i]) - 1 : lane;
-            old[i] = __shfl(old[i], leader);
-        }
-        // exclusive starts over the 256 digits (4 per lane)
+        // 2. digit starts (exclusive scan of the 256 counts, 4 per lane); s_cnt[256] = len
         {
-            uint32_t c4[4], s4 = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                c4[u] = s_cnt[lane * 4 + u];
-                s4 += c4[u];
-            }
-            uint32_t incl = s4;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off);
-                if (lane >= off) incl += y;
-            }
-            uint32_t run = incl - s4;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                s_cnt[lane * 4 + u] = run;
-                run += c4[u];
-            }
-            if (lane == 63) s_cnt[256] = run;
+            const uint4 c = reinterpret_cast<const uint4 *>(s_cnt)[lane];
+            const uint32_t s4 = c.x + c.y + c.z + c.w;
+            const uint32_t incl = wave_incl_scan(s4);
+            const uint32_t r0 = incl - s4;
+            reinterpret_cast<uint4 *>(s_cnt)[lane] = make_uint4(r0, r0 + c.x, r0 + c.x + c.y, r0 + c.x + c.y + c.z);
+            if (lane == 63) s_cnt[256] = incl;
         }
-        uint32_t slot[I];
+        // 3. slots; the key bits below the digit staged there
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            slot[i] = CAP;
             if (i >= live) continue;
-            slot[i] = valid[i] ? s_cnt[dig[i]] + old[i] + rank_in[i] : (uint32_t)CAP;
-            s_k[slot[i]] = key[i];
+            const uint32_t d = pk[i] >> 16, r = pk[i] & 0xFFFFu;
+            const uint32_t sb = s_cnt[d], size = s_cnt[d + 1] - sb;
+            if ((uint32_t)(i * 64 + lane) < len) s_k[sb + r] = key[i] & lowm;
+            pk[i] = (r << 21) | (size << 10) | sb;
         }
-
-        // final position and head flag of every element (reads precede writes: one wave)
-        uint32_t out[I];
-        uint8_t hd[I];
+        // 4. final slot and group-head flag of every element
         bool any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            out[i] = slot[i];
-            hd[i] = 0;
             if (i >= live) continue;
-            const uint32_t sb = s_cnt[dig[i]], size = s_cnt[dig[i] + 1] - sb;
-            hd[i] = slot[i] == sb;
-            if (valid[i] && size > 1 && !last) {
-                if (size <= small) {
-                    const uint32_t me = slot[i] - sb;
-                    uint32_t lt = 0, eq = 0;
-                    // 4 keys per step (their LDS reads in flight together); indices past the
-                    // sub-bucket are clamped and not counted
-                    for (uint32_t j0 = 0; j0 < size; j0 += 4) {
-                        uint64_t kj[4];
+            const uint32_t sb = pk[i] & 0x3FFu, size = (pk[i] >> 10) & 0x7FFu, r = pk[i] >> 21;
+            uint32_t o = sb + r, h = 0;
+            if ((uint32_t)(i * 64 + lane) >= len) {
+                o = CAP;  // sink
+            } else if (size == 1) {
+                h = 1;
+            } else if (last) {
+                h = r == 0;  // equal keys, in start order
+            } else if (size > small) {
+                any = true;  // re-listed: the next round writes its order and heads
+            } else {
+                const uint64_t me = key[i] & lowm;
+                uint32_t lt = 0, eq = 0;
+                // rank-by-count over the sub-bucket, 4 staged values per step (reads in flight
+                // together; indices past the sub-bucket clamped and not counted)
+                for (uint32_t j0 = 0; j0 < size; j0 += 4) {
+                    uint64_t x[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) kj[u] = s_k[min(sb + j0 + u, (uint32_t)CAP)];
+                    for (int u = 0; u < 4; ++u) x[u] = s_k[min(sb + j0 + u, (uint32_t)CAP)];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const uint32_t j = j0 + u;
-                            lt += j < size && kj[u] < key[i];
-                            eq += j < me && kj[u] == key[i];
-                        }
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t j = j0 + u;
+                        lt += (j < size) & (x[u] < me);
+                        eq += (j < r) & (x[u] == me);
                     }
-                    out[i] = sb + lt + eq;
-                    hd[i] = eq == 0;
-                } else {
-                    hd[i] = 2;
-                    any = true;
                 }
+                o = sb + lt + eq;
+                h = eq == 0;
             }
+            pk[i] = o | (h << 16);
         }
         const bool relist = __ballot(any) != 0;
-        if (relist) {  // re-list the large sub-buckets (rare)
+        if (relist) {  // (rare) one entry per re-listed sub-bucket, from its first element
 #pragma unroll
             for (int i = 0; i < I; ++i) {
-                const bool first = valid[i] && hd[i] == 2 && slot[i] == s_cnt[dig[i]];
-                const uint32_t size = first ? s_cnt[dig[i] + 1] - s_cnt[dig[i]] : 0;
-                route((uint32_t)st + slot[i], size, nhi, B, 0, false, *Lp, ctr, lane);
+                uint32_t size = 0, at = 0;
+                if (i < live && (uint32_t)(i * 64 + lane) < len) {
+                    const uint32_t d = dg_of(key[i], dd);
+                    const uint32_t sb = s_cnt[d];
+                    size = s_cnt[d + 1] - sb;
+                    at = pk[i] & 0xFFFFu;
+                    if (size <= small || last || at != sb) size = 0;
+                }
+                route((uint32_t)st + at, size, hi + 8, B, 0, false, *Lp, ctr, lane);
             }
         }
-        // write-back staged through LDS: every element goes to its final slot (the keys' slots are
-        // read above, and one wave's LDS operations complete in order), then the wave stores the
-        // bucket contiguously -- full-line stores of keys, starts and head flags.  The head flag is
-        // "key differs from its predecessor" read from the sorted keys (a bucket starts a group).
-        // The starts are staged in the digit-mask array, all zero at this point.  The next
-        // bucket's loads are issued first so they fly during the stores.
-        uint32_t *s_v = reinterpret_cast<uint32_t *>(s_mask);
+        // 5. stage at the final slots (after every rank-by-count read of s_k: in order)
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            const uint32_t o = (i < live && valid[i]) ? out[i] : (uint32_t)CAP;
-            s_k[o] = key[i];
+            if (i >= live) continue;
+            const uint32_t o = pk[i] & 0xFFFFu;
+            s_k[o] = B < 64 ? key[i] | ((uint64_t)(pk[i] >> 16) << 63) : key[i];
             s_v[o] = val[i];
         }
-        local_load<64, I>(e, k0, v0, k1, v1, key, val, pf, &ci, B);  // the next bucket
-        const bool wk = relist || wkeys;  // keys: final-key sorts, or buckets with re-listed elements
+        // 6. write-back: contiguous, static count (slots past the bucket repeat its last element)
+        const bool wk = WK || relist;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            const uint32_t j = (uint32_t)(i * 64 + lane);
-            if (i < live && j < len) {
-                const uint64_t kj = s_k[j];
+            const uint32_t j = min((uint32_t)(i * 64 + lane), len - 1);
+            uint64_t kj = s_k[j];
+            const uint32_t vj = s_v[j];
+            uint8_t h;
+            if (B < 64) {
+                h = (uint8_t)(kj >> 63);
+                kj &= ~(1ull << 63);
+            } else {
                 const uint64_t kp = s_k[j > 0 ? j - 1 : 0];
-                if (wk) k0[st + j] = kj;
-                v0[st + j] = s_v[j];
-                heads[st + j] = (j == 0 || kj != kp) ? 1 : 0;
+                h = (j == 0 || kj != kp) ? 1 : 0;
             }
+            if (wk) gmem(k0)[st + j] = kj;
+            gmem(v0)[st + j] = vj;
+            gmem(heads)[st + j] = h;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s_mask[u * 64 + lane] = 0;  // the digit masks of the next bucket
+        idx += lstep;
+        if (idx >= lend) break;
+        unpack(en, pfn, a, b, key, val);  // waits for the loads only: they precede the stores
+        e = en;
+        pf = pfn;
+        en = enn;
+        pfn = pfnn;
     }
 }
 
@@ -1795,12 +1827,6 @@ static bool no_compact() { return std::getenv("GKM_NO_COMPACT") != nullptr; }  /
 // timing only: GKM_L0_PROF=1 times the phases of the 2-bit L0 partition (tools)
 static bool l0_prof() {
     static const bool v = std::getenv("GKM_L0_PROF") != nullptr;
-    return v;
-}
-
-// tuning only (A/B runs): GKM_WAVE_OCC=4 runs the 8-key wave class at 4 waves per SIMD
-static int wave_occ() {
-    static const int v = std::getenv("GKM_WAVE_OCC") ? std::atoi(std::getenv("GKM_WAVE_OCC")) : 5;
     return v;
 }
 
@@ -2446,24 +2472,25 @@ struct MsdDriver {
             if (g >= 8) g = xcd_walk_off() ? g - ((g & 7) == 0) : (g & ~7ull);  // the wave kernels' XCD-aware walk
             return dim3((unsigned)g);
         };
-        switch (k) {
-        case 0:  // (capped for 8 waves per SIMD it spills 12 B and runs 11 % slower on C5)
-            hipLaunchKernelGGL((msd_wave_kernel<4>), grid((const void *)msd_wave_kernel<4>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
-            break;
-        case 1:  // registers capped for 5 waves per SIMD (107 -> 96 VGPRs, 44 B of spills): measured
-                 // 17.5-17.7 ms against 19.0 at C3 (GKM_WAVE_OCC A/B, one box); 6 waves spill 64 B: 25.6
-            if (wave_occ() == 4)
-                hipLaunchKernelGGL((msd_wave_kernel<8, 4>), grid((const void *)msd_wave_kernel<8, 4>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
+        // wave classes: msd_wave_kernel<I, waves per SIMD, keys written>
+        auto wave = [&](auto fn_wk, auto fn_nk) {
+            const void *fn = wkeys ? (const void *)fn_wk : (const void *)fn_nk;
+            if (wkeys)
+                hipLaunchKernelGGL(fn_wk, grid(fn, 64), dim3(64), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads,
+                                   d_nl, ctr, skip, small, ci.pref, ci.nd);
             else
-                hipLaunchKernelGGL((msd_wave_kernel<8, 5>), grid((const void *)msd_wave_kernel<8, 5>, 64), dim3(64), 0,
-                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
+                hipLaunchKernelGGL(fn_nk, grid(fn, 64), dim3(64), 0, c->stream, lst, cnt, B, k0, v0, k1, v1, heads,
+                                   d_nl, ctr, skip, small, ci.pref, ci.nd);
+        };
+        switch (k) {
+        case 0:
+            wave(msd_wave_kernel<4, kWaveOcc4, true>, msd_wave_kernel<4, kWaveOcc4, false>);
             break;
-        case 2:  // capped for 3 waves per SIMD (188 -> 168 VGPRs, 24 B of spills): 10.4 against 12.3 ms
-                 // on C5 (A/B, one box)
-            hipLaunchKernelGGL((msd_wave_kernel<16, 3>), grid((const void *)msd_wave_kernel<16, 3>, 64), dim3(64), 0,
-                               c->stream, lst, cnt, B, k0, v0, k1, v1, heads, d_nl, ctr, skip, small, wkeys, ci);
+        case 1:
+            wave(msd_wave_kernel<8, kWaveOcc8, true>, msd_wave_kernel<8, kWaveOcc8, false>);
+            break;
+        case 2:
+            wave(msd_wave_kernel<16, kWaveOcc16, true>, msd_wave_kernel<16, kWaveOcc16, false>);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),

@@ -10,6 +10,17 @@
 
 namespace gkm {
 
+// global-memory views of device pointers: the kernels' arguments are generic pointers, and
+// where the compiler cannot infer that one stays global (a pointer chosen at run time, a
+// reinterpretation) it emits flat loads / stores, which wait for LDS and memory counters together
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *gmem(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
+typedef __attribute__((address_space(1))) const uint64_t gu64;
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const uint32_t __attribute__((aligned(1))) gu32u;  // unaligned
+
 // workgroup barrier that orders LDS only: global stores stay in flight across it (__syncthreads
 // would wait for every outstanding store of the wave before the barrier)
 __device__ __forceinline__ void lds_barrier() {
@@ -47,77 +58,52 @@ __host__ __device__ inline uint2 local_entry(uint32_t start, uint32_t len, int h
 // ---------------------------------------------------------------------------------------------
 // shared building blocks
 // ---------------------------------------------------------------------------------------------
-// lanes of the wave holding the same R-bit digit (and valid): R ballots; per bit the lane keeps
-// the ballot or its complement via a sign-extended bit (one 3-input bitop per half)
-template <int R>
-__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool valid) {
-    const uint64_t v = __ballot(valid);
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-    for (int b = 0; b < R; ++b) {
-        const uint32_t m = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);  // 0 or ~0
-        const uint64_t bb = __ballot(m != 0);
-        lo &= ~((uint32_t)bb ^ m);
-        hi &= ~((uint32_t)(bb >> 32) ^ m);
-    }
-    return ((uint64_t)hi << 32) | lo;
-}
-
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// stable 64-lane ranking of I wave-striped items by an R-bit digit (per-wave LDS counters):
-// every lane reads its digit's counter, the first lane of each peer group bumps it.  LDS ops of
-// one wave complete in order, so item i+1 reads item i's update.
-template <int I, int R>
+// Stable rank of a wave-striped item by its digit, ONE LDS instruction: every valid lane adds 1 to
+// its digit's counter with a returning atomic and gets the counter's value before its add.  The
+// LDS of gfx950 applies the same-address lanes of one wave instruction in increasing lane order, so
+// that value is the count before the instruction plus the lanes below with the same digit -- the
+// stable rank.  Successive items of a wave accumulate in order (one wave's LDS operations complete
+// in order).  A ballot-match takes R + 1 ballots per item and the LDS-mask round trip five LDS
+// instructions (tools/lds_rank_probe.hip: 3.9 vs 0.88 T items/s chip-wide).  The lane order is a
+// hardware property, not an ISA guarantee: gk_create checks it once per process (gkm_capi.hip,
+// lds_rank_check) and refuses a device where it does not hold.
+__device__ __forceinline__ uint32_t rank_atomic(uint32_t *wc, uint32_t d, bool valid) {
+    return valid ? atomicAdd(&wc[d], 1u) : 0u;
+}
+
+// ranks of I items (items >= live hold no valid element: skipped, wave-uniform)
+template <int I>
 __device__ __forceinline__ void rank_items(const uint32_t (&dig)[I], const bool (&valid)[I], uint32_t *s_wc_wave,
                                            uint32_t (&rank)[I], int live = I) {
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         rank[i] = 0;
-        if (i >= live) continue;  // wave-uniform: no valid item in this or later slots
-        const uint64_t peers = match_peers<R>(dig[i], valid[i]);
-        const uint32_t rank_in = lanes_below(peers);
-        const uint32_t old = s_wc_wave[dig[i]];
-        if (valid[i] && rank_in == 0) s_wc_wave[dig[i]] = old + (uint32_t)__popcll(peers);
-        rank[i] = old + rank_in;
+        if (i >= live) continue;
+        rank[i] = rank_atomic(s_wc_wave, dig[i], valid[i]);
     }
 }
 
-// The same ranking with LDS masks instead of ballots (msd_wave_kernel's scheme): per item, each
-// valid lane ORs its bit into s_mask_wave[digit], reads the mask back (its peers) and zeroes it;
-// the first peer adds the item's count to the counter with a returning atomic and broadcasts the
-// old value.  s_mask_wave (RADIX u64) must be zero on entry and is zero on exit.
-template <int I, int R>
-__device__ __forceinline__ void rank_items_mask(const uint32_t (&dig)[I], const bool (&valid)[I],
-                                                uint32_t *s_wc_wave, uint64_t *s_mask_wave, uint32_t (&rank)[I],
-                                                int live = I) {
-    const int lane = threadIdx.x & 63;
-    const unsigned long long me_bit = 1ull << lane;
-    uint64_t peers[I];
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-        peers[i] = 0;
-        if (i >= live) continue;  // wave-uniform
-        if (valid[i]) atomicOr((unsigned long long *)&s_mask_wave[dig[i]], me_bit);
-        peers[i] = s_mask_wave[dig[i]];
-        s_mask_wave[dig[i]] = 0;  // all lanes of the digit, after the wave's read
-    }
-    uint32_t old[I], rin[I];
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-        old[i] = 0;
-        rin[i] = lanes_below(peers[i]);
-        if (i < live && valid[i] && rin[i] == 0) old[i] = atomicAdd(&s_wc_wave[dig[i]], (uint32_t)__popcll(peers[i]));
-    }
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-        rank[i] = 0;
-        if (i >= live) continue;
-        const int leader = valid[i] ? __ffsll((unsigned long long)peers[i]) - 1 : lane;
-        rank[i] = __shfl(old[i], leader) + rin[i];
-    }
+// inclusive scan of one u32 per lane over the wave, VALU only: row_shr 1/2/4/8 inside rows of 16
+// lanes, then the gfx9 DPP row broadcasts row_bcast:15 and row_bcast:31 (rocPRIM's gfx9 warp scan)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63, rl = lane & 15;
+    uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    if (rl >= 1) v += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    if (rl >= 2) v += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    if (rl >= 4) v += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    if (rl >= 8) v += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if (lane & 16) v += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (lane >= 32) v += t;
+    return v;
 }
 
 template <int T, int I, int R>
@@ -142,7 +128,6 @@ struct PartSmem {
 // s_start[RADIX + 1] receives the tile-local digit starts (s_start[RADIX] = item count) and
 // slot[] each item's staging slot (invalid items: the sink slot kTile); s_toff may be null.
 // live (wave-uniform): items >= live of this wave hold no valid element and are skipped.
-// s_mask (optional, kWaves * RADIX u64, zero): rank with LDS masks instead of ballots.
 // PROF (timing builds of tools/radix_bench only): thread 0 adds the clock ticks of each phase to
 // prof[0..3] (rank, scan, slots, staging).
 template <int T, int I, int R, bool PROF = false>
@@ -150,7 +135,7 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
                                                 const bool (&valid)[I], Dig d, unsigned char *s_raw,
                                                 uint32_t *s_toff, uint32_t *s_wsum, uint32_t *s_start,
                                                 uint32_t (&slot)[I], unsigned long long *prof = nullptr,
-                                                int live = I, uint64_t *s_mask = nullptr) {
+                                                int live = I) {
     using SM = PartSmem<T, I, R>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -171,10 +156,7 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
     uint32_t dig[I], rank[I];
 #pragma unroll
     for (int i = 0; i < I; ++i) dig[i] = dg_of(key[i], d);
-    if (s_mask)  // LDS-mask ranking (per-wave masks of RADIX u64)
-        rank_items_mask<I, R>(dig, valid, s_wc + wave * RADIX, s_mask + wave * RADIX, rank, live);
-    else
-        rank_items<I, R>(dig, valid, s_wc + wave * RADIX, rank, live);
+    rank_items<I>(dig, valid, s_wc + wave * RADIX, rank, live);
     lds_barrier();
     mark(0);
     // per-digit totals over the waves -> per-wave exclusive prefixes; block scan over digits
@@ -195,12 +177,7 @@ __device__ __forceinline__ void partition_stage(const uint64_t (&key)[I], const 
             }
             sum += total[k];
         }
-        incl = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
+        incl = wave_incl_scan(sum);
         if (lane == 63) s_wsum[wave] = incl;
     }
     lds_barrier();
@@ -524,11 +501,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
         for (int i = 0; i < I; ++i) {
             valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
             dig[i] = dg_of(key[i], dl);
-            const uint64_t peers = match_peers<R>(dig[i], valid[i]);
-            const uint32_t rank_in = lanes_below(peers);
-            const uint32_t old = wc[dig[i]];
-            if (valid[i] && rank_in == 0) wc[dig[i]] = old + (uint32_t)__popcll(peers);
-            rank[i] = old + rank_in;
+            rank[i] = rank_atomic(wc, dig[i], valid[i]);
             if (PRE + i < I) pipe_store<T, I, R, MODE, ND>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);
         }
         lds_barrier();  // ranks final; the previous tile's staging has been read out
@@ -540,12 +513,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
                 s_wc[w * RADIX + tid] = total;
                 total += v;
             }
-            incl = total;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off);
-                if (lane >= off) incl += y;
-            }
+            incl = wave_incl_scan(total);
             if (lane == 63) s_wsum[wave] = incl;
         }
         lds_barrier();

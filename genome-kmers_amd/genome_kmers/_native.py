@@ -51,7 +51,7 @@ EXPORTED = (
     "gk_create", "gk_destroy", "gk_last_error", "gk_sync", "gk_device_count", "gk_set_sequence",
     "gk_alphabet_is_acgt", "gk_enumerate", "gk_set_start_indices", "gk_sort", "gk_num_kmers",
     "gk_copy_start_indices", "gk_copy_start_range", "gk_key_layout", "gk_copy_keys", "gk_set_filter_mask",
-    "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_unique", "gk_device_views",
+    "gk_set_group_heads", "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range",
@@ -109,6 +109,7 @@ _SIGS = {
     "gk_key_layout": ([_P, _U32P, _U32P, _U32P], ctypes.c_int),
     "gk_copy_keys": ([_P, _U64P, ctypes.c_uint64], ctypes.c_int),
     "gk_set_filter_mask": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
+    "gk_set_group_heads": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
     "gk_group_hist": ([_P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(GkFilter), ctypes.c_int64, ctypes.c_int64,
                        ctypes.c_int64, _I64P, _I64P, _I32P, _U64P], ctypes.c_int),
     "gk_group_members": ([_P, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(GkFilter), ctypes.c_int64,
@@ -154,6 +155,13 @@ def _share_hip_runtime():
         if hip.exists():
             ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
             return
+
+
+GROUPS_FROM_HEADS = 2  # gk_group_hist / gk_group_members: groups from gk_set_group_heads
+
+
+def _group_mode(is_sorted) -> int:
+    return GROUPS_FROM_HEADS if is_sorted == GROUPS_FROM_HEADS else int(bool(is_sorted))
 
 
 def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -317,6 +325,10 @@ class Engine:
         m = np.ascontiguousarray(mask, dtype=np.uint8)
         self._check(self.lib.gk_set_filter_mask(self.ctx, _ptr(m, ctypes.c_uint8), m.size))
 
+    def set_group_heads(self, heads: np.ndarray):
+        h = np.ascontiguousarray(heads, dtype=np.uint8)
+        self._check(self.lib.gk_set_group_heads(self.ctx, _ptr(h, ctypes.c_uint8), h.size))
+
     def _raise_filter(self, rc, code, idx):
         if rc == GK_E_FILTER:
             raise FilterRaised(code.value, idx.value)
@@ -326,7 +338,7 @@ class Engine:
         hist = np.zeros(max_counts_bin + 1, dtype=np.int64)
         total = ctypes.c_int64(0)
         code, idx = ctypes.c_int32(0), ctypes.c_uint64(0)
-        rc = self.lib.gk_group_hist(self.ctx, int(bool(is_sorted)), -1 if kmer_len is None else int(kmer_len),
+        rc = self.lib.gk_group_hist(self.ctx, _group_mode(is_sorted), -1 if kmer_len is None else int(kmer_len),
                                     ctypes.byref(filt), int(min_group_size),
                                     -1 if max_group_size is None else int(max_group_size), int(max_counts_bin),
                                     _ptr(hist, ctypes.c_int64), ctypes.byref(total), ctypes.byref(code),
@@ -335,7 +347,7 @@ class Engine:
         return hist, int(total.value)
 
     def group_members(self, is_sorted, kmer_len, filt: GkFilter, min_group_size, max_group_size, yield_first_n):
-        args = (int(bool(is_sorted)), -1 if kmer_len is None else int(kmer_len), ctypes.byref(filt),
+        args = (_group_mode(is_sorted), -1 if kmer_len is None else int(kmer_len), ctypes.byref(filt),
                 int(min_group_size), -1 if max_group_size is None else int(max_group_size),
                 -1 if yield_first_n is None else int(yield_first_n))
         count = ctypes.c_uint64(0)

@@ -280,13 +280,41 @@ def _device_filter(engine: "_native.Engine", filt, sba, sba_strand, starts_fn) -
 
 
 def _comparator_mode(cmp) -> tuple:
-    """(is_sorted, kmer_len) for a recognised comparator."""
+    """(is_sorted, kmer_len) for a recognised comparator; (None, None) for a custom one."""
     if isinstance(cmp, _Comparator):
         return (not cmp.always_less), cmp.kmer_len
-    raise NotImplementedError(
-        "genome_kmers runs the group pass on the GPU and supports the comparators built by "
-        "get_compare_sba_kmers_func / compare_sba_kmers_always_less_than only"
-    )
+    if not callable(cmp):
+        raise TypeError("kmer_comparison_func must be callable")
+    return None, None
+
+
+def _custom_groups(engine: "_native.Engine", cmp, filt, sba, sba_strand, starts) -> _native.GkFilter:
+    """A custom ``kmer_comparison_func`` (user code: the device cannot run it) decides the groups on
+    the host, as the reference's generator does (kmers.py:579-601): each k-mer that passes the
+    filter is compared with the previous one that passed, ``comparison == 0`` meaning the same
+    group.  The filter runs on the host too, so that filter and comparator are called in the
+    reference's order and the first raise is the reference's.  The device then runs the group
+    pass over the resulting head mask (gk_set_group_heads); returns the filter spec to pass."""
+    starts = np.asarray(starts)
+    keep_all = isinstance(filt, _DeviceFilter) and filt.kind == _native.FILTER_KEEP_ALL
+    if not keep_all and not callable(filt):
+        raise TypeError("kmer_filter_func must be callable")
+    valid = np.ones(len(starts), dtype=np.uint8)
+    heads = np.zeros(len(starts), dtype=np.uint8)
+    prev = None
+    for i, s in enumerate(starts.tolist()):
+        if not keep_all and not filt(sba, sba_strand, s):
+            valid[i] = 0
+            continue
+        if prev is not None:
+            comparison, _ = cmp(sba, sba, prev, s)
+            heads[i] = comparison != 0
+        prev = s
+    engine.set_group_heads(heads)
+    if keep_all:
+        return filt.gk_filter()
+    engine.set_filter_mask(valid)
+    return _native.GkFilter(_native.FILTER_MASK, 0, 0, 0, 0)
 
 
 def _engine_for_arrays(sba: np.ndarray, kmer_start_indices: np.ndarray) -> "_native.Engine":
@@ -309,6 +337,9 @@ def get_kmer_group_size_hist(sba, sba_strand, kmer_len, kmer_start_indices, kmer
     if len(kmer_start_indices) == 0:
         return np.zeros(max_counts_bin + 1, dtype=np.int64), 0
     eng = _engine_for_arrays(sba, kmer_start_indices)
+    if is_sorted is None:  # custom comparator: groups decided on the host, counted on the device
+        filt = _custom_groups(eng, kmer_comparison_func, kmer_filter_func, sba, sba_strand, kmer_start_indices)
+        return eng.group_hist(_native.GROUPS_FROM_HEADS, None, filt, min_group_size, max_group_size, max_counts_bin)
     filt = _device_filter(eng, kmer_filter_func, sba, sba_strand, lambda: kmer_start_indices)
     try:
         return eng.group_hist(is_sorted, cmp_len, filt, min_group_size, max_group_size, max_counts_bin)
@@ -327,12 +358,17 @@ def kmer_info_by_group_generator(sba, sba_strand, kmer_len, kmer_start_indices, 
     if len(kmer_start_indices) == 0:
         return
     eng = _engine_for_arrays(sba, kmer_start_indices)
-    filt = _device_filter(eng, kmer_filter_func, sba, sba_strand, lambda: kmer_start_indices)
-    try:
-        nums, yielded, totals = eng.group_members(is_sorted, cmp_len, filt, min_group_size, max_group_size,
-                                                  yield_first_n)
-    except _native.FilterRaised as e:
-        raise _filter_error(e.ferr, e.sba_idx, kmer_filter_func) from None
+    if is_sorted is None:  # custom comparator: groups decided on the host, members on the device
+        filt = _custom_groups(eng, kmer_comparison_func, kmer_filter_func, sba, sba_strand, kmer_start_indices)
+        nums, yielded, totals = eng.group_members(_native.GROUPS_FROM_HEADS, None, filt, min_group_size,
+                                                  max_group_size, yield_first_n)
+    else:
+        filt = _device_filter(eng, kmer_filter_func, sba, sba_strand, lambda: kmer_start_indices)
+        try:
+            nums, yielded, totals = eng.group_members(is_sorted, cmp_len, filt, min_group_size, max_group_size,
+                                                      yield_first_n)
+        except _native.FilterRaised as e:
+            raise _filter_error(e.ferr, e.sba_idx, kmer_filter_func) from None
     for num, y, t in zip(nums.tolist(), yielded.tolist(), totals.tolist()):
         yield kmer_info_func(num, kmer_start_indices, sba, kmer_len, y, t)
 
@@ -833,6 +869,17 @@ class Kmers:
     # ---- sort (kmers.py:1624-1731) -----------------------------------------------------------
     def sort(self, *, canonical: bool = False):
         """Sort the start indices by k-mer on the GPU (in place from the caller's point of view).
+
+        Tie order: equal k-mers come back in ascending start order -- the reference's
+        ``get_is_less_than_func(break_ties=True)`` order (kmers.py:1710-1711).  The reference's own
+        ``sort()`` uses ``break_ties=False`` and leaves equal k-mers in whatever order numba's
+        quicksort produces (kmers.py:1624-1652); no parallel sort reproduces that.  Sorted k-mers,
+        encoded keys, group sizes, counts, histograms and the ``(kmer_num, group_size_yielded,
+        group_size_total)`` tuples of ``get_kmers`` are identical either way, because ties only
+        permute the members of a group inside the group's index range.  What can differ is WHICH
+        members a tie group reports: the start (and so the location) behind a given ``kmer_num``
+        inside a group, i.e. the members ``yield_first_n`` picks and the locations of
+        ``kmer_info_to_yield="full"``.  Here they are the group's smallest start indices.
 
         canonical=True (this build's extension; the reference has no canonical k-mers,
         kmers.py:689-696): order by min(k-mer, reverse complement) with the reference's IUPAC

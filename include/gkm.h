@@ -133,10 +133,18 @@ int gk_copy_strands(gk_ctx *ctx, uint8_t *dst, uint64_t n);
 /* ---- groups ---------------------------------------------------------------------------------- */
 /* mask for GK_FILTER_MASK: one byte per position of the current start-index order */
 int gk_set_filter_mask(gk_ctx *ctx, const uint8_t *mask, uint64_t n);
+/* Group boundaries decided by a caller's comparison (a custom kmer_comparison_func the device cannot
+ * run, kmers.py:285-303, 597-601): heads[i] = 1 if the k-mer at position i of the current order
+ * differs from the previous VALID k-mer (passing the filter), 0 if it is equal; read at valid
+ * positions only, the first valid k-mer always starts a group.  Used by gk_group_hist /
+ * gk_group_members called with is_sorted = GK_GROUPS_FROM_HEADS. */
+int gk_set_group_heads(gk_ctx *ctx, const uint8_t *heads, uint64_t n);
+#define GK_GROUPS_FROM_HEADS 2
 /*
  * Histogram of group sizes over k-mers passing `filter`; groups are runs of equal k-mers under
  * compare_sba_kmers_lexicographically(kmer_len) (kmer_len < 0 = None) when is_sorted, else every
- * k-mer is its own group (compare_sba_kmers_always_less_than).  max_group_size < 0 = None.
+ * k-mer is its own group (compare_sba_kmers_always_less_than); is_sorted = GK_GROUPS_FROM_HEADS: the
+ * groups gk_set_group_heads described.  max_group_size < 0 = None.
  * hist has max_counts_bin + 1 entries.  On GK_E_FILTER, *err_code / *err_idx name the failing
  * filter check and the SBA index of the first (in start-index order) k-mer that raised.
  */

@@ -39,6 +39,11 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "sorted 31-mers/sec end-to-end on 3.1 Gb synthetic genome; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# BASELINE.md section 3's byte model of the whole step: an 8-pass LSD sort of 8-byte keys with a
+# 4-byte payload -- read 1 (sequence) + 8 (histogram) + 8 x 12 = 105 B per 31-mer, total 201 B
+BASELINE_READ_B, BASELINE_TOTAL_B = 105, 201
+# the wave-local finishing kernel's instantiation (gkm_msd.hip: msd_wave_kernel<I, waves/SIMD, keys>)
+WAVE8_KERNEL = "msd_wave_kernel<8,5,true>"
 
 
 def parse():
@@ -209,18 +214,21 @@ def pipelined_e2e(torch, eng, sba, step, log, reps: int = 3) -> dict:
 
 
 def load_traffic(path: str, kernel: str):
-    """HBM bytes per launch of `kernel` (an instantiation prefix such as
-    "msd_pipe_kernel<1024,11,8,4") from a tools/pmc_traffic.py summary, or None."""
+    """(HBM bytes per launch, source) of `kernel` (an instantiation prefix such as
+    "msd_pipe_kernel<1024,11,8,4") from a tools/pmc_traffic.py summary -- rocprofv3 --pmc passes
+    of FETCH_SIZE and WRITE_SIZE over this same bench command on a builder's box (a bench run
+    cannot read PMC counters itself); (None, reason) when the file has no such kernel."""
     try:
         with open(path) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
-        return None
+        return None, f"{path}: not found"
+    rel = os.path.relpath(path, ROOT)
     want = kernel.replace(" ", "").rstrip(">")
     for name, rec in t.items():
         if not name.startswith("_") and "<" in name and name.startswith(want):
-            return rec.get("hbm_bytes_max_launch")
-    return None
+            return rec.get("hbm_bytes_max_launch"), f"{rel} ({t.get('_label', '')}; {t.get('_convention', '')})"
+    return None, f"{rel}: no {kernel} record"
 
 
 def main():
@@ -379,7 +387,7 @@ def main():
     # dominant kernel: the stage with the most time among the device kernels with a byte model
     # (the level partitions, the compact level, the L0 partition, the wave-local finishing kernel)
     kinds = {"msd_pass_l0": ("msd0_pipe_kernel<2,1024,18,7,true>", "the L0 partition, straight from the sequence"),
-             "msd_local_wave8": ("msd_wave_kernel<8,5>", "wave-local finishing of buckets <= 512")}
+             "msd_local_wave8": (WAVE8_KERNEL, "wave-local finishing of buckets <= 512")}
     timed = {n: v for n, v in report.items() if stage_bytes(n, v) and v["total_ms"] > 0 and
              (n in kinds or n.startswith("msd_pass_l"))}
     dom = max(timed, key=lambda n: timed[n]["total_ms"]) if timed else None
@@ -395,9 +403,19 @@ def main():
     bytes_per_launch = dom_bytes / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
-    traffic = load_traffic(args.traffic, kdesc)
+    traffic, traffic_src = load_traffic(args.traffic, kdesc)
+    # BASELINE.md section 3, verbatim: the step's read roofline n * 105 B / t (device boundary and
+    # end to end), and the total-traffic fraction n * 201 B / t -- a model of the whole step, beside
+    # the dominant kernel's own byte model above
+    t_dev, t_e2e = ms_per_step * 1e-3, (ms_per_step + boundary["h2d_pinned_ms"]) * 1e-3
+    base = {"baseline_read_frac": round(n_units * BASELINE_READ_B / t_dev / (HBM_PEAK_GBS * 1e9), 4),
+            "baseline_read_frac_e2e": round(n_units * BASELINE_READ_B / t_e2e / (HBM_PEAK_GBS * 1e9), 4),
+            "baseline_total_frac": round(n_units * BASELINE_TOTAL_B / t_dev / (HBM_PEAK_GBS * 1e9), 4),
+            "baseline_model": "BASELINE.md section 3: read 105 B, total 201 B per 31-mer (8-pass LSD model) / "
+                              "ms_per_step (device) or ms_per_step + h2d_pinned_ms (e2e) / 8 TB/s"}
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                **base,
                 "kernel": f"{kdesc} ({dom}: {what})",
                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "units_per_launch": int(rp["units"] / max(rp["count"], 1)),

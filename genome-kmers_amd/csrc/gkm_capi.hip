@@ -500,11 +500,16 @@ int gkm::ensure_keys(gk_ctx *c) {
     // buffer (one aligned row per k-mer instead of a ~70-byte window at a random position)
     static const bool no_table = std::getenv("GKM_NO_KEY_TABLE") != nullptr;  // (A/B)
     const KeySpec &ks = c->spec;
+    // (the table path answers hipErrorNotSupported when it does not apply -- e.g. per-contig k-mer
+    // counts that do not add up to n -- and the window gather, always correct, runs instead)
+    hipError_t te = hipErrorNotSupported;
     if (c->enum_sorted && !no_table && ks.words >= 2 && ks.symbols == ks.min_len && ks.symbols <= 64 &&
         (ks.bits == 2 || ks.bits == 4) && c->n >= 4096 && c->key_words_b[c->cur ^ 1] >= ks.words)
-        GK_TRY_HIP(c, launch_encode_table_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur], c->keys[c->cur ^ 1]));
-    else
+        te = launch_encode_table_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur], c->keys[c->cur ^ 1]);
+    if (te == hipErrorNotSupported)
         GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
+    else
+        GK_TRY_HIP(c, te);
     timer_end(c, slot);
     c->keys_valid = true;
     c->keys_stale = false;

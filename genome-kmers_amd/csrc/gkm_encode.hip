@@ -709,7 +709,7 @@ hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32
         const uint64_t len = end - c->hseg[s] + 1;
         if (len >= (uint64_t)ks.symbols) acc += len - ks.symbols + 1;
     }
-    if (acc != n) return hipErrorInvalidValue;  // not the whole enumeration
+    if (acc != n) return hipErrorNotSupported;  // not the whole enumeration: the caller gathers windows
     uint32_t *d_kb = nullptr;
     if (scratch(c, "enc_kb", std::max<uint64_t>(c->nseg, 1), &d_kb) != hipSuccess) return hipErrorOutOfMemory;
     e = hipMemcpyAsync(d_kb, kb.data(), 4 * c->nseg, hipMemcpyHostToDevice, c->stream);
@@ -718,14 +718,14 @@ hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32
     if (ks.bits == 2) {
         switch (ks.words) {
         case 2: e = table_gather_w<2, 2>(c, k, starts, n, keys, table, d_kb); break;
-        default: return hipErrorInvalidValue;
+        default: return hipErrorNotSupported;
         }
     } else {
         switch (ks.words) {
         case 2: e = table_gather_w<2, 4>(c, k, starts, n, keys, table, d_kb); break;
         case 3: e = table_gather_w<3, 4>(c, k, starts, n, keys, table, d_kb); break;
         case 4: e = table_gather_w<4, 4>(c, k, starts, n, keys, table, d_kb); break;
-        default: return hipErrorInvalidValue;
+        default: return hipErrorNotSupported;
         }
     }
     if (e != hipSuccess) return e;

@@ -621,8 +621,10 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
         timer_begin(c, "filter", &slot);
         // per position, then gathered (filter_pos_kernel); a mask is per sorted index, and
         // GKM_FILTER_PER_KMER=1 (A/B) evaluates every k-mer's window in sorted order
+        // The per-position pass costs O(sba_len) whatever n is: used when the k-mers are a sizeable
+        // share of the positions (a full enumeration), not for a small user-assigned start subset
         static const bool per_kmer = std::getenv("GKM_FILTER_PER_KMER") != nullptr;
-        if (kind != GK_FILTER_MASK && !per_kmer && c->sba_len > 0) {
+        if (kind != GK_FILTER_MASK && !per_kmer && c->sba_len > 0 && n * 8 >= c->sba_len) {
             uint64_t *words;
             GK_TRY_HIP(c, scratch(c, "filter_pos", (c->sba_len + 63) / 64 * 2, &words));
             hipLaunchKernelGGL(filter_pos_kernel, dim3(grid_for((c->sba_len + 255) / 256 * 256, 16384)), dim3(256), 0,

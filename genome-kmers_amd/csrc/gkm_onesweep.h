@@ -2,8 +2,8 @@
 //
 // Tile = THREADS x ITEMS keys, loaded wave-striped (item i of lane l in wave w is element
 // w*ITEMS*64 + i*64 + l, so every load instruction is one contiguous 64-lane burst).
-//   1. stable in-tile rank: per item, 8 ballots give the 64-lane "same digit" mask; the lowest lane
-//      of each mask bumps the wave's LDS counter for that digit (waves own disjoint counters);
+//   1. stable in-tile rank: per item one returning LDS atomic on the wave's counter of the digit
+//      (rank_atomic, gkm_partition.h; waves own disjoint counters);
 //   2. per-digit tile totals -> wave prefixes and tile-local digit starts (block scan);
 //   3. decoupled look-back: the tile publishes its per-digit counts as epoch-tagged 64-bit words
 //      (flag | epoch | value) with agent-scope relaxed atomics -- the word is its own flag, so no
@@ -14,6 +14,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "gkm_partition.h"
 
 namespace gkm {
 
@@ -92,28 +94,9 @@ __global__ __launch_bounds__(THREADS) void onesweep_kernel(
         }
     }
 
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
-        const bool valid = wbase + i * 64 < n;
-        const uint32_t kw = digit_of<W>(key[i], word, shift);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (kw >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const int leader = valid ? (__ffsll((unsigned long long)peers) - 1) : lane;
-        const uint32_t rank_in = __popcll(peers & lt_mask);
-        uint32_t old = 0;
-        if (valid && lane == leader) {
-            old = s_wc[wave * 256 + kw];
-            s_wc[wave * 256 + kw] = old + (uint32_t)__popcll(peers);
-        }
-        old = __shfl(old, leader);
-        rank[i] = old + rank_in;
-    }
+    for (int i = 0; i < I; ++i)  // stable rank: one returning LDS atomic (rank_atomic, gkm_partition.h)
+        rank[i] = rank_atomic(s_wc + wave * 256, digit_of<W>(key[i], word, shift), wbase + i * 64 < n);
     __syncthreads();
 
     uint32_t total = 0;
@@ -125,12 +108,7 @@ __global__ __launch_bounds__(THREADS) void onesweep_kernel(
             s_wc[w * 256 + d] = total;
             total += v;
         }
-        uint32_t incl = total;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
+        const uint32_t incl = wave_incl_scan(total);
         if (lane == 63) s_wsum[wave] = incl;
         s_tile_start[d] = incl - total;  // wave-local for now
     }

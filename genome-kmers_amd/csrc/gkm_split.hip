@@ -637,8 +637,18 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         }
         rc = ensure_elems(c, nA + nB + 1, 1);  // keeps vals[0] (nA)
         if (rc != GK_OK) return rc;
+        // the merge's output buffer at its final width now, not mid-merge (keys[0] may hold A's
+        // keys: it is only regrown on the nA == 0 path below, where they are not used)
+        if (WK && a_keys != c->keys[1])
+            if (int r = grow_key_buffer(c, 1, WK)) return r;
         c->n = nA + nB;
     } else {
+        // both key buffers at the final key width before the A sort (which uses word 0 of each):
+        // nothing is freed or re-allocated between the A sort and the merge
+        if (WK) {
+            if (int r = grow_key_buffer(c, 0, WK)) return r;
+            if (int r = grow_key_buffer(c, 1, WK)) return r;
+        }
         c->n = nA;
         rc = nA > 0 ? msd_sort(c, ka) : GK_OK;
         c->msd_force_keys = false;
@@ -652,6 +662,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
         GK_TRY_HIP(c, hipMemcpyAsync(hd, b_heads, nB, hipMemcpyDeviceToDevice, c->stream));
         if (WK) {
+            if (b_keys == c->keys[0]) return fail(c, GK_E_STATE, "split sort: B keys alias the key buffer");
             if (int r = grow_key_buffer(c, 0, WK)) return r;
             GK_TRY_HIP(c, hipMemcpyAsync(c->keys[0], b_keys, 8 * (uint64_t)WK * nB, hipMemcpyDeviceToDevice,
                                          c->stream));  // stride nB == n
@@ -664,6 +675,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     }
     if (nB == 0) {  // msd_sort left vals[0] / heads in place; A's keys expanded next to them
         if (WK) {
+            if (a_keys == c->keys[1]) return fail(c, GK_E_STATE, "split sort: A keys alias the output buffer");
             if (int r = grow_key_buffer(c, 1, WK)) return r;
             const uint64_t nn = nA;
             if (WK == 1)
@@ -692,7 +704,9 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, hipGetLastError());
     uint8_t *hd;
     GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
-    if (WK) {
+    if (WK) {  // (a no-op after the pre-sizing above; a_keys / b_keys never live in keys[1])
+        if (a_keys == c->keys[1] || b_keys == c->keys[1])
+            return fail(c, GK_E_STATE, "split sort: input keys alias the merge output buffer");
         int r = grow_key_buffer(c, 1, WK);
         if (r != GK_OK) return r;
     }

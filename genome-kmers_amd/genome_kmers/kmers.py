@@ -765,11 +765,15 @@ class Kmers:
             g["track_strands_separately"] = self.track_strands_separately
             g["_is_initialized"] = self._is_initialized
             g["_is_set"] = self._is_set
-            g["_is_sorted"] = self._is_sorted
+            # a canonical order is not the reference's sort order: the file says "not sorted" to the
+            # reference's loader (kmers.py:1435-1472), which then re-sorts instead of trusting it,
+            # and keeps the canonical state in keys of its own, which only this build reads
+            g["_is_sorted"] = False if self._canonical else self._is_sorted
             s = self.kmer_sba_start_indices
             g["kmer_sba_start_indices"] = np.array([], dtype=np.uint32) if s is None else s
-            if self._canonical:  # this build's extension; the reference's loader ignores the extra key
+            if self._canonical:
                 g["_canonical"] = True
+                g["_canonical_sorted"] = bool(self._is_sorted)
         if include_sequence_collection:
             self.seq_coll.save(save_file_path, mode="a", format="hdf5")
 
@@ -802,6 +806,8 @@ class Kmers:
             s = g["kmer_sba_start_indices"][:]
             starts = None if s.shape == (0,) else s
             canonical = bool(g["_canonical"][()]) if "_canonical" in g else False
+            if canonical:
+                self._is_sorted = bool(g["_canonical_sorted"][()])
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="hdf5")
@@ -813,8 +819,10 @@ class Kmers:
                       "_is_initialized", "_is_set", "_is_sorted"):
                 db[k] = getattr(self, k)
             db["kmer_sba_start_indices"] = self.kmer_sba_start_indices
-            if self._canonical:  # this build's extension; the reference's loader ignores the extra key
+            if self._canonical:  # as _save_hdf5: "not sorted" for the reference, canonical state apart
+                db["_is_sorted"] = False
                 db["_canonical"] = True
+                db["_canonical_sorted"] = bool(self._is_sorted)
         if include_sequence_collection:
             self.seq_coll.save(save_file_path, format="shelve")
 
@@ -825,6 +833,8 @@ class Kmers:
                 setattr(self, k, db[k])
             starts = db["kmer_sba_start_indices"]
             canonical = bool(db.get("_canonical", False))
+            if canonical:
+                self._is_sorted = bool(db["_canonical_sorted"])
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="shelve")

@@ -294,9 +294,10 @@ def test_hdf5_contracts_under_an_interpreter_with_h5py():
 
 @pytest.mark.gpu
 def test_canonical_sort_survives_save_load(tmp_path):
-    """A canonical sort (this build's extension) is saved with an extra key the reference's loader
-    ignores; loading it restores the canonical groups, and loading a forward file into an object
-    that was sorted canonically restores forward groups."""
+    """A canonical sort (this build's extension) is saved as "not sorted" for the reference's
+    loader (which then re-sorts rather than trusting a non-reference order) with the canonical
+    state in keys of its own; loading it here restores the canonical groups, and loading a forward
+    file into an object that was sorted canonically restores forward groups."""
     if not _gpu():
         pytest.skip("no GPU")
     from oracle import oracle
@@ -317,8 +318,13 @@ def test_canonical_sort_survives_save_load(tmp_path):
     p, q = str(tmp_path / "canon"), str(tmp_path / "fwd")
     km.save(p, include_sequence_collection=True, format="shelve")
     fwd.save(q, include_sequence_collection=True, format="shelve")
+    import shelve
+
+    with shelve.open(p) as db:  # what the reference's loader reads (kmers.py:1497-1525)
+        assert db["_is_sorted"] is False and db["_canonical"] is True and db["_canonical_sorted"] is True
     back = gk.Kmers()
     back.load(p, format="shelve")
+    assert back._is_sorted and back._canonical
     got = back.get_kmer_group_counts(21, max_counts_bin=32)
     np.testing.assert_array_equal(got[0], want[0])
     np.testing.assert_array_equal(back.kmer_sba_start_indices, km.kmer_sba_start_indices)

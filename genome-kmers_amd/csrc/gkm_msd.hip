@@ -1274,10 +1274,8 @@ __device__ __forceinline__ void wave_entry(const uint2 *__restrict__ list, const
 }
 
 // raw elements of a wave-class bucket: compact (x = low << 32 | start, next-digit byte) or full
-// (key, start).  Branch-free, one instruction per word, so the compiler's count of loads and
-// stores in flight stays static and the bucket loop never drains its stores: the second word is a
-// 4-byte load either way -- of the start, or unaligned at the digit byte (its low byte; the digit
-// array is padded past n).  Buffers chosen by integer selects (pointer selects between kernel
+// (key, start).  One global load instruction per word either way (so the compiler's count of
+// loads in flight is static); buffers chosen by integer selects (pointer selects between kernel
 // arguments went through the stack as flat loads).  Loads clamped to the bucket.
 template <int I>
 __device__ __forceinline__ void wave_load(const uint2 e, uint64_t pf, int lane, const uint64_t *k0, const uint64_t *k1,
@@ -1291,6 +1289,15 @@ __device__ __forceinline__ void wave_load(const uint2 e, uint64_t pf, int lane, 
     const int sh = cmp ? 0 : 2;
     uint32_t q = lane;
     asm volatile("" : "+v"(q));
+    if (cmp) {  // byte loads of the digits: 0.1-0.3 ms faster than unaligned 4-byte ones at C3 (A/B)
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint64_t at = st + min(q + i * 64, len - 1);
+            a[i] = *reinterpret_cast<gu64 *>(kb + 8 * at);
+            b[i] = *reinterpret_cast<gu8 *>(bb + at);
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < I; ++i) {
         const uint64_t at = st + min(q + i * 64, len - 1);
@@ -1311,10 +1318,9 @@ __device__ __forceinline__ void wave_load(const uint2 e, uint64_t pf, int lane, 
 //          re-listed for another round; a sub-bucket whose key bits are exhausted is final
 //   write  keys (the group-head flag in bit 63 when B < 64) and starts staged at their final slots,
 //          then stored contiguously: keys, starts and head flags of the whole bucket
-// The NEXT bucket's elements are loaded at the top of the current one, so they fly during its
-// whole ranking and write-back (round 2 issued them just before the write-back); the write-back is
-// branch-free with a static store count (slots clamped to the bucket), so the next iteration waits
-// for those loads without draining the stores.  The list entries and prefixes are scalar loads two
+// The next bucket's elements are loaded once the current one is staged in LDS, so they fly during
+// its write-back; loads and write-back are branch-free with static counts (slots clamped to the
+// bucket), so the next iteration waits for those loads without draining the stores.  The list entries and prefixes are scalar loads two
 // buckets ahead.  LDS per wave: staged keys (aliased by the low bits of the ranking: one wave's LDS
 // operations complete in order), staged starts, digit counts -- 7.2 KB at I = 8.
 // WK: keys are written back (one-word sorts); otherwise only for buckets with re-listed elements.
@@ -1326,7 +1332,8 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                                                       int skip, uint32_t small, const uint64_t *__restrict__ cpref,
                                                       const uint8_t *__restrict__ cnd) {
     constexpr int CAP = 64 * I;
-    __shared__ uint64_t s_k[CAP + 1];  // staged keys (slot CAP: sink); the low bits while ranking
+    constexpr int MINLIVE = I > 4 ? I / 2 + 1 : 1;  // items a bucket of the class always fills
+    __shared__ uint64_t s_k[CAP + 4];  // staged keys (slot CAP: sink); rank-by-count values + sentinels
     __shared__ uint32_t s_v[CAP + 1];  // staged starts
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[260];  // digit counts -> starts; [256] = len
     const int lane = threadIdx.x;
@@ -1363,14 +1370,11 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
     pfn = pf;
     if (idx + lstep < lend) wave_entry(list, cpref, idx + lstep, en, pfn);
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    unpack(e, pf, a, b, key, val);
     for (;;) {
         const uint64_t st = e.x;
         const uint32_t len = e.y >> 8;
         const int hi0 = (e.y >> 1) & 127;
-        // the next bucket's raw elements fly during this whole bucket; they are unpacked after its
-        // write-back (so the loop carries keys, not loads: no register copy waits for memory)
-        wave_load<I>(en, pfn, lane, k0, k1, v0, v1, cnd, a, b);  // after the last: itself again
+        unpack(e, pf, a, b, key, val);
         uint2 enn = en;
         uint64_t pfnn = pfn;
         if (idx + 2 * lstep < lend) wave_entry(list, cpref, idx + 2 * lstep, enn, pfnn);
@@ -1409,50 +1413,59 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
             reinterpret_cast<uint4 *>(s_cnt)[lane] = make_uint4(r0, r0 + c.x, r0 + c.x + c.y, r0 + c.x + c.y + c.z);
             if (lane == 63) s_cnt[256] = incl;
         }
-        // 3. slots; the key bits below the digit staged there
+        // 3. slots.  Staged at each element's slot: its key bits below the sorted ones (digit and
+        // low bits) with the slot appended -- (x << 10) | slot, unique, and in sub-bucket order
+        // exactly the stable order -- when they fit 64 bits; otherwise the low bits alone.  Four
+        // sentinels (all ones) follow the bucket, so a rank-by-count may read past its sub-bucket
+        // unpredicated: later digits and sentinels are larger than any of its values.
+        const bool cmpst = hi + 64 - 10 >= B;  // composite values (C3: 39 + 10 bits)
+        const uint64_t xm = B - hi >= 64 ? ~0ull : (1ull << (B - hi)) - 1ull;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             if (i >= live) continue;
             const uint32_t d = pk[i] >> 16, r = pk[i] & 0xFFFFu;
             const uint32_t sb = s_cnt[d], size = s_cnt[d + 1] - sb;
-            if ((uint32_t)(i * 64 + lane) < len) s_k[sb + r] = key[i] & lowm;
+            if ((uint32_t)(i * 64 + lane) < len)
+                s_k[sb + r] = cmpst ? ((key[i] & xm) << 10) | (sb + r) : key[i] & lowm;
             pk[i] = (r << 21) | (size << 10) | sb;
         }
-        // 4. final slot and group-head flag of every element
+        if (lane < 4) s_k[len + lane] = ~0ull;
+        // 4. final slot of every element: sub-buckets of 2..small elements by rank-by-count
         bool any = false;
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             if (i >= live) continue;
             const uint32_t sb = pk[i] & 0x3FFu, size = (pk[i] >> 10) & 0x7FFu, r = pk[i] >> 21;
-            uint32_t o = sb + r, h = 0;
-            if ((uint32_t)(i * 64 + lane) >= len) {
-                o = CAP;  // sink
-            } else if (size == 1) {
-                h = 1;
-            } else if (last) {
-                h = r == 0;  // equal keys, in start order
-            } else if (size > small) {
-                any = true;  // re-listed: the next round writes its order and heads
-            } else {
-                const uint64_t me = key[i] & lowm;
-                uint32_t lt = 0, eq = 0;
-                // rank-by-count over the sub-bucket, 4 staged values per step (reads in flight
-                // together; indices past the sub-bucket clamped and not counted)
-                for (uint32_t j0 = 0; j0 < size; j0 += 4) {
-                    uint64_t x[4];
+            const bool valid = (uint32_t)(i * 64 + lane) < len;
+            uint32_t o = valid ? sb + r : (uint32_t)CAP;  // invalid items: the sink
+            any |= valid && size > small && !last;        // re-listed: ordered by the next round
+            if (valid && size > 1 && size <= small && !last) {
+                uint32_t cnt = 0;
+                if (cmpst) {
+                    const uint64_t me = ((key[i] & xm) << 10) | (sb + r);
+                    for (uint32_t j0 = 0; j0 < size; j0 += 4) {
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) x[u] = s_k[min(sb + j0 + u, (uint32_t)CAP)];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t j = j0 + u;
-                        lt += (j < size) & (x[u] < me);
-                        eq += (j < r) & (x[u] == me);
+                        for (int u = 0; u < 4; ++u) cnt += s_k[sb + j0 + u] < me;
                     }
+                } else {  // low bits; ties by slot
+                    const uint64_t me = key[i] & lowm;
+                    uint32_t lt = 0, eq = 0;
+                    for (uint32_t j0 = 0; j0 < size; j0 += 4) {
+                        uint64_t x[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) x[u] = s_k[sb + j0 + u];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t j = j0 + u;
+                            lt += (j < size) & (x[u] < me);
+                            eq += (j < r) & (x[u] == me);
+                        }
+                    }
+                    cnt = lt + eq;
                 }
-                o = sb + lt + eq;
-                h = eq == 0;
+                o = sb + cnt;
             }
-            pk[i] = o | (h << 16);
+            pk[i] = o;
         }
         const bool relist = __ballot(any) != 0;
         if (relist) {  // (rare) one entry per re-listed sub-bucket, from its first element
@@ -1463,7 +1476,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                     const uint32_t d = dg_of(key[i], dd);
                     const uint32_t sb = s_cnt[d];
                     size = s_cnt[d + 1] - sb;
-                    at = pk[i] & 0xFFFFu;
+                    at = pk[i];
                     if (size <= small || last || at != sb) size = 0;
                 }
                 route((uint32_t)st + at, size, hi + 8, B, 0, false, *Lp, ctr, lane);
@@ -1473,32 +1486,35 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             if (i >= live) continue;
-            const uint32_t o = pk[i] & 0xFFFFu;
-            s_k[o] = B < 64 ? key[i] | ((uint64_t)(pk[i] >> 16) << 63) : key[i];
-            s_v[o] = val[i];
+            s_k[pk[i]] = key[i];
+            s_v[pk[i]] = val[i];
         }
-        // 6. write-back: contiguous, static count (slots past the bucket repeat its last element)
+        // the next bucket's raw elements (after the last: this one again -- a static count): its
+        // keys and starts are staged, so their registers take the loads, which fly during the
+        // write-back (loading at the top of the bucket instead kept two buckets in registers:
+        // 4 waves per SIMD, measured 22.2 against 20.3 ms at C3)
+        wave_load<I>(en, pfn, lane, k0, k1, v0, v1, cnd, a, b);
+        // 6. write-back: contiguous; group-head flag = the key differs from its predecessor (a
+        // bucket starts a group; re-listed elements get provisional flags).  Items that may be
+        // empty first, skipped when they are; then the MINLIVE items every bucket of the class
+        // fills (its buckets hold more than CAP / 2 elements), unconditionally: the compiler then
+        // knows at least 3 MINLIVE stores follow the next bucket's loads, and the next iteration
+        // waits for those loads without draining them (a branch around every item's stores
+        // drained all; stores for empty items cost more than the drain)
         const bool wk = WK || relist;
 #pragma unroll
-        for (int i = 0; i < I; ++i) {
+        for (int ii = 0; ii < I; ++ii) {
+            const int i = ii < I - MINLIVE ? MINLIVE + ii : ii - (I - MINLIVE);
+            if (i >= MINLIVE && i >= live) continue;
             const uint32_t j = min((uint32_t)(i * 64 + lane), len - 1);
-            uint64_t kj = s_k[j];
+            const uint64_t kj = s_k[j], kp = s_k[j > 0 ? j - 1 : 0];
             const uint32_t vj = s_v[j];
-            uint8_t h;
-            if (B < 64) {
-                h = (uint8_t)(kj >> 63);
-                kj &= ~(1ull << 63);
-            } else {
-                const uint64_t kp = s_k[j > 0 ? j - 1 : 0];
-                h = (j == 0 || kj != kp) ? 1 : 0;
-            }
             if (wk) gmem(k0)[st + j] = kj;
             gmem(v0)[st + j] = vj;
-            gmem(heads)[st + j] = h;
+            gmem(heads)[st + j] = (j == 0 || kj != kp) ? 1 : 0;
         }
         idx += lstep;
         if (idx >= lend) break;
-        unpack(en, pfn, a, b, key, val);  // waits for the loads only: they precede the stores
         e = en;
         pf = pfn;
         en = enn;

@@ -177,6 +177,8 @@ def load_library(path: Path = LIB_PATH) -> ctypes.CDLL:
     _share_hip_runtime()
     lib = ctypes.CDLL(str(path))
     for name, (args, res) in _SIGS.items():
+        if os.environ.get("GKM_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B (tuning only): entry points it lacks stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

@@ -45,6 +45,12 @@ constexpr int kSmall = 24;
 #define GKM_WAVE_OCC8 5
 #endif
 constexpr int kWaveOcc4 = 6, kWaveOcc8 = GKM_WAVE_OCC8, kWaveOcc16 = 3;
+// digit bits of the wave-local kernels' in-LDS partition: buckets of ~370 keys (C3) over 512
+// digits leave sub-buckets of ~0.7 keys (rank-by-count reads half of what 256 digits need)
+#ifndef GKM_WAVE_R8
+#define GKM_WAVE_R8 9
+#endif
+constexpr int kWaveR4 = 8, kWaveR8 = GKM_WAVE_R8, kWaveR16 = 10;
 // later local rounds (buckets re-listed because a sub-bucket outgrew kSmall: repeat families) and
 // later phases finish sub-buckets of up to kSmallLate by rank-by-count instead of re-listing them
 // for another round -- a round costs a bucket load, ranking and write-back per bucket
@@ -1324,7 +1330,7 @@ __device__ __forceinline__ void wave_load(const uint2 e, uint64_t pf, int lane, 
 // buckets ahead.  LDS per wave: staged keys (aliased by the low bits of the ranking: one wave's LDS
 // operations complete in order), staged starts, digit counts -- 7.2 KB at I = 8.
 // WK: keys are written back (one-word sorts); otherwise only for buckets with re-listed elements.
-template <int I, int MINW, bool WK>
+template <int I, int MINW, bool WK, int R>
 __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                       uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                       const uint32_t *v1, uint8_t *__restrict__ heads,
@@ -1333,9 +1339,15 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                                                       const uint8_t *__restrict__ cnd) {
     constexpr int CAP = 64 * I;
     constexpr int MINLIVE = I > 4 ? I / 2 + 1 : 1;  // items a bucket of the class always fills
+    constexpr int RADIX = 1 << R, CPL = RADIX / 64;  // digits; counters per lane in the scan
+    static_assert(CPL % 4 == 0, "16-byte counter groups");
     __shared__ uint64_t s_k[CAP + 4];  // staged keys (slot CAP: sink); rank-by-count values + sentinels
-    __shared__ uint32_t s_v[CAP + 1];  // staged starts
-    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[260];  // digit counts -> starts; [256] = len
+    // digit counts -> starts (s_cnt[RADIX] = len); once the ranks are final, the staged starts
+    // (slot CAP: sink) -- one wave's LDS operations complete in order
+    constexpr int kUnion = (RADIX + 4) > (CAP + 1) ? (RADIX + 4) : (CAP + 1);
+    __shared__ __attribute__((aligned(16))) uint32_t s_cv[kUnion];
+    uint32_t *const s_cnt = s_cv;
+    uint32_t *const s_v = s_cv;
     const int lane = threadIdx.x;
     // XCD-aware walk (grid a multiple of 8): workgroup b takes the (b % 8)-th eighth of the list,
     // so the list's neighbouring buckets -- neighbours in memory, since classify appends a level's
@@ -1389,13 +1401,14 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                 if ((uint32_t)(i * 64 + lane) < len) x |= key[i] ^ kf;
             hi = skip_hi(wave_or64(x), B, hi);
         }
-        const Dig dd = dig_at(B, hi, 8);
-        const bool last = hi + 8 >= B;                      // a sub-bucket's keys are equal
+        const Dig dd = dig_at(B, hi, R);
+        const bool last = hi + R >= B;                      // a sub-bucket's keys are equal
         const uint64_t lowm = (1ull << dd.shift) - 1ull;    // key bits below the digit
         const int live = min(I, (int)((len + 63) >> 6));    // items holding elements (wave-uniform)
 
         // 1. stable rank inside the digit
-        reinterpret_cast<uint4 *>(s_cnt)[lane] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < CPL / 4; ++u) reinterpret_cast<uint4 *>(s_cnt)[lane * (CPL / 4) + u] = make_uint4(0, 0, 0, 0);
         uint32_t pk[I];  // rank | digit << 16, then rank << 21 | size << 10 | sub-bucket start
 #pragma unroll
         for (int i = 0; i < I; ++i) {
@@ -1404,14 +1417,24 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
             const uint32_t d = dg_of(key[i], dd);
             pk[i] = rank_atomic(s_cnt, d, (uint32_t)(i * 64 + lane) < len) | (d << 16);
         }
-        // 2. digit starts (exclusive scan of the 256 counts, 4 per lane); s_cnt[256] = len
+        // 2. digit starts (exclusive scan of the RADIX counts, CPL per lane); s_cnt[RADIX] = len
         {
-            const uint4 c = reinterpret_cast<const uint4 *>(s_cnt)[lane];
-            const uint32_t s4 = c.x + c.y + c.z + c.w;
-            const uint32_t incl = wave_incl_scan(s4);
-            const uint32_t r0 = incl - s4;
-            reinterpret_cast<uint4 *>(s_cnt)[lane] = make_uint4(r0, r0 + c.x, r0 + c.x + c.y, r0 + c.x + c.y + c.z);
-            if (lane == 63) s_cnt[256] = incl;
+            uint4 c[CPL / 4];
+            uint32_t sl = 0;
+#pragma unroll
+            for (int u = 0; u < CPL / 4; ++u) {
+                c[u] = reinterpret_cast<const uint4 *>(s_cnt)[lane * (CPL / 4) + u];
+                sl += c[u].x + c[u].y + c[u].z + c[u].w;
+            }
+            const uint32_t incl = wave_incl_scan(sl);
+            uint32_t r0 = incl - sl;
+#pragma unroll
+            for (int u = 0; u < CPL / 4; ++u) {
+                const uint4 o = make_uint4(r0, r0 + c[u].x, r0 + c[u].x + c[u].y, r0 + c[u].x + c[u].y + c[u].z);
+                reinterpret_cast<uint4 *>(s_cnt)[lane * (CPL / 4) + u] = o;
+                r0 = o.w + c[u].w;
+            }
+            if (lane == 63) s_cnt[RADIX] = incl;
         }
         // 3. slots.  Staged at each element's slot: its key bits below the sorted ones (digit and
         // low bits) with the slot appended -- (x << 10) | slot, unique, and in sub-bucket order
@@ -1479,7 +1502,7 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                     at = pk[i];
                     if (size <= small || last || at != sb) size = 0;
                 }
-                route((uint32_t)st + at, size, hi + 8, B, 0, false, *Lp, ctr, lane);
+                route((uint32_t)st + at, size, hi + R, B, 0, false, *Lp, ctr, lane);
             }
         }
         // 5. stage at the final slots (after every rank-by-count read of s_k: in order)
@@ -2500,13 +2523,13 @@ struct MsdDriver {
         };
         switch (k) {
         case 0:
-            wave(msd_wave_kernel<4, kWaveOcc4, true>, msd_wave_kernel<4, kWaveOcc4, false>);
+            wave(msd_wave_kernel<4, kWaveOcc4, true, kWaveR4>, msd_wave_kernel<4, kWaveOcc4, false, kWaveR4>);
             break;
         case 1:
-            wave(msd_wave_kernel<8, kWaveOcc8, true>, msd_wave_kernel<8, kWaveOcc8, false>);
+            wave(msd_wave_kernel<8, kWaveOcc8, true, kWaveR8>, msd_wave_kernel<8, kWaveOcc8, false, kWaveR8>);
             break;
         case 2:
-            wave(msd_wave_kernel<16, kWaveOcc16, true>, msd_wave_kernel<16, kWaveOcc16, false>);
+            wave(msd_wave_kernel<16, kWaveOcc16, true, kWaveR16>, msd_wave_kernel<16, kWaveOcc16, false, kWaveR16>);
             break;
         case 3:
             hipLaunchKernelGGL((msd_local_kernel<kBT, kBI, kBR>),

@@ -14,6 +14,7 @@ Usage (on the GPU box's host, ~10 min): python tools/cpu_baseline_prefixes.py [O
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -41,6 +42,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def heartbeat(stop):
+    """A progress line every 30 s while a long sort runs (ctypes releases the GIL)."""
+    t0 = time.time()
+    while not stop.wait(30):
+        print(f"[cpu baseline] ... {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+
 def main():
     out = Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "profiles" / "r3" / "cpu_baseline_prefixes.json"
     runs = []
@@ -49,9 +57,14 @@ def main():
         n = L - K + 1
         starts = np.arange(n, dtype=np.uint32)
         print(f"[cpu baseline] {L:,} bases, {n:,} k-mers: sorting ...", file=sys.stderr, flush=True)
+        stop = threading.Event()
+        hb = threading.Thread(target=heartbeat, args=(stop,), daemon=True)
+        hb.start()
         t0 = time.perf_counter()
         got = oracle.quicksort(sba, starts, K, K)
         dt = time.perf_counter() - t0
+        stop.set()
+        hb.join()
         # spot check: windows of the sorted order are non-decreasing by bytes
         for off in (0, n // 2, n - 1000):
             w = got[off:off + 1000].astype(np.int64)

@@ -107,6 +107,17 @@ def cpu_baseline(sba: np.ndarray, k: int, sample: int, n_full: int) -> dict:
         at, sub = 0, np.ascontiguousarray(sba[: sample + k - 1])
     ns, dt = timed(sub, k)
     t_full = dt * (n_full * np.log2(n_full)) / (ns * np.log2(ns))
+    # BASELINE.md section 2's prefix runs (1e8 / 3e8 bases of this genome), measured outside the
+    # bench's budget by tools/cpu_baseline_prefixes.py on a GPU box's host (~10 min)
+    prefixes = None
+    pre_path = ROOT / "profiles" / "r3" / "cpu_baseline_prefixes.json"
+    try:
+        with open(pre_path) as fh:
+            pre = json.load(fh)
+        prefixes = {"source": str(pre_path.relative_to(ROOT)), "cpu_model": pre["cpu_model"],
+                    "runs": pre["prefixes"], "full_workload": pre["full_workload"]}
+    except (OSError, ValueError, KeyError):
+        pass
     return {"value": ns / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": f"{ns:,} consecutive {k}-mers of this run's genome, numba-quicksort restatement with "
                       f"validate_kmers, gcc -O3, 1 thread; {dt:.1f} s",
@@ -116,7 +127,8 @@ def cpu_baseline(sba: np.ndarray, k: int, sample: int, n_full: int) -> dict:
             "full_workload_extrapolated": {"kmers": n_full, "seconds": round(t_full, 1),
                                            "kmers_per_s": round(n_full / t_full, 1),
                                            "method": "sample time x (N log2 N) / (n log2 n); extrapolated, "
-                                                     "not measured"}}
+                                                     "not measured"},
+            "prefix_runs": prefixes}
 
 
 def window_check(eng, sba: np.ndarray, k: int, canonical: bool, width: int = 2048) -> int:

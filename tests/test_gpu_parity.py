@@ -425,6 +425,44 @@ def test_unique_counts_match_groups():
     assert int(counts.sum()) == len(want)
 
 
+@pytest.mark.parametrize("shape", ["one_group", "all_distinct", "mixed_runs", "sparse_heads"])
+def test_unique_counts_many_tiles(shape):
+    """gk_unique_counts' one-pass selection (look-back over 4096-flag tiles, 16-byte output groups)
+    at sizes with thousands of tiles: runs of head-less tiles longer than one look-back window,
+    every position a head, and ragged mixtures; first index + multiplicity vs numpy on the keys."""
+    rng = np.random.default_rng(hash(shape) % 1000)
+    k = 31
+    if shape == "one_group":
+        s = np.full(3_000_000, ord("A"), np.uint8)
+    elif shape == "all_distinct":
+        s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 2_500_000)].copy()
+    elif shape == "mixed_runs":
+        s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 3_000_000)].copy()
+        for L in (40, 300, 5000, 70_000, 400_000):  # homopolymer runs: groups of L - k + 1
+            p = int(rng.integers(0, len(s) - L))
+            s[p:p + L] = ord("C")
+        rep = s[:2000].copy()
+        for p in rng.integers(0, len(s) - 2000, 50):
+            s[p:p + 2000] = rep
+    else:  # few distinct k-mers: long head-less stretches between heads
+        s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 3_000_000)].copy()
+        s[:] = np.repeat(s[::50_000], 50_000)[:len(s)]
+    e = _native.Engine()
+    e.set_sequence(s, np.array([0], np.uint32))
+    e.enumerate(k)
+    e.sort(k)
+    keys = e.copy_keys()
+    n = e.n
+    flat = keys.reshape(n, -1)
+    head = np.ones(n, dtype=bool)
+    head[1:] = (flat[1:] != flat[:-1]).any(axis=1)
+    want_first = np.flatnonzero(head)
+    want_cnt = np.diff(np.append(want_first, n))
+    first, counts = e.unique_counts()
+    np.testing.assert_array_equal(first, want_first)
+    np.testing.assert_array_equal(counts, want_cnt)
+
+
 def test_single_kmer_and_tiny_inputs():
     sc = SequenceCollection(sequence_list=[("a", "ACGTA")])
     km = gk.Kmers(sc, min_kmer_len=5, max_kmer_len=5)

@@ -1010,8 +1010,61 @@ extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     return rc;
 }
 
+// the weight of a homopolymer k-mer in the ownership histogram, in 16ths of a sorted k-mer: it
+// skips the MSD sort, but is selected, grouped, keyed and merged
+constexpr uint32_t kHomoWeight16 = 8;
+
+extern "C" int gk_shard_class_b(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
+                                uint64_t *n_rest, uint64_t *n_runs) {
+    if (!c || !h_hist || !n_rest || !n_runs) return GK_E_ARG;
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    *n_rest = *n_runs = 0;
+    c->shard_rest.clear();
+    c->shard_runs.clear();
+    if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
+    KeySpec ks;
+    int rc = shard_spec(c, k, flags, &ks);
+    if (rc != GK_OK) return rc;
+    if (!range_split(c, ks)) return GK_OK;  // no class B: ACGT-only sba, or k < 4
+    const int ob = range_own_bits(acgt_spec(ks));
+    std::vector<uint32_t> bins(1u << ob);
+    for (uint32_t d = 0; d < bins.size(); ++d) bins[d] = range_prefix(d, true, ob);
+    rc = split_shard_class_b(c, ks, lo, hi, bins, (ob + 1) / 2, kHomoWeight16, h_hist, &c->shard_rest, &c->shard_runs);
+    if (rc != GK_OK) return rc;
+    *n_rest = c->shard_rest.size();
+    *n_runs = c->shard_runs.size() / 3;
+    return GK_OK;
+}
+
+extern "C" int gk_shard_class_b_copy(gk_ctx *c, uint32_t *rest, uint64_t n_rest, uint32_t *runs, uint64_t n_runs) {
+    if (!c) return GK_E_ARG;
+    if (n_rest != c->shard_rest.size() || 3 * n_runs != c->shard_runs.size())
+        return fail(c, GK_E_ARG, "gk_shard_class_b_copy: sizes differ from gk_shard_class_b's");
+    if ((n_rest && !rest) || (n_runs && !runs)) return GK_E_ARG;
+    if (n_rest) std::memcpy(rest, c->shard_rest.data(), 4 * n_rest);
+    if (n_runs) std::memcpy(runs, c->shard_runs.data(), 12 * n_runs);
+    return GK_OK;
+}
+
+static int shard_sort_range_impl(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                                 const uint32_t *rest, uint64_t n_rest, const uint32_t *runs, uint64_t n_runs,
+                                 bool given, uint64_t *n_kept);
+
+extern "C" int gk_shard_sort_range_b(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                                     const uint32_t *rest, uint64_t n_rest, const uint32_t *runs, uint64_t n_runs,
+                                     uint64_t *n_kept) {
+    if ((n_rest && !rest) || (n_runs && !runs)) return GK_E_ARG;
+    return shard_sort_range_impl(c, k, flags, digit_lo, digit_hi, rest, n_rest, runs, n_runs, true, n_kept);
+}
+
 extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
                                    uint64_t *n_kept) {
+    return shard_sort_range_impl(c, k, flags, digit_lo, digit_hi, nullptr, 0, nullptr, 0, false, n_kept);
+}
+
+static int shard_sort_range_impl(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                                 const uint32_t *rest, uint64_t n_rest, const uint32_t *runs, uint64_t n_runs,
+                                 bool given, uint64_t *n_kept) {
     if (!c || !n_kept) return GK_E_ARG;
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
@@ -1027,6 +1080,11 @@ extern "C" int gk_shard_sort_range(gk_ctx *c, uint32_t k, uint32_t flags, uint32
     if (range_split(c, ks)) {  // mixed sba: ACGT-only k-mers by 2-bit digit, the rest by prefix
         const int ob = range_own_bits(acgt_spec(ks));
         SplitRange rg{digit_lo, digit_hi, range_prefix(digit_lo, true, ob), range_prefix(digit_hi, false, ob), (ob + 1) / 2};
+        rg.given = given;
+        rg.rest = rest;
+        rg.n_rest = n_rest;
+        rg.runs = runs;
+        rg.n_runs = n_runs;
         bool used = false;
         rc = split_sort(c, ks, &used, &rg);
         if (rc == GK_OK && !used) rc = fail(c, GK_E_HIP, "key-range split sort not applicable");

@@ -128,6 +128,7 @@ struct gk_ctx {
     uint64_t dhist_cap = 0;
     uint8_t *mask = nullptr;
     uint64_t mask_cap = 0, mask_n = 0;
+    std::vector<uint32_t> shard_rest, shard_runs;  // gk_shard_class_b's lists (host)
     uint8_t *hmask = nullptr;  // gk_set_group_heads
     uint64_t hmask_cap = 0, hmask_n = 0;
     uint32_t *ranks = nullptr;      // doubling: rank per sba position
@@ -181,8 +182,17 @@ int msd_sort(gk_ctx *c, const KeySpec &ks);
 struct SplitRange {
     uint32_t d_lo, d_hi, p4_lo, p4_hi;
     int pns = 4;  // symbols of the (4-bit) prefixes p4_lo / p4_hi (no upper bound: 1 << 4 pns)
+    // given: the class-B k-mers of the whole sba, selected per position share and gathered
+    // (gk_shard_class_b), instead of a whole-sequence scan: non-homopolymer starts and
+    // homopolymer runs (first start, count, canonical letter), host memory, in start order
+    bool given = false;
+    const uint32_t *rest = nullptr, *runs = nullptr;
+    uint64_t n_rest = 0, n_runs = 0;
 };
 int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg = nullptr);
+int split_shard_class_b(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, const std::vector<uint32_t> &bins,
+                        int pns, uint32_t homo_w16, uint64_t *hist, std::vector<uint32_t> *rest,
+                        std::vector<uint32_t> *runs);
 // multi-GPU shards (gkm_msd.hip): send-side partition of the k-mers starting in [lo, hi) by the
 // top msd_radix_bits() key bits; receive-side sort of buckets given as pieces
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,

@@ -92,7 +92,8 @@ __device__ __forceinline__ uint32_t b_prefix(const uint8_t *sba, uint64_t p, int
 // thread t owns positions 32 t .. 32 t + 31).  Key-range shards keep only the k-mers whose
 // b_prefix4 lies in their interval.
 template <bool STORE>
-__global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__restrict__ sba, uint64_t L, int k,
+__global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__restrict__ sba, uint64_t base,
+                                                             uint64_t L, int k,
                                                              int canonical, uint32_t p4_lo, uint32_t p4_hi, int pns,
                                                              uint32_t *__restrict__ cnt_r, uint32_t *__restrict__ cnt_h,
                                                              const uint32_t *__restrict__ off_r,
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void class_b_select_kernel(const uint8_t *__re
     s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
     s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
     const bool ranged = p4_lo != 0 || p4_hi != (1u << (4 * pns));
-    const uint64_t P0 = (uint64_t)blockIdx.x * kFlagTile;
+    const uint64_t P0 = base + (uint64_t)blockIdx.x * kFlagTile;  // positions >= L are not taken
     // the tile's 256 groups and the 3 halo groups: every load issued before any flag work (a second
     // loop trip for the halo would double the load latency of the tile)
     static_assert(kFlagGroups - 256 <= 256, "one halo group per thread at most");
@@ -254,6 +255,89 @@ __global__ __launch_bounds__(256) void gather_u32_kernel(const uint32_t *__restr
                                                          const uint32_t *__restrict__ idx, uint64_t n,
                                                          uint32_t *__restrict__ dst) {
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[idx[i]];
+}
+
+// ---------------------------------------------------------------------------------------------
+// key-range shards with position-sharded class-B selection (gk_shard_class_b)
+// ---------------------------------------------------------------------------------------------
+// Homopolymer starts (in start order) as runs: a run continues while the starts are consecutive
+// and the (canonical) letter stays the same
+__global__ __launch_bounds__(256) void homo_run_heads_kernel(const uint8_t *__restrict__ sba,
+                                                             const uint32_t *__restrict__ hs, uint64_t n, int canonical,
+                                                             uint8_t *__restrict__ f) {
+    __shared__ uint8_t s_comp[256];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t p = hs[i];
+        f[i] = (i == 0 || hs[i - 1] + 1 != p ||
+                homo_letter(sba, hs[i - 1], canonical, s_comp) != homo_letter(sba, p, canonical, s_comp)) ? 1 : 0;
+    }
+}
+
+// runs[3 g .. 3 g + 2] = (first start, number of starts, canonical letter)
+__global__ __launch_bounds__(256) void homo_runs_kernel(const uint8_t *__restrict__ sba, const uint32_t *__restrict__ hs,
+                                                        uint64_t n, const uint32_t *__restrict__ heads, uint64_t G,
+                                                        int canonical, uint32_t *__restrict__ runs) {
+    __shared__ uint8_t s_comp[256];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < G; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t p = hs[heads[g]];
+        runs[3 * g] = p;
+        runs[3 * g + 1] = (uint32_t)((g + 1 < G ? heads[g + 1] : n) - heads[g]);
+        runs[3 * g + 2] = homo_letter(sba, p, canonical, s_comp);
+    }
+}
+
+// ownership bin of each non-homopolymer B k-mer: the largest digit d with prefix(d) <= its prefix
+// (prefix(d) = bins[d], ascending), counted into hist
+__global__ __launch_bounds__(256) void b_bin_kernel(const uint8_t *__restrict__ sba, const uint32_t *__restrict__ st,
+                                                    uint64_t n, int k, int canonical, int pns,
+                                                    const uint32_t *__restrict__ bins, uint32_t nbins,
+                                                    uint32_t *__restrict__ hist) {
+    __shared__ uint8_t s_lut4[256], s_comp[256];
+    s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t x = b_prefix(sba, st[i], k, false, canonical, s_lut4, s_comp, pns);
+        uint32_t lo = 0, hi = nbins;  // first bin with bins[d] > x
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (bins[mid] <= x) lo = mid + 1;
+            else hi = mid;
+        }
+        atomicAdd(&hist[lo - 1], 1u);  // bins[0] == 0 <= x
+    }
+}
+
+// keep flags of gathered non-homopolymer B starts: (canonical) prefix in [p4_lo, p4_hi)
+__global__ __launch_bounds__(256) void b_keep_kernel(const uint8_t *__restrict__ sba, const uint32_t *__restrict__ st,
+                                                     uint64_t n, int k, int canonical, int pns, uint32_t p4_lo,
+                                                     uint32_t p4_hi, uint8_t *__restrict__ f) {
+    __shared__ uint8_t s_lut4[256], s_comp[256];
+    s_lut4[threadIdx.x] = c_code4_split[threadIdx.x];
+    s_comp[threadIdx.x] = c_comp_split[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t x = b_prefix(sba, st[i], k, false, canonical, s_lut4, s_comp, pns);
+        f[i] = (x >= p4_lo && x < p4_hi) ? 1 : 0;
+    }
+}
+
+// the owned homopolymer runs expanded into starts: run r = (first start, output offset)
+__global__ __launch_bounds__(256) void expand_runs_kernel(const uint32_t *__restrict__ rs, const uint64_t *__restrict__ ro,
+                                                          uint32_t nr, uint64_t n, uint32_t *__restrict__ out) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        uint32_t lo = 0, hi = nr;  // last run with ro[r] <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ro[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        out[i] = rs[lo] + (uint32_t)(i - ro[lo]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -414,6 +498,98 @@ __global__ __launch_bounds__(256) void fill_u64_kernel(uint64_t *__restrict__ p,
 
 static unsigned grid_of_n(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384)); }
 
+static const char kAlpha4[] = "$ABCDGHKMNRSTVWY";  // 4-bit code = index
+
+static uint32_t letter_code4(uint32_t ch) {
+    const char *at = ch ? std::strchr(kAlpha4, (int)ch) : nullptr;
+    return at ? (uint32_t)(at - kAlpha4) : 0;
+}
+
+// the pns-symbol 4-bit prefix of a homopolymer k-mer of (canonical) letter ch
+static uint32_t homo_prefix(uint32_t ch, int pns) {
+    uint32_t v = 0;
+    for (int t = 0; t < pns; ++t) v = (v << 4) | letter_code4(ch);
+    return v;
+}
+
+// Class-B k-mers starting in [lo, hi) for key-range shards (gk_shard_class_b): the non-homopolymer
+// starts and the homopolymer runs (first start, count, canonical letter) to the host, in start
+// order, and their ownership bins added to hist (bins[d] = the pns-symbol prefix of digit d's
+// smallest k-mer, ascending; a homopolymer k-mer weighs homo_w16 / 16 of a k-mer)
+int split_shard_class_b(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, const std::vector<uint32_t> &bins,
+                        int pns, uint32_t homo_w16, uint64_t *hist, std::vector<uint32_t> *rest,
+                        std::vector<uint32_t> *runs) {
+    rest->clear();
+    runs->clear();
+    hi = std::min<uint64_t>(hi, c->sba_len);
+    if (hi <= lo) return GK_OK;
+    if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
+    GK_TRY_HIP(c, split_tables());
+    const int k = ks.symbols;
+    const unsigned ftiles = (unsigned)((hi - lo + kFlagTile - 1) / kFlagTile);
+    uint32_t *cr, *chh, *orr, *ohh, *rs, *hs;
+    GK_TRY_HIP(c, scratch(c, "split_cnt_r", ftiles + 1, &cr));
+    GK_TRY_HIP(c, scratch(c, "split_cnt_h", ftiles + 1, &chh));
+    GK_TRY_HIP(c, scratch(c, "split_off_r", ftiles + 1, &orr));
+    GK_TRY_HIP(c, scratch(c, "split_off_h", ftiles + 1, &ohh));
+    int slot;
+    timer_begin(c, "split_b_select", &slot);
+    const uint32_t all = 1u << (4 * 4);
+    hipLaunchKernelGGL(class_b_select_kernel<false>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, lo, hi, k,
+                       ks.canonical, 0u, all, 4, cr, chh, nullptr, nullptr, nullptr, nullptr);
+    GK_TRY_HIP(c, hipGetLastError());
+    uint64_t nR = 0, nH = 0;
+    GK_TRY_HIP(c, scan_u32_exclusive_pair(c, cr, orr, chh, ohh, ftiles, &nR, &nH));
+    GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &rs));
+    GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &hs));
+    hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, lo, hi, k,
+                       ks.canonical, 0u, all, 4, cr, chh, orr, ohh, rs, hs);
+    GK_TRY_HIP(c, hipGetLastError());
+    timer_end(c, slot);
+    const uint32_t nbins = (uint32_t)bins.size();
+    if (nR > 0) {
+        rest->resize(nR);
+        GK_TRY_HIP(c, hipMemcpyAsync(rest->data(), rs, 4 * nR, hipMemcpyDeviceToHost, c->stream));
+        uint32_t *d_bins, *d_hist;
+        GK_TRY_HIP(c, scratch(c, "split_bins", nbins, &d_bins));
+        GK_TRY_HIP(c, scratch(c, "split_bhist", nbins, &d_hist));
+        GK_TRY_HIP(c, hipMemcpyAsync(d_bins, bins.data(), 4 * nbins, hipMemcpyHostToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(d_hist, 0, 4 * nbins, c->stream));
+        hipLaunchKernelGGL(b_bin_kernel, dim3(grid_of_n(nR)), dim3(256), 0, c->stream, c->sba, rs, nR, k, ks.canonical,
+                           pns, d_bins, nbins, d_hist);
+        GK_TRY_HIP(c, hipGetLastError());
+        std::vector<uint32_t> bh(nbins);
+        GK_TRY_HIP(c, hipMemcpyAsync(bh.data(), d_hist, 4 * nbins, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint32_t d = 0; d < nbins; ++d) hist[d] += bh[d];
+    }
+    if (nH > 0) {
+        uint8_t *f;
+        uint32_t *heads, *d_runs;
+        GK_TRY_HIP(c, scratch(c, "split_h_lf", nH + 64, &f));
+        GK_TRY_HIP(c, scratch(c, "split_h_idx", nH + 64, &heads));
+        hipLaunchKernelGGL(homo_run_heads_kernel, dim3(grid_of_n(nH)), dim3(256), 0, c->stream, c->sba, hs, nH,
+                           ks.canonical, f);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t G = 0;
+        GK_TRY_HIP(c, select_flags(c, f, nH, heads, &G));
+        GK_TRY_HIP(c, scratch(c, "split_runs", 3 * G + 64, &d_runs));
+        hipLaunchKernelGGL(homo_runs_kernel, dim3(grid_of_n(G)), dim3(256), 0, c->stream, c->sba, hs, nH, heads, G,
+                           ks.canonical, d_runs);
+        GK_TRY_HIP(c, hipGetLastError());
+        runs->resize(3 * G);
+        GK_TRY_HIP(c, hipMemcpyAsync(runs->data(), d_runs, 12 * G, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint64_t g = 0; g < G; ++g) {
+            const uint32_t x = homo_prefix((*runs)[3 * g + 2], pns);
+            const uint64_t d = (uint64_t)(std::upper_bound(bins.begin(), bins.end(), x) - bins.begin()) - 1;
+            hist[d] += ((uint64_t)(*runs)[3 * g + 1] * homo_w16 + 15) / 16;
+        }
+    }
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // driver
 // ---------------------------------------------------------------------------------------------
@@ -440,18 +616,65 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     GK_TRY_HIP(c, scratch(c, "split_off_h", ftiles + 1, &ohh));
     const int pns = rg ? rg->pns : 4;
     const uint32_t p4_lo = rg ? rg->p4_lo : 0u, p4_hi = rg ? rg->p4_hi : (1u << (4 * pns));
+    uint64_t nR = 0, nH = 0;
+    if (rg && rg->given) {
+        // 1'. the B k-mers of every rank's position share, gathered (gk_shard_class_b): keep the
+        // non-homopolymer ones whose prefix is in the rank's interval, expand the owned runs
+        timer_begin(c, "split_b_given", &slot);
+        uint32_t *g_rest = nullptr;
+        uint8_t *f;
+        if (rg->n_rest > 0) {
+            GK_TRY_HIP(c, scratch(c, "split_g_rest", rg->n_rest + 64, &g_rest));
+            GK_TRY_HIP(c, scratch(c, "split_h_lf", rg->n_rest + 64, &f));
+            GK_TRY_HIP(c, scratch(c, "split_h_idx", rg->n_rest + 64, &b_st[1]));
+            GK_TRY_HIP(c, hipMemcpyAsync(g_rest, rg->rest, 4 * rg->n_rest, hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(b_keep_kernel, dim3(grid_of_n(rg->n_rest)), dim3(256), 0, c->stream, c->sba, g_rest,
+                               rg->n_rest, k, ks.canonical, pns, p4_lo, p4_hi, f);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, select_flags(c, f, rg->n_rest, b_st[1], &nR));
+        }
+        std::vector<uint32_t> own_s;
+        std::vector<uint64_t> own_o;
+        for (uint64_t g = 0; g < rg->n_runs; ++g) {
+            const uint32_t x = homo_prefix(rg->runs[3 * g + 2], pns);
+            if (x < p4_lo || x >= p4_hi) continue;
+            own_s.push_back(rg->runs[3 * g]);
+            own_o.push_back(nH);
+            nH += rg->runs[3 * g + 1];
+        }
+        GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &b_st[0]));
+        GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &h_st));
+        if (nR > 0) {
+            hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_of_n(nR)), dim3(256), 0, c->stream, g_rest, b_st[1], nR,
+                               b_st[0]);
+            GK_TRY_HIP(c, hipGetLastError());
+        }
+        if (nH > 0) {
+            uint32_t *d_rs;
+            uint64_t *d_ro;
+            GK_TRY_HIP(c, scratch(c, "split_own_rs", own_s.size() + 1, &d_rs));
+            GK_TRY_HIP(c, scratch(c, "split_own_ro", own_o.size() + 1, &d_ro));
+            GK_TRY_HIP(c, hipMemcpyAsync(d_rs, own_s.data(), 4 * own_s.size(), hipMemcpyHostToDevice, c->stream));
+            GK_TRY_HIP(c, hipMemcpyAsync(d_ro, own_o.data(), 8 * own_o.size(), hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(expand_runs_kernel, dim3(grid_of_n(nH)), dim3(256), 0, c->stream, d_rs, d_ro,
+                               (uint32_t)own_s.size(), nH, h_st);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));  // own_s / own_o leave scope
+        }
+        timer_end(c, slot);
+    } else {
     timer_begin(c, "split_b_select", &slot);
-    hipLaunchKernelGGL(class_b_select_kernel<false>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
+    hipLaunchKernelGGL(class_b_select_kernel<false>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, 0ull, L, k,
                        ks.canonical, p4_lo, p4_hi, pns, cr, chh, nullptr, nullptr, nullptr, nullptr);
     GK_TRY_HIP(c, hipGetLastError());
-    uint64_t nR = 0, nH = 0;
     GK_TRY_HIP(c, scan_u32_exclusive_pair(c, cr, orr, chh, ohh, ftiles, &nR, &nH));
     GK_TRY_HIP(c, scratch(c, "split_b_st0", nR + 64, &b_st[0]));
     GK_TRY_HIP(c, scratch(c, "split_h_st", nH + 64, &h_st));
-    hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, L, k,
+    hipLaunchKernelGGL(class_b_select_kernel<true>, dim3(ftiles), dim3(256), 0, c->stream, c->sba, 0ull, L, k,
                        ks.canonical, p4_lo, p4_hi, pns, cr, chh, orr, ohh, b_st[0], h_st);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
+    }
     const uint64_t nB = nR + nH;
     if (nB > n) return fail(c, GK_E_HIP, "split: more class-B k-mers than k-mers");
     if (!rg && nB * 4 > n) return GK_OK;  // mostly non-ACGT k-mers: the plain 4-bit MSD is the better sort
@@ -586,7 +809,6 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
             out += m;
             return e;
         };
-        static const char kAlpha4[] = "$ABCDGHKMNRSTVWY";  // 4-bit code = index
         for (size_t g = 0; g < letters.size(); ++g) {
             GK_TRY_HIP(c, copy_rest(ins[g]));
             const uint64_t m = hc[letters[g]];
@@ -594,8 +816,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
             GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 0, m, c->stream));
             GK_TRY_HIP(c, hipMemsetAsync(fhd + out, 1, 1, c->stream));  // one group: one head
             if (WK) {  // the group's k-mer: its (canonical) letter k times
-                const char *at = std::strchr(kAlpha4, (int)letters[g]);
-                const uint64_t c4 = at && letters[g] ? (uint64_t)(at - kAlpha4) : 0;
+                const uint64_t c4 = letter_code4(letters[g]);
                 for (int q = 0; q < WK; ++q) {  // q: word from the most significant end
                     uint64_t v = 0;
                     const int lo_sym = 16 * (WK - 1 - q);  // nibble index of the word's bit 0

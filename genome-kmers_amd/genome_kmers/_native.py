@@ -54,7 +54,8 @@ EXPORTED = (
     "gk_set_group_heads", "gk_group_hist", "gk_group_members", "gk_unique_counts", "gk_copy_unique", "gk_device_unique", "gk_device_views",
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
-    "gk_shard_histogram", "gk_shard_sort_range",
+    "gk_shard_histogram", "gk_shard_sort_range", "gk_shard_class_b", "gk_shard_class_b_copy",
+    "gk_shard_sort_range_b",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
@@ -131,6 +132,11 @@ _SIGS = {
                            ctypes.c_int),
     "gk_shard_sort_range": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U64P],
                             ctypes.c_int),
+    "gk_shard_class_b": ([_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _U64P, _U64P,
+                          _U64P], ctypes.c_int),
+    "gk_shard_class_b_copy": ([_P, _U32P, ctypes.c_uint64, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_shard_sort_range_b": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _U32P,
+                               ctypes.c_uint64, _U32P, ctypes.c_uint64, _U64P], ctypes.c_int),
     "gk_fasta_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P), _U64P, _U64P, _U64P], ctypes.c_int),
     "gk_fasta_fill": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_char_p, _U8P], ctypes.c_int),
     "gk_fasta_close": ([_P], None),
@@ -422,6 +428,35 @@ class Engine:
         self._check(self.lib.gk_shard_histogram(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
                                                 _ptr(hist, ctypes.c_uint64), ctypes.byref(bits)))
         return hist[:1 << bits.value].copy(), bits.value
+
+    def shard_class_b(self, lo: int, hi: int, k: int, hist: np.ndarray, canonical: bool = False):
+        """Class-B k-mers starting in [lo, hi) (gk_shard_class_b): (non-homopolymer starts uint32[m],
+        homopolymer runs uint32[r, 3] = (first start, count, letter)); their ownership bins are added
+        to ``hist`` (uint64, gk_shard_histogram's bins) in place.  ACGT-only sba: two empty arrays."""
+        full = np.zeros(4096, dtype=np.uint64)
+        full[:len(hist)] = hist
+        nr, nh = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._check(self.lib.gk_shard_class_b(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
+                                              _ptr(full, ctypes.c_uint64), ctypes.byref(nr), ctypes.byref(nh)))
+        hist[:] = full[:len(hist)]
+        rest = np.empty(nr.value, dtype=np.uint32)
+        runs = np.empty((nh.value, 3), dtype=np.uint32)
+        self._check(self.lib.gk_shard_class_b_copy(self.ctx, _ptr(rest, ctypes.c_uint32), nr.value,
+                                                   _ptr(runs, ctypes.c_uint32), nh.value))
+        return rest, runs
+
+    def shard_sort_range_b(self, k: int, digit_lo: int, digit_hi: int, rest: np.ndarray, runs: np.ndarray,
+                           canonical: bool = False) -> int:
+        """shard_sort_range with the class-B k-mers of the whole sba given (every rank's
+        shard_class_b lists concatenated in rank order) instead of scanned for."""
+        rest = np.ascontiguousarray(rest, dtype=np.uint32)
+        runs = np.ascontiguousarray(runs, dtype=np.uint32).reshape(-1, 3)
+        n = ctypes.c_uint64(0)
+        self._check(self.lib.gk_shard_sort_range_b(self.ctx, k, SORT_CANONICAL if canonical else 0, digit_lo,
+                                                   digit_hi, _ptr(rest, ctypes.c_uint32), len(rest),
+                                                   _ptr(runs, ctypes.c_uint32), len(runs), ctypes.byref(n)))
+        self.n = n.value
+        return n.value
 
     def shard_sort_range(self, k: int, digit_lo: int, digit_hi: int, canonical: bool = False) -> int:
         """Sort the k-mers of the whole sequence whose top digit is in [digit_lo, digit_hi); returns

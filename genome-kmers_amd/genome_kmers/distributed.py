@@ -200,10 +200,16 @@ class KeyRangeKmerSort:
     moving k-mers to their owner, each rank re-derives its own from the sequence:
 
     1. ``shard_histogram``: top-digit histogram of the k-mers starting in the rank's position share;
-    2. ``all_reduce`` (sum) of the 4096-digit histograms -- 32 KiB, the only collective -- and the same split of
-       the digits into N contiguous ranges of about n/N k-mers on every rank (``split_buckets``);
-    3. ``shard_sort_range``: the rank scans the whole sequence, keeps the k-mers of its digit range
-       (compacted per wave before ranking, so the kept share sets the cost) and sorts them.
+       on a mixed sba (N runs, IUPAC letters) also ``shard_class_b``: the share's class-B k-mers
+       (some non-ACGT letter) as short host lists -- non-homopolymer starts and homopolymer runs --
+       with their ownership digits added to the histogram;
+    2. ``all_reduce`` (sum) of the 4096-digit histograms -- 32 KiB -- and the same split of the
+       digits into N contiguous ranges of about n/N k-mers on every rank (``split_buckets``); on a
+       mixed sba an ``all_gather`` of the class-B lists (runs keep them small: GRCh38's N runs are
+       ~100 runs, not 150 M starts);
+    3. ``shard_sort_range`` / ``shard_sort_range_b``: the rank scans the whole sequence for its
+       ACGT-only k-mers (compacted per wave before ranking, so the kept share sets the cost), keeps
+       the gathered class-B k-mers of its interval, and sorts them.
 
     Rank r's sorted k-mers are the r-th slice of the single-GPU order (``Kmers.sort``,
     kmers.py:1624-1652, with break_ties=True, kmers.py:1710-1711): digit ranges ascend with the
@@ -234,15 +240,43 @@ class KeyRangeKmerSort:
         self.local_kmers = 0
         self.digit_bounds = None
 
+    def _gather_class_b(self, rest: np.ndarray, runs: np.ndarray):
+        """all_gather of every rank's class-B lists; concatenated in rank order = start order."""
+        torch, dist = self.torch, self.dist
+        sizes = torch.tensor([len(rest), len(runs)], dtype=torch.int64, device=self.dev)
+        every = [torch.zeros_like(sizes) for _ in range(self.world)]
+        dist.all_gather(every, sizes, group=self.group)
+        every = [(int(t[0]), int(t[1])) for t in (e.cpu() for e in every)]
+        width = max(1, max(a + 3 * b for a, b in every))
+        mine = np.zeros(width, dtype=np.uint32)
+        mine[:len(rest)] = rest
+        mine[len(rest):len(rest) + runs.size] = runs.reshape(-1)
+        buf = torch.from_numpy(mine.view(np.int32)).to(self.dev)
+        out = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(out, buf, group=self.group)
+        got = [o.cpu().numpy().view(np.uint32) for o in out]
+        rest_all = np.concatenate([g[:a] for g, (a, b) in zip(got, every)])
+        runs_all = np.concatenate([g[a:a + 3 * b] for g, (a, b) in zip(got, every)]).reshape(-1, 3)
+        return rest_all, runs_all
+
     def run(self) -> int:
         """One sort; returns this rank's number of distinct k-mers."""
         torch, dist = self.torch, self.dist
         hist, bits = self.engine.shard_histogram(self.lo, self.hi, self.k, canonical=self.canonical)
-        h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to(self.dev)
+        hist = np.asarray(hist, dtype=np.uint64)
+        mixed = not self.engine.is_acgt() and self.k >= 4  # the same on every rank (same sba)
+        if mixed:
+            rest, runs = self.engine.shard_class_b(self.lo, self.hi, self.k, hist, canonical=self.canonical)
+        h = torch.from_numpy(hist.astype(np.int64)).to(self.dev)
         dist.all_reduce(h, group=self.group)
         bounds = split_buckets(h.cpu().numpy(), self.world)
         self.digit_bounds = bounds
-        self.local_kmers = self.engine.shard_sort_range(self.k, bounds[self.rank], bounds[self.rank + 1],
-                                                        canonical=self.canonical)
+        if mixed:
+            rest_all, runs_all = self._gather_class_b(rest, runs)
+            self.local_kmers = self.engine.shard_sort_range_b(self.k, bounds[self.rank], bounds[self.rank + 1],
+                                                              rest_all, runs_all, canonical=self.canonical)
+        else:
+            self.local_kmers = self.engine.shard_sort_range(self.k, bounds[self.rank], bounds[self.rank + 1],
+                                                            canonical=self.canonical)
         self.engine.materialize_keys()  # sorted keys + unique starts and counts stay in HBM
         return self.engine.unique_count_only()

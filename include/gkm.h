@@ -224,6 +224,23 @@ int gk_shard_histogram(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32
                        uint32_t *bits);
 int gk_shard_sort_range(gk_ctx *ctx, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
                         uint64_t *n_kept);
+/* Key-range shards of a mixed sba (N runs, IUPAC letters) without a whole-sequence class-B scan
+ * per rank:
+ * gk_shard_class_b: the class-B k-mers (some non-ACGT letter) STARTING in [lo, hi) -- the rank's
+ *   position share -- kept in the context as host lists in start order: n_rest non-homopolymer
+ *   starts and n_runs homopolymer runs (first start, count, canonical letter: three uint32 each);
+ *   their ownership digits are ADDED to h_hist (gk_shard_histogram's bins; a homopolymer k-mer
+ *   weighs half), so the all-reduced histogram balances them too.  An ACGT-only sba gives 0, 0.
+ * gk_shard_class_b_copy: the two lists out (sizes as returned).
+ * gk_shard_sort_range_b: gk_shard_sort_range with the class-B k-mers of the WHOLE sba given as the
+ *   concatenation, in rank order, of every rank's lists (all-gathered): the rank keeps those in its
+ *   interval instead of scanning the sequence for them. */
+int gk_shard_class_b(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
+                     uint64_t *n_rest, uint64_t *n_runs);
+int gk_shard_class_b_copy(gk_ctx *ctx, uint32_t *rest, uint64_t n_rest, uint32_t *runs, uint64_t n_runs);
+int gk_shard_sort_range_b(gk_ctx *ctx, uint32_t k, uint32_t flags, uint32_t digit_lo, uint32_t digit_hi,
+                          const uint32_t *rest, uint64_t n_rest, const uint32_t *runs, uint64_t n_runs,
+                          uint64_t *n_kept);
 
 /* Location of selected k-mers for Kmers.get_kmers(kmer_info_to_yield="full") (kmers.py:1180-1264):
  * sba_idx[i] = kmer_sba_start_indices[kmer_nums[i]] and seg[i] = the segment holding it

@@ -110,6 +110,9 @@ class NumpyShardEngine:
         self.keys, self.starts = key[order], s[order]
         return len(s)
 
+    def is_acgt(self):
+        return bool(np.isin(self.sba, np.frombuffer(b"ACGT$", dtype=np.uint8)).all())
+
     def materialize_keys(self):
         return 1  # the double keeps its sorted keys on the host
 
@@ -215,6 +218,68 @@ def test_gloo_world2_matches_oracle(scheme, contigs, chunk):
     assert sum(r[2] for r in res) == len(np.unique(_keys(sba, starts.astype(np.int64), K)))
 
 
+class ClassBGatherEngine(NumpyShardEngine):
+    """A mixed-alphabet double for the class-B exchange of KeyRangeKmerSort: each rank reports
+    made-up class-B lists of uneven sizes (one rank none) and the lists it is handed back are
+    recorded; the sort itself is the ACGT double's."""
+
+    def is_acgt(self):
+        return False
+
+    def shard_class_b(self, lo, hi, k, hist, canonical=False):
+        r = int(lo // 1024)
+        rest = np.arange(lo, lo + 3 * r, 3, dtype=np.uint32)
+        runs = np.array([[lo + 1000 + j, 40 + j, ord("N")] for j in range(r % 3)], dtype=np.uint32).reshape(-1, 3)
+        hist[0] += np.uint64(len(rest) + runs[:, 1].sum() // 2)
+        return rest, runs
+
+    def shard_sort_range_b(self, k, dlo, dhi, rest, runs, canonical=False):
+        self.given = (rest.tolist(), runs.tolist())
+        return self.shard_sort_range(k, dlo, dhi, canonical)
+
+
+def _gather_worker(rank, world, port, sba, seg, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        job = D.KeyRangeKmerSort(sba, seg, K, rank, world, engine=ClassBGatherEngine(),
+                                 torch_device=torch.device("cpu"))
+        job.lo, job.hi = 1024 * rank, 1024 * (rank + 1)  # (the double derives its lists from lo)
+        job.run()
+        q.put((rank, job.engine.given))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_class_b_lists_gathered_in_rank_order():
+    """KeyRangeKmerSort on a mixed sba: every rank receives the concatenation, in rank order, of
+    every rank's class-B lists (uneven sizes, an empty rank, runs as triples) over gloo."""
+    import torch.multiprocessing as mp
+
+    sba, seg = _random_sba(6000, 5)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, sba, seg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_rest, want_runs = [], []
+    for r in range(world):
+        want_rest += list(range(1024 * r, 1024 * r + 3 * r, 3))
+        want_runs += [[1024 * r + 1000 + j, 40 + j, ord("N")] for j in range(r % 3)]
+    for _, (rest, runs) in res:
+        assert rest == want_rest and runs == want_runs
+
+
 # ---- device shard entry points, two ranks in one process ---------------------------------------
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
@@ -306,6 +371,64 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     got, keys, uniq, kept = [], [], 0, 0
     for r in range(world):
         kept += e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
+        got.append(e.copy_starts())
+        keys.append(e.copy_keys())
+        uniq += e.unique_count_only()
+    assert kept == total
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(k)
+    ref.sort(k, canonical=canonical)
+    np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
+    np.testing.assert_array_equal(np.concatenate(keys), ref.copy_keys())
+    assert uniq == ref.unique_count_only()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,canonical", [
+    (2, 2, 63, True), (2, 1, 40, False), (5, 3, 31, False), (8, 2, 31, True), (3, 1, 5, False), (4, 2, 6, False)])
+def test_gpu_key_ranges_class_b_given(world, contigs, k, canonical):
+    """gk_shard_class_b per position share + gk_shard_sort_range_b with the gathered lists (no
+    whole-sequence class-B scan per rank): the histogram gains every class-B k-mer (homopolymers at
+    half weight), the ranks keep every k-mer exactly once, and their concatenation is gk_sort's."""
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(200_000 + 17, 3 + world, contigs)
+    sba[150_100:151_000] = sba[1000:1900]
+    sba[160_000:160_900] = oracle.reverse_complement(sba[1000:1900])
+    sba[5000:5100] = ord("N")
+    sba[90_000:90_050:7] = ord("R")
+    sba[120_000:120_300] = ord("N")
+    sba[130_000:130_080] = ord("Y")
+    sba[140_000:140_090] = ord("R")
+    bounds = D.position_ranges(len(sba), world)
+    bounds[1] = 120_128 if world == 2 else bounds[1]  # a homopolymer run across a share boundary
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    hist, rests, runs_l, plain = None, [], [], None
+    for r in range(world):
+        h, bits = e.shard_histogram(bounds[r], bounds[r + 1], k, canonical=canonical)
+        h = np.asarray(h, dtype=np.uint64)
+        h0 = h.astype(np.int64)
+        plain = h0 if plain is None else plain + h0
+        rest, runs = e.shard_class_b(bounds[r], bounds[r + 1], k, h, canonical=canonical)
+        assert np.all(rest >= bounds[r]) and np.all(rest < bounds[r + 1])
+        assert np.all(np.diff(rest.astype(np.int64)) > 0)
+        if len(runs):
+            assert np.all(runs[:, 0] >= bounds[r]) and np.all(runs[:, 0] < bounds[r + 1])
+        added = int(h.astype(np.int64).sum()) - int(h0.sum())
+        assert added == len(rest) + sum((int(c) + 1) // 2 for c in runs[:, 1])
+        hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
+        rests.append(rest)
+        runs_l.append(runs)
+    rest_all, runs_all = np.concatenate(rests), np.concatenate(runs_l).reshape(-1, 3)
+    total = D.count_kmers(len(sba), seg, k)
+    # every non-ACGT k-mer is in exactly one list entry
+    assert int(plain.sum()) + len(rest_all) + int(runs_all[:, 1].sum()) == total
+    db = D.split_buckets(hist, world)
+    got, keys, uniq, kept = [], [], 0, 0
+    for r in range(world):
+        kept += e.shard_sort_range_b(k, db[r], db[r + 1], rest_all, runs_all, canonical=canonical)
         got.append(e.copy_starts())
         keys.append(e.copy_keys())
         uniq += e.unique_count_only()
@@ -430,7 +553,8 @@ def _gpu_range_worker(rank, world, port, sba, seg, k, q):
 
 
 @pytest.mark.gpu
-def test_gpu_key_range_two_processes():
+@pytest.mark.parametrize("iupac", [False, True])
+def test_gpu_key_range_two_processes(iupac):
     """Two ranks as separate processes (gloo for the 2 KiB all-reduce), each with its own libgkm
     engine on GPU 0: the rank-ordered concatenation equals the single-GPU sort."""
     import torch.multiprocessing as mp
@@ -439,6 +563,10 @@ def test_gpu_key_range_two_processes():
 
     sba, seg = _random_sba(300_000 + 5, 11, 3)
     sba[250_000:251_000] = sba[2000:3000]  # a repeat across contigs (inside the third one)
+    if iupac:  # class-B lists gathered over gloo (gk_shard_class_b / gk_shard_sort_range_b)
+        sba[60_000:60_400] = ord("N")
+        sba[149_000:151_000] = ord("N")  # across the two position shares
+        sba[90_000:90_050:7] = ord("R")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

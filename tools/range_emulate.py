@@ -3,9 +3,13 @@
 Every rank's device work runs on a single MI355X one after another, so each rank's device time is
 measured exactly; what a real N-GPU run adds is the collective:
 
-  --scheme range (KeyRangeKmerSort): gk_shard_histogram over the rank's position share, then
-      gk_shard_sort_range over its digit range (keys materialised, unique counts); the missing
-      collective is the 1 KiB all-reduce of the histograms.
+  --scheme range (KeyRangeKmerSort): gk_shard_histogram over the rank's position share (on a mixed
+      sba also gk_shard_class_b: the share's class-B lists), then gk_shard_sort_range (mixed:
+      gk_shard_sort_range_b with every share's lists) over its digit range (keys materialised,
+      unique counts); the collectives -- the 32 KiB all-reduce of the histograms, on a mixed sba
+      the all-gathers of the list sizes and lists, and the closing barrier -- are added as
+      collective_ms: a MEASURED one-rank RCCL run of the same calls (launch + host round trips) plus
+      a MODELLED ring cost per extra rank (RING_STEP_US per step, bytes at one xGMI link).
   --scheme a2a (ShardedKmerSort): gk_shard_partition of the rank's position share, then
       gk_shard_sort of the buckets it owns (pieces sliced from every rank's send buffer on the same
       GPU); the missing collective is the all-to-all, reported as a link-bound estimate: the
@@ -31,6 +35,51 @@ sys.path.insert(0, str(ROOT / "genome-kmers_amd"))
 sys.path.insert(0, str(ROOT))
 
 LINK_GBS = 153.0  # one xGMI link, per direction (MI355X_MICROARCH.md)
+RING_STEP_US = 10.0  # assumed latency of one ring step of a small RCCL collective over xGMI (modelled)
+
+
+def measure_collectives(reps=20):
+    """One-rank RCCL (world size 1) all-reduce of the 4096-bin histogram, two all-gathers and a
+    barrier, as KeyRangeKmerSort.run issues them: the launch and host round-trip part of the
+    collectives, measured (ms, best of reps)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    dev = torch.device("cuda", 0)
+    h = torch.zeros(4096, dtype=torch.int64, device=dev)
+    sz = torch.zeros(2, dtype=torch.int64, device=dev)
+    lst = torch.zeros(1024, dtype=torch.int32, device=dev)
+    out = {}
+    for name, fn in (("all_reduce", lambda: (dist.all_reduce(h), h.cpu())),
+                     ("all_gather_pair", lambda: (dist.all_gather([torch.empty_like(sz)], sz), sz.cpu(),
+                                                  dist.all_gather([torch.empty_like(lst)], lst), lst.cpu())),
+                     ("barrier", lambda: dist.barrier())):
+        best = None
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) * 1e3
+            best = dt if best is None else min(best, dt)
+        out[name] = round(best, 4)
+    dist.destroy_process_group()
+    return out
+
+
+def collective_ms(world, measured, gather_bytes, mixed):
+    """Measured one-rank cost + modelled ring steps: all-reduce 2 (N - 1) steps, all-gather N - 1
+    each, barrier ~ an all-reduce of nothing; bytes at one xGMI link."""
+    steps = 2 * (world - 1) + (2 * (world - 1) if mixed else 0) + 2 * (world - 1)
+    wire = (2 * (world - 1) / world * 32768 + ((world - 1) / world * gather_bytes if mixed else 0)) / (LINK_GBS * 1e9)
+    base = measured["all_reduce"] + measured["barrier"] + (measured["all_gather_pair"] if mixed else 0)
+    return base + steps * RING_STEP_US * 1e-3 + wire * 1e3
 
 
 def best_of(fn, reps, sync):
@@ -54,6 +103,8 @@ def main():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--worlds", type=str, default="8,4,2")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--b-scan", action="store_true",
+                    help="mixed sba: every rank scans the whole sequence for its class-B k-mers (round-2 path)")
     args = ap.parse_args()
 
     from genome_kmers import _native, synthetic
@@ -77,8 +128,12 @@ def main():
         return e.unique_count_only()
 
     single_ms, u1 = best_of(single, args.reps, e.sync)
+    mixed = not e.is_acgt() and k >= 4 and not args.b_scan
+    measured = measure_collectives() if args.scheme == "range" else None
     print(json.dumps({"config": args.config, "scheme": args.scheme, "single_gpu_ms": round(single_ms, 2),
-                      "kmers": total, "unique": u1, "timing": f"best of {args.reps} after a warm-up"}), flush=True)
+                      "kmers": total, "unique": u1, "timing": f"best of {args.reps} after a warm-up",
+                      "collectives_one_rank_ms": measured, "ring_step_us_modelled": RING_STEP_US,
+                      "label": "per-rank emulation on one GPU; unmeasured on multi-GPU hardware"}), flush=True)
 
     for world in [int(x) for x in args.worlds.split(",")]:
         pb = D.position_ranges(len(sba), world)
@@ -92,22 +147,37 @@ def main():
 
         if args.scheme == "range":
             full = np.zeros(4096, dtype=np.int64)
+            rests, runs_l = [], []
             for s in range(world):
                 h, bits = e.shard_histogram(pb[s], pb[s + 1], k, canonical=canonical)
+                h = np.asarray(h, dtype=np.uint64)
+                if mixed:
+                    rest, runs = e.shard_class_b(pb[s], pb[s + 1], k, h, canonical=canonical)
+                    rests.append(rest)
+                    runs_l.append(runs)
                 full[:len(h)] += h.astype(np.int64)
             db = D.split_buckets(full[:1 << bits], world)
+            rest_all = np.concatenate(rests) if mixed else None
+            runs_all = np.concatenate(runs_l).reshape(-1, 3) if mixed else None
+            gather_bytes = (4 * len(rest_all) + 12 * len(runs_all)) if mixed else 0
+            coll = collective_ms(world, measured, gather_bytes, mixed)
             for r in range(world):
                 def rank(last, r=r):
                     e.profile_enable(last)
-                    e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share
-                    n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
+                    h, _ = e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share
+                    if mixed:
+                        e.shard_class_b(pb[r], pb[r + 1], k, np.asarray(h, dtype=np.uint64), canonical=canonical)
+                        n = e.shard_sort_range_b(k, db[r], db[r + 1], rest_all, runs_all, canonical=canonical)
+                    else:
+                        n = e.shard_sort_range(k, db[r], db[r + 1], canonical=canonical)
                     e.materialize_keys()
                     u = e.unique_count_only()
                     rep = e.profile_report() if last else None
                     e.profile_enable(False)
                     return n, u, rep
                 ms, (n, u, rep) = best_of(rank, args.reps, e.sync)
-                record(ms, rep)
+                extra.append({"device_ms": round(ms, 2), "collective_ms": round(coll, 3), "kmers": int(n)})
+                record(ms + coll, rep)
                 uniq += u
                 kept += n
         else:

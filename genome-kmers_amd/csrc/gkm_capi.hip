@@ -1011,8 +1011,9 @@ extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
 }
 
 // the weight of a homopolymer k-mer in the ownership histogram, in 16ths of a sorted k-mer: it
-// skips the MSD sort, but is selected, grouped, keyed and merged
-constexpr uint32_t kHomoWeight16 = 8;
+// skips the MSD sort, but is expanded, grouped, keyed and merged (fitted to
+// the C4 emulation: 11/16 balances the rank that owns the N runs with the others)
+constexpr uint32_t kHomoWeight16 = 11;
 
 extern "C" int gk_shard_class_b(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
                                 uint64_t *n_rest, uint64_t *n_runs) {

@@ -1004,7 +1004,12 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
         if (li == l) put_entry(L, l, at[l], st, size, hi, parity, pref);
 }
 
-// keys of compact elements (one workgroup per bucket): prefix | digit | low bits
+// workgroups per bucket (grid.y) of the per-bucket copy kernels below: the buckets they see are
+// few but can be huge (a repeat's group of identical k-mers: 250 K elements at C4), and one
+// workgroup walking such a bucket alone took 3 ms per C4 rank
+static unsigned bucket_split(uint64_t nbuckets) { return nbuckets <= 4096 ? 32u : nbuckets <= 65536 ? 4u : 1u; }
+
+// keys of compact elements (gridDim.y workgroups per bucket): prefix | digit | low bits
 __global__ __launch_bounds__(256) void expand_compact_kernel(const uint32_t *__restrict__ bst,
                                                              const uint32_t *__restrict__ blen,
                                                              const uint64_t *__restrict__ bpref, int hi, int B,
@@ -1013,7 +1018,7 @@ __global__ __launch_bounds__(256) void expand_compact_kernel(const uint32_t *__r
     const uint64_t st = bst[blockIdx.x];
     const uint32_t len = blen[blockIdx.x];
     const uint64_t pf = bpref[blockIdx.x];
-    for (uint32_t e = threadIdx.x; e < len; e += 256) {
+    for (uint32_t e = blockIdx.y * 256 + threadIdx.x; e < len; e += gridDim.y * 256) {
         const uint64_t x = kio[st + e];
         kio[st + e] = compact_key(pf, hi, B, nd[st + e], (uint32_t)(x >> 32));
         vout[st + e] = (uint32_t)x;
@@ -1754,8 +1759,41 @@ __global__ __launch_bounds__(256) void tie_encode_flat_kernel(const uint8_t *__r
     }
 }
 
+// Next-level buckets whose keys are all equal (a repeat's group of identical k-mers: 250 K
+// elements of (CA)n at C4) would go through every remaining global level without splitting, each
+// with its host round trips.  uniform_flag_kernel marks the buckets holding two different keys
+// (gridDim.y workgroups per bucket); route_uniform_kernel sends the others to the done list.
+__global__ __launch_bounds__(256) void uniform_flag_kernel(const uint32_t *__restrict__ bst,
+                                                           const uint32_t *__restrict__ blen,
+                                                           const uint64_t *__restrict__ keys,
+                                                           uint32_t *__restrict__ mixed) {
+    const uint64_t st = bst[blockIdx.x];
+    const uint32_t len = blen[blockIdx.x];
+    const uint64_t k0 = keys[st];
+    uint64_t acc = 0;
+    for (uint32_t e = blockIdx.y * 256 + threadIdx.x; e < len; e += gridDim.y * 256) acc |= keys[st + e] ^ k0;
+    if (__syncthreads_or(acc != 0) && threadIdx.x == 0) atomicOr(&mixed[blockIdx.x], 1u);
+}
+
+__global__ __launch_bounds__(256) void route_uniform_kernel(const uint32_t *__restrict__ bst,
+                                                            const uint32_t *__restrict__ blen,
+                                                            const uint64_t *__restrict__ bpref, uint32_t nb,
+                                                            const uint32_t *__restrict__ mixed, Lists L, int parity,
+                                                            uint32_t *__restrict__ ctr,
+                                                            unsigned long long *__restrict__ sums) {
+    for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < nb; b += gridDim.x * 256) {
+        if (mixed[b]) {
+            const uint32_t at = atomicAdd(&ctr[kCtrBig], 1u);
+            put_entry(L, kCtrBig, at, bst[b], blen[b], 0, parity, bpref ? bpref[b] : 0);
+            atomicAdd(&sums[kCtrBig], (unsigned long long)blen[b]);
+        } else {
+            put_entry(L, kCtrDone, atomicAdd(&ctr[kCtrDone], 1u), bst[b], blen[b], 0, parity);
+        }
+    }
+}
+
 // sub-buckets whose key bits are exhausted: in order already (copied to buffer 0 if needed);
-// all keys equal, so the only head is the first element
+// all keys equal, so the only head is the first element (gridDim.y workgroups per bucket)
 __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restrict__ dn_start,
                                                         const uint32_t *__restrict__ dn_len,
                                                         const uint8_t *__restrict__ dn_par, const uint32_t *__restrict__ v1,
@@ -1765,7 +1803,7 @@ __global__ __launch_bounds__(256) void done_copy_kernel(const uint32_t *__restri
     const uint64_t st = dn_start[s];
     const uint32_t len = dn_len[s];
     const bool copy = dn_par[s];
-    for (uint32_t i = threadIdx.x; i < len; i += 256) {  // keys only in final-key sorts (k1 != null)
+    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < len; i += gridDim.y * 256) {  // keys: final-key sorts
         if (copy) v0[st + i] = v1[st + i];
         if (copy && k1) k0[st + i] = k1[st + i];
         heads[st + i] = i == 0;
@@ -2207,7 +2245,7 @@ struct MsdDriver {
     // back in keys[out], so that level reads keys as usual (the digit bytes stay valid for it)
     int expand_big(int out) {
         if (!compact_now || nbig == 0) return GK_OK;
-        hipLaunchKernelGGL(expand_compact_kernel, dim3(nbig), dim3(256), 0, c->stream, big_start[cur_big],
+        hipLaunchKernelGGL(expand_compact_kernel, dim3(nbig, bucket_split(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
                            big_len[cur_big], big_pref[cur_big], compact_hi, B, nd, c->keys[out], c->vals[out]);
         GK_TRY_HIP(c, hipGetLastError());
         return GK_OK;
@@ -2455,6 +2493,33 @@ struct MsdDriver {
         return finish();
     }
 
+    // before another global level: its buckets whose keys are all equal go to the done list
+    // (checked once the big buckets hold few elements: after L1 of a random genome they hold
+    // all of them and never are)
+    int drop_uniform(int level, int out) {
+        if (nbig == 0 || level < 1 || big_elems * 64 > std::max<uint64_t>(c->n, 1)) return GK_OK;
+        uint32_t *mixed;
+        GK_TRY_HIP(c, scratch(c, "uni_mixed", nbig, &mixed));
+        GK_TRY_HIP(c, hipMemsetAsync(mixed, 0, 4ull * nbig, c->stream));
+        hipLaunchKernelGGL(uniform_flag_kernel, dim3(nbig, bucket_split(nbig)), dim3(256), 0, c->stream,
+                           big_start[cur_big], big_len[cur_big], c->keys[out], mixed);
+        GK_TRY_HIP(c, grow_keep(c, "dn_start", ndone + nbig, ndone, &dn_start));
+        GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nbig, ndone, &dn_len));
+        GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nbig, ndone, &dn_par));
+        GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums + kCtrBig, 0, 8, c->stream));
+        hipLaunchKernelGGL(route_uniform_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
+                           big_len[cur_big], big_pref[cur_big], nbig, mixed, lists(0, cur_big ^ 1), out, ctr, sums);
+        GK_TRY_HIP(c, hipGetLastError());
+        cur_big ^= 1;
+        int r = read_ctr();
+        if (r != GK_OK) return r;
+        ndone = h[kCtrDone];
+        nbig = h[kCtrBig];
+        big_elems = hs[kCtrBig];
+        return GK_OK;
+    }
+
     // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
     // key bits are sorted
     int levels(int level, int hi, int in) {
@@ -2485,6 +2550,7 @@ struct MsdDriver {
             rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big, nullptr, nullptr, 1,
                           big_pref[cur_big ^ 1], width(level), compact_now ? 1 : 0);
             if (rc == GK_OK) rc = expand_big(out);
+            if (rc == GK_OK) rc = drop_uniform(level, out);
             if (rc != GK_OK) return rc;
             ++level;
             hi += width(level - 1);
@@ -2606,7 +2672,8 @@ struct MsdDriver {
             if (++round > 64) return fail(c, GK_E_HIP, "msd local rounds did not converge");
         }
         if (ndone > 0) {
-            hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone), dim3(256), 0, c->stream, dn_start, dn_len,
+            hipLaunchKernelGGL(done_copy_kernel, dim3((unsigned)ndone, bucket_split(ndone)), dim3(256), 0, c->stream,
+                               dn_start, dn_len,
                                dn_par, c->vals[1], c->vals[0], wkeys ? c->keys[1] : nullptr, c->keys[0], heads);
             GK_TRY_HIP(c, hipGetLastError());
         }

@@ -230,7 +230,7 @@ int gk_shard_sort_range(gk_ctx *ctx, uint32_t k, uint32_t flags, uint32_t digit_
  *   position share -- kept in the context as host lists in start order: n_rest non-homopolymer
  *   starts and n_runs homopolymer runs (first start, count, canonical letter: three uint32 each);
  *   their ownership digits are ADDED to h_hist (gk_shard_histogram's bins; a homopolymer k-mer
- *   weighs half), so the all-reduced histogram balances them too.  An ACGT-only sba gives 0, 0.
+ *   weighs 11/16), so the all-reduced histogram balances them too.  An ACGT-only sba gives 0, 0.
  * gk_shard_class_b_copy: the two lists out (sizes as returned).
  * gk_shard_sort_range_b: gk_shard_sort_range with the class-B k-mers of the WHOLE sba given as the
  *   concatenation, in rank order, of every rank's lists (all-gathered): the rank keeps those in its

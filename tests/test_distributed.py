@@ -390,7 +390,7 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
 def test_gpu_key_ranges_class_b_given(world, contigs, k, canonical):
     """gk_shard_class_b per position share + gk_shard_sort_range_b with the gathered lists (no
     whole-sequence class-B scan per rank): the histogram gains every class-B k-mer (homopolymers at
-    half weight), the ranks keep every k-mer exactly once, and their concatenation is gk_sort's."""
+    11/16 weight), the ranks keep every k-mer exactly once, and their concatenation is gk_sort's."""
     from genome_kmers import _native
 
     sba, seg = _random_sba(200_000 + 17, 3 + world, contigs)
@@ -417,7 +417,7 @@ def test_gpu_key_ranges_class_b_given(world, contigs, k, canonical):
         if len(runs):
             assert np.all(runs[:, 0] >= bounds[r]) and np.all(runs[:, 0] < bounds[r + 1])
         added = int(h.astype(np.int64).sum()) - int(h0.sum())
-        assert added == len(rest) + sum((int(c) + 1) // 2 for c in runs[:, 1])
+        assert added == len(rest) + sum((int(c) * 11 + 15) // 16 for c in runs[:, 1])
         hist = h.astype(np.int64) if hist is None else hist + h.astype(np.int64)
         rests.append(rest)
         runs_l.append(runs)

@@ -463,6 +463,43 @@ def test_unique_counts_many_tiles(shape):
     np.testing.assert_array_equal(counts, want_cnt)
 
 
+@pytest.mark.parametrize("k,canonical", [(31, False), (31, True), (63, False)])
+def test_big_groups_of_identical_kmers(k, canonical):
+    """Groups of identical k-mers larger than a local bucket (poly-A, (CA)n and a 300-bp unit in
+    thousands of exact copies) inside a genome large enough that the MSD driver sends them from the
+    next-level list straight to the done list (drop_uniform) instead of partitioning them level by
+    level: starts, keys and unique counts vs the oracle."""
+    rng = np.random.default_rng(77 + k)
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 3_200_000)].copy()
+    s[100_000:110_000] = ord("A")
+    s[500_000:514_000] = np.frombuffer(b"CA" * 7000, dtype=np.uint8)
+    unit = s[900_000:900_300].copy()
+    for p in range(1_000_000, 1_000_000 + 6000 * 300, 300):
+        s[p:p + 300] = unit
+    seg = np.array([0], dtype=np.uint32)
+    e = _native.Engine()
+    e.set_sequence(s, seg)
+    e.enumerate(k)
+    e.sort(k, canonical=canonical)
+    unsorted = oracle.enumerate_starts(s, seg, k)
+    if canonical:
+        want = oracle.canonical_sort(s, unsorted, k)
+        keys = oracle.canonical_keys(s, want, k, 2)
+    else:
+        want = oracle.quicksort(s, unsorted, k, k, break_ties=True)
+        keys = oracle.encode_keys(s, want, *oracle.key_spec(True, k, k))
+    np.testing.assert_array_equal(e.copy_starts(), want)
+    got = e.copy_keys()
+    np.testing.assert_array_equal(got, keys.reshape(got.shape))
+    flat = got.reshape(len(got), -1)
+    head = np.ones(len(flat), dtype=bool)
+    head[1:] = (flat[1:] != flat[:-1]).any(axis=1)
+    first, counts = e.unique_counts()
+    np.testing.assert_array_equal(first, np.flatnonzero(head))
+    np.testing.assert_array_equal(counts, np.diff(np.append(np.flatnonzero(head), len(flat))))
+    assert counts.max() >= 5000  # the groups the test is about
+
+
 def test_single_kmer_and_tiny_inputs():
     sc = SequenceCollection(sequence_list=[("a", "ACGTA")])
     km = gk.Kmers(sc, min_kmer_len=5, max_kmer_len=5)

@@ -139,10 +139,14 @@ def main():
         pb = D.position_ranges(len(sba), world)
         per_rank, extra, stages, uniq, kept = [], [], None, 0, 0
 
+        all_stages = []
+
         def record(ms, rep_stages):
             nonlocal stages
+            st = {name: round(v["total_ms"], 3) for name, v in rep_stages.items()}
             if not per_rank or ms > max(per_rank):
-                stages = {name: round(v["total_ms"], 3) for name, v in rep_stages.items()}
+                stages = st
+            all_stages.append(st)
             per_rank.append(round(ms, 2))
 
         if args.scheme == "range":
@@ -235,6 +239,10 @@ def main():
                 "kmers_per_s": round(total / (worst * 1e-3), 1),
                 "speedup_vs_single": round(single_ms / worst, 2), "unique": uniq,
                 "slowest_rank_stages_ms": stages}
+        # the stages where ranks differ most (max - min over ranks > 0.2 ms)
+        names = sorted({n for st in all_stages for n in st})
+        spread = {n: [st.get(n, 0.0) for st in all_stages] for n in names}
+        line["stage_spread_ms"] = {n: v for n, v in spread.items() if max(v) - min(v) > 0.2}
         if extra:
             line["ranks"] = extra
         print(json.dumps(line), flush=True)

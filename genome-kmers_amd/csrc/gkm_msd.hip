@@ -42,7 +42,7 @@ constexpr int kSmall = 24;
 // waves per SIMD the wave-local kernels' registers are capped for (msd_wave_kernel<I, W, .>); the
 // LDS (7.2 KB per wave at I = 8) admits 5 per SIMD
 #ifndef GKM_WAVE_OCC8
-#define GKM_WAVE_OCC8 5
+#define GKM_WAVE_OCC8 4
 #endif
 constexpr int kWaveOcc4 = 6, kWaveOcc8 = GKM_WAVE_OCC8, kWaveOcc16 = 3;
 // digit bits of the wave-local kernels' in-LDS partition: buckets of ~370 keys (C3) over 512

@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # 4-byte payload -- read 1 (sequence) + 8 (histogram) + 8 x 12 = 105 B per 31-mer, total 201 B
 BASELINE_READ_B, BASELINE_TOTAL_B = 105, 201
 # the wave-local finishing kernel's instantiation (gkm_msd.hip: msd_wave_kernel<I, waves/SIMD, keys>)
-WAVE8_KERNEL = "msd_wave_kernel<8,5,true,9>"
+WAVE8_KERNEL = "msd_wave_kernel<8,4,true,9>"
 
 
 def parse():

@@ -566,12 +566,16 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                                                           uint8_t *__restrict__ nd_out) {
     constexpr bool STORE = MODE != 0;
     using P = L0Pack<BITS, kSTile>;
-    constexpr int kStage = STORE ? kSTile : 1;  // per-wave staging of the kept (key, start): 512 each
+    // per-wave staging of the kept positions (tile-relative u16; the key is re-derived from the
+    // tile's codes when it is stored): 512 slots + one dump slot per lane for the positions not
+    // kept, so the staging writes need no branch.  (Staged as (key, start), 48 KB, the kernel fit
+    // 3 workgroups per CU and its divergent staging loop cost more scalar than vector work.)
+    constexpr int kSlots = 512 + 64;
+    constexpr int kStage = STORE ? kSW * kSlots : 1;
     __shared__ uint64_t s_code[P::kCodeWords];
     __shared__ uint32_t s_dol[P::kGroups];
     __shared__ uint8_t s_lut4[256];
-    __shared__ uint64_t s_skey[kStage];
-    __shared__ uint32_t s_sval[kStage];
+    __shared__ uint16_t s_spos[kStage];
     __shared__ uint32_t s_wtot[kSW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
@@ -644,36 +648,32 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
                 }
             }
             const uint32_t cnt = (uint32_t)__popc(keepm);
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off);
-                if (lane >= off) incl += y;
-            }
-            const uint32_t total = __shfl(incl, 63);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             if (!STORE) {
                 if (lane == 63) wave_cnt[wslot] = incl;
                 continue;
             }
             const uint64_t o = MODE == 2 ? chunk_offset(total) : (uint64_t)wave_off[wslot];
-            // stage the wave's kept k-mers in position order (keys only for them), then store them
-            // as one coalesced run
-            uint64_t *sk = s_skey + wave * 512;
-            uint32_t *sv = s_sval + wave * 512;
+            // stage the wave's kept positions in position order, then store the k-mers as one
+            // coalesced run
+            uint16_t *sp = s_spos + wave * kSlots;
             uint32_t j = incl - cnt;
-            for (uint32_t m = keepm; m; m &= m - 1) {
-                const int i = __ffs(m) - 1;
-                sk[j] = CANON ? l0_key_of<2, true>(s_code, q0 + i, a.total_bits, a.symbols) : win8_key(win8, i, a.total_bits);
-                sv[j] = (uint32_t)(P0 + q0 + i);
-                ++j;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t kp = (keepm >> i) & 1u;
+                sp[kp ? j : 512u + (uint32_t)lane] = (uint16_t)(q0 + i);
+                j += kp;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
             for (uint32_t e = lane; e < total; e += 64) {
-                const uint64_t k = sk[e];
+                const uint32_t p = sp[e];
+                const uint64_t k = CANON ? l0_key_of<2, true>(s_code, p, a.total_bits, a.symbols)
+                                         : l0_key<2>(s_code, p, a.total_bits);
                 kout[o + e] = k;
-                vout[o + e] = sv[e];
+                vout[o + e] = (uint32_t)(P0 + p);
                 nd_out[o + e] = (uint8_t)dg_of(k, d0);
             }
             continue;

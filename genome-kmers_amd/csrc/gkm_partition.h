@@ -286,10 +286,17 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
                                                            const uint8_t *__restrict__ nd,
                                                            uint32_t *__restrict__ tile_hist) {
     constexpr int RADIX = 1 << R;
-    __shared__ uint32_t s_hist[RADIX];
+#ifndef GKM_COUNT_COPIES
+#define GKM_COUNT_COPIES 4
+#endif
+    // NC interleaved histogram copies (digit d, copy c at NC d + c; copy = thread % NC): lanes of
+    // one atomic that share a digit land on NC different words in NC banks
+    constexpr int NC = GKM_COUNT_COPIES;
+    __shared__ uint32_t s_hist[RADIX * NC];
     const int t = threadIdx.x;
-    for (int i = t; i < RADIX; i += 256) s_hist[i] = 0;
+    for (int i = t; i < RADIX * NC; i += 256) s_hist[i] = 0;
     lds_barrier();
+    uint32_t *hc = s_hist + (t & (NC - 1));
     const uint64_t b = t_start[blockIdx.x];
     const uint32_t m = t_count[blockIdx.x];
     // 16 digits per load where the run is 16-byte aligned (a tile's ~11 K digits: <= 3 loads per
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
     const uint32_t head = min<uint32_t>((uint32_t)((16 - ((uintptr_t)(nd + b) & 15)) & 15), m);
     const uint32_t quads = (m - head) >> 4;
     const uint4 *w = reinterpret_cast<const uint4 *>(nd + b + head);
-    if (t < (int)head) atomicAdd(&s_hist[nd[b + t]], 1u);
+    if (t < (int)head) atomicAdd(&hc[NC * nd[b + t]], 1u);
     for (uint32_t i0 = 0; i0 < quads; i0 += 3 * 256) {
         uint4 x4[3];
 #pragma unroll
@@ -311,17 +318,22 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
             const uint32_t xs[4] = {x4[r].x, x4[r].y, x4[r].z, x4[r].w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                atomicAdd(&s_hist[xs[u] & 0xFF], 1u);
-                atomicAdd(&s_hist[(xs[u] >> 8) & 0xFF], 1u);
-                atomicAdd(&s_hist[(xs[u] >> 16) & 0xFF], 1u);
-                atomicAdd(&s_hist[xs[u] >> 24], 1u);
+                atomicAdd(&hc[NC * (xs[u] & 0xFF)], 1u);
+                atomicAdd(&hc[NC * ((xs[u] >> 8) & 0xFF)], 1u);
+                atomicAdd(&hc[NC * ((xs[u] >> 16) & 0xFF)], 1u);
+                atomicAdd(&hc[NC * (xs[u] >> 24)], 1u);
             }
         }
     }
     const uint32_t tail0 = head + 16 * quads;  // < 16 bytes left
-    if (tail0 + t < m) atomicAdd(&s_hist[nd[b + tail0 + t]], 1u);
+    if (tail0 + t < m) atomicAdd(&hc[NC * nd[b + tail0 + t]], 1u);
     lds_barrier();
-    for (int i = t; i < RADIX; i += 256) tile_hist[(uint64_t)blockIdx.x * RADIX + i] = s_hist[i];
+    for (int i = t; i < RADIX; i += 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v += s_hist[NC * i + c];
+        tile_hist[(uint64_t)blockIdx.x * RADIX + i] = v;
+    }
 }
 
 // persistent: grid = a multiple of 8 blocks, each walks its XCD's tiles; the next tile's keys

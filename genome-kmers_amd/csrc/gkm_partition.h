@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
                                                            uint32_t *__restrict__ tile_hist) {
     constexpr int RADIX = 1 << R;
 #ifndef GKM_COUNT_COPIES
-#define GKM_COUNT_COPIES 4
+#define GKM_COUNT_COPIES 1
 #endif
     // NC interleaved histogram copies (digit d, copy c at NC d + c; copy = thread % NC): lanes of
     // one atomic that share a digit land on NC different words in NC banks

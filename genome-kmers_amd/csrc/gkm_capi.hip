@@ -505,7 +505,8 @@ int gkm::ensure_keys(gk_ctx *c) {
     hipError_t te = hipErrorNotSupported;
     if (c->enum_sorted && !no_table && ks.words >= 2 && ks.symbols == ks.min_len && ks.symbols <= 64 &&
         (ks.bits == 2 || ks.bits == 4) && c->n >= 4096 && c->key_words_b[c->cur ^ 1] >= ks.words)
-        te = launch_encode_table_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur], c->keys[c->cur ^ 1]);
+        te = launch_encode_table_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur], c->keys[c->cur ^ 1],
+                                        8 * (uint64_t)c->key_words_b[c->cur ^ 1] * (c->elem_cap + 64));
     if (te == hipErrorNotSupported)
         GK_TRY_HIP(c, launch_encode_gather(c, c->spec, c->vals[c->cur], c->n, c->keys[c->cur]));
     else

@@ -429,6 +429,24 @@ __device__ __forceinline__ void canon2(int k, uint64_t &hi, uint64_t &lo) {
     }
 }
 
+// the W key words (BITS-bit symbols) of a k-symbol ACGT k-mer given as a right-aligned 2k-bit value
+template <int W, int BITS>
+__device__ __forceinline__ void key_from_2bit(uint64_t hi, uint64_t lo, int k, uint64_t (&w)[W]) {
+    if (BITS == 2) {
+        w[W - 1] = lo;
+        if (W > 1) w[0] = hi;
+    } else {
+        const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
+#pragma unroll
+        for (int q = 0; q < W; ++q) {  // q: word from the least significant end
+            uint64_t e = expand4_16((uint32_t)part[q]);
+            const int left = k - 16 * q;  // symbols in this word
+            if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
+            w[W - 1 - q] = e;
+        }
+    }
+}
+
 // the W key words of the fixed-length k-mer at st: SWAR for windows of A/C/G/T, per symbol otherwise
 template <int W, int BITS>
 __device__ __forceinline__ void fast_window_key(const uint8_t *__restrict__ sba, const KS &ks, uint32_t st,
@@ -437,19 +455,7 @@ __device__ __forceinline__ void fast_window_key(const uint8_t *__restrict__ sba,
     uint64_t hi, lo;
     if (window2_acgt(sba, st, k, hi, lo)) {
         if (ks.canonical) canon2(k, hi, lo);
-        if (BITS == 2) {
-            w[W - 1] = lo;
-            if (W > 1) w[0] = hi;
-        } else {
-            const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
-#pragma unroll
-            for (int q = 0; q < W; ++q) {  // q: word from the least significant end
-                uint64_t e = expand4_16((uint32_t)part[q]);
-                const int left = k - 16 * q;  // symbols in this word
-                if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
-                w[W - 1 - q] = e;
-            }
-        }
+        key_from_2bit<W, BITS>(hi, lo, k, w);
     } else {
         const uint8_t *b = sba + st;
         if (ks.canonical) {
@@ -571,6 +577,247 @@ static hipError_t table_gather_w(gk_ctx *c, const KS &k, const uint32_t *starts,
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((table_gather_kernel<W>), dim3(grid), dim3(256), 0, c->stream, starts, c->seg, kb,
                        (uint32_t)c->nseg, n, table, keys);
+    return hipGetLastError();
+}
+
+// Keys through a position-indexed table of 2-bit rows (k <= 63; C5's canonical 63-mers under a
+// 4-bit key spec).  The enumeration-order table above computes every key from its own window (a
+// contig search, 9 unaligned words, a SWAR pack and a 4-bit expansion per k-mer: 64 ms at C5) and
+// stores W words per row (99 GB at C5).  Here a lane computes the keys of kRowPos consecutive
+// positions: the first window by SWAR from aligned words, the next ones by rolling the forward and
+// reverse-complement values one symbol at a time, and it stores 16 B per position (hi, lo of the
+// 2-bit key; 49 GB at C5).  A window holding a byte other than A/C/G/T (IUPAC, N, the '$'
+// separators and pad) gets a marker row -- bit 63 of hi, which a 2-bit key of <= 63 symbols never
+// sets -- and the gather computes those keys from the window itself.  The gather reads the row of
+// each sorted start at its sba position (no contig search) and expands it to the key spec.
+constexpr int kRowPos = 16;  // positions per lane
+constexpr uint64_t kRowMarker = 1ull << 63;
+
+// Rows leave through LDS: a lane's kRowPos rows are consecutive positions, so stored straight from
+// the lane every store instruction would write 64 separate 16-B pieces (3.1e9 partial-line write
+// requests at C5: 22 ms); staged per wave in halves of 8 rows, each store writes whole lines.
+__global__ __launch_bounds__(256) void key_rows2_kernel(const uint8_t *__restrict__ sba, uint64_t sba_len, int k,
+                                                        int canonical, uint64_t *__restrict__ rows) {
+    constexpr int kHalf = kRowPos / 2;
+    __shared__ uint4 s_rows[4][64 * kHalf + 64];  // per wave; row q at q + q / 8 (conflict-free writes)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint4 *sr = s_rows[wave];
+    const uint64_t ng = (sba_len + kRowPos - 1) / kRowPos;
+    const int s = 128 - 2 * k;  // right-alignment shift of the first 64 symbols (2 <= s < 128)
+    const uint64_t mhi = k > 32 ? (~0ull >> (128 - 2 * k)) : 0ull;
+    const uint64_t mlo = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1);
+    const int top = 2 * k - 2;  // bit of the newest symbol's complement in the reverse strand
+    // wave-uniform trips: every lane reaches the staging below
+    for (uint64_t gw = blockIdx.x * 256ull + wave * 64; gw < ng; gw += (uint64_t)gridDim.x * 256) {
+        const uint64_t g = gw + lane;
+        const uint64_t p0 = (g < ng ? g : 0) * kRowPos;  // (a lane past the end computes rows it does not store)
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(sba + p0);  // 16-B aligned
+        // the first window (bytes 0..k-1 after p0): 8 words = 64 symbols left-aligned in fh:fl
+        uint64_t fh = 0, fl = 0;
+        int lb = -1;  // the last non-ACGT byte so far (relative to p0)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t x = src[j];
+            const uint64_t v = pack2_8e(x);  // byte 0 in the most significant pair
+            if (j < 4) fh |= v << (48 - 16 * j);
+            else fl |= v << (48 - 16 * (j - 4));
+            const int nb = min(8, max(0, k - 8 * j));
+            const uint64_t m = non_acgt_bytes(x) & (nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1));
+            if (m) lb = 8 * j + ((63 - __builtin_clzll(m)) >> 3);
+        }
+        if (s >= 64) {
+            fl = fh >> (s - 64);
+            fh = 0;
+        } else {
+            fl = (fl >> s) | (fh << (64 - s));
+            fh >>= s;
+        }
+        // its reverse complement, right-aligned (canon2's construction)
+        uint64_t rh = rev_pairs(~fl), rl = rev_pairs(~fh);
+        if (s >= 64) {
+            rl = rh >> (s - 64);
+            rh = 0;
+        } else {
+            rl = (rl >> s) | (rh << (64 - s));
+            rh >>= s;
+        }
+        // bytes k .. k + 14 after p0: the symbols rolled in for positions 1 .. 15
+        const uint64_t a = p0 + (uint64_t)k;
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(sba + (a & ~7ull));
+        const int sh = (int)(a & 7) * 8;
+        const uint64_t u0 = q[0], u1 = q[1], u2 = q[2];
+        const uint64_t n0 = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
+        const uint64_t n1 = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
+        const uint64_t c0 = ((n0 >> 1) ^ (n0 >> 2)) & 0x0303030303030303ull;
+        const uint64_t c1 = ((n1 >> 1) ^ (n1 >> 2)) & 0x0303030303030303ull;
+        const uint64_t b0 = non_acgt_bytes(n0), b1 = non_acgt_bytes(n1);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+            for (int rr = 0; rr < kHalf; ++rr) {
+                const int r = half * kHalf + rr;
+                if (r > 0) {  // roll in byte k - 1 + r
+                    const int i = r - 1;
+                    const uint64_t c = ((i < 8 ? c0 : c1) >> (8 * (i & 7))) & 3;
+                    if (((i < 8 ? b0 : b1) >> (8 * (i & 7) + 7)) & 1) lb = k - 1 + r;
+                    fh = ((fh << 2) | (fl >> 62)) & mhi;
+                    fl = ((fl << 2) | c) & mlo;
+                    rl = (rl >> 2) | (rh << 62);
+                    rh >>= 2;
+                    if (top >= 64) rh |= (3 - c) << (top - 64);
+                    else rl |= (3 - c) << top;
+                }
+                uint64_t h = fh, l = fl;
+                if (canonical && (rh < fh || (rh == fh && rl < fl))) {
+                    h = rh;
+                    l = rl;
+                }
+                if (lb >= r) {
+                    h = kRowMarker;
+                    l = 0;
+                }
+                const int qi = lane * kHalf + rr;
+                sr[qi + (qi >> 3)] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)l, (uint32_t)(l >> 32));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            // staged row qi = lane' * 8 + rr' is position gw * 16 + 16 lane' + 8 half + rr': runs of 8
+            // rows (128 B, line-aligned) per lane'
+#pragma unroll
+            for (int j = 0; j < kHalf; ++j) {
+                const int qi = j * 64 + lane;
+                const uint64_t pos = (gw + (uint64_t)(qi >> 3)) * kRowPos + half * kHalf + (qi & 7);
+                const uint4 v = sr[qi + (qi >> 3)];
+                if (pos < sba_len) *reinterpret_cast<uint4 *>(rows + 2 * pos) = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();  // the staging is read before the next half overwrites it
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        }
+    }
+}
+
+// The gather proper is a small kernel (many waves, U rows in flight per lane: random-row gathers
+// are bound by the loads in flight); the keys of marker rows -- about 5 % of C5's k-mers, the N
+// runs, sorted together -- are left to row2_fix_kernel through a list appended per wave (one atomic
+// per wave).  With the per-byte path inlined in the gather, its registers cut the waves in flight
+// and the gather took 125 ms at C5 against 93 ms for the W-word rows.
+template <int W, int BITS>
+__global__ __launch_bounds__(256) void row2_gather_kernel(KS ks, const uint32_t *__restrict__ starts, uint64_t n,
+                                                          const uint64_t *__restrict__ rows,
+                                                          uint64_t *__restrict__ keys, uint32_t *__restrict__ fix_cnt,
+                                                          uint32_t *__restrict__ fix_idx) {
+    constexpr int U = 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i0 < n + (U - 1) * stride; i0 += U * stride) {
+        uint32_t p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + u * stride;
+            p[u] = i < n ? starts[i] : 0u;
+        }
+        uint4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = *reinterpret_cast<const uint4 *>(rows + 2 * (uint64_t)p[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + u * stride;
+            const uint64_t hi = ((uint64_t)r[u].y << 32) | r[u].x, lo = ((uint64_t)r[u].w << 32) | r[u].z;
+            const bool mk = i < n && (hi & kRowMarker);
+            const uint64_t m = __ballot(mk);
+            if (m) {  // wave-uniform
+                const int leader = __builtin_ctzll(m);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(fix_cnt, (uint32_t)__popcll(m));
+                base = __shfl(base, leader);
+                if (mk)
+                    fix_idx[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)i;
+            }
+            if (i < n && !mk) {
+                uint64_t w[W];
+                key_from_2bit<W, BITS>(hi, lo, ks.symbols, w);
+#pragma unroll
+                for (int q = 0; q < W; ++q) keys[(uint64_t)q * n + i] = w[q];
+            }
+        }
+    }
+}
+
+// true iff the k (<= 64) bytes from sba[s] all equal ch (8-byte loads from s & ~7, as window2_acgt)
+__device__ __forceinline__ bool window_homo(const uint8_t *sba, uint64_t s, int k, uint32_t ch) {
+    const uint64_t pat = 0x0101010101010101ull * ch;
+    const uint64_t a = s & ~7ull;
+    const int sh = (int)(s - a) * 8;
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(sba + a);
+    uint64_t prev = p[0], diff = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (8 * j >= k) break;
+        const uint64_t nxt = p[j + 1];
+        const uint64_t w = sh ? (prev >> sh) | (nxt << (64 - sh)) : prev;
+        prev = nxt;
+        const int nb = min(8, k - 8 * j);
+        diff |= (w ^ pat) & (nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1));
+    }
+    return diff == 0;
+}
+
+// keys of the sorted entries whose rows are markers (a window with a non-ACGT byte), from the window.
+// Homopolymers (one letter k times: GRCh38's N runs, ~150 M of C5's markers, sorted together) take
+// a short path: the letter's code -- canonical: the smaller of it and its complement's -- k times.
+template <int W, int BITS>
+__global__ __launch_bounds__(256) void row2_fix_kernel(const uint8_t *__restrict__ sba, KS ks,
+                                                       const uint32_t *__restrict__ starts, uint64_t n,
+                                                       const uint32_t *__restrict__ fix_cnt,
+                                                       const uint32_t *__restrict__ fix_idx,
+                                                       uint64_t *__restrict__ keys) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    __syncthreads();
+    const uint32_t cnt = *fix_cnt;
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < cnt; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = fix_idx[j];
+        const uint32_t p = starts[i];
+        uint64_t w[W];
+        const uint32_t ch = sba[p];
+        if (BITS == 4 && window_homo(sba, p, ks.symbols, ch)) {
+            uint32_t code = s_lut4[ch];
+            if (ks.canonical) code = min(code, comp_sym<4>(code));
+            const uint64_t rep = (uint64_t)code * 0x1111111111111111ull;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {  // q: word from the least significant end (key_from_2bit)
+                const int left = ks.symbols - 16 * q;
+                w[W - 1 - q] = left >= 16 ? rep : left <= 0 ? 0ull : rep & (~0ull >> (64 - 4 * left));
+            }
+        } else {
+            fast_window_key<W, BITS>(sba, ks, p, s_lut4, w);
+        }
+#pragma unroll
+        for (int q = 0; q < W; ++q) keys[(uint64_t)q * n + i] = w[q];
+    }
+}
+
+template <int W, int BITS>
+static hipError_t row2_gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys,
+                                uint64_t *rows, uint32_t *fix_cnt, uint32_t *fix_idx) {
+    const uint64_t ng = (c->sba_len + kRowPos - 1) / kRowPos;
+    const int g1 = (int)std::max<uint64_t>(1, std::min<uint64_t>((ng + 255) / 256, 8192));
+    hipLaunchKernelGGL(key_rows2_kernel, dim3(g1), dim3(256), 0, c->stream, c->sba, (uint64_t)c->sba_len, k.symbols,
+                       k.canonical, rows);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(fix_cnt, 0, 4, c->stream);
+    if (e != hipSuccess) return e;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+    hipLaunchKernelGGL((row2_gather_kernel<W, BITS>), dim3(grid), dim3(256), 0, c->stream, k, starts, n, rows, keys,
+                       fix_cnt, fix_idx);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((row2_fix_kernel<W, BITS>), dim3(2048), dim3(256), 0, c->stream, c->sba, k, starts, n, fix_cnt,
+                       fix_idx, keys);
     return hipGetLastError();
 }
 
@@ -697,9 +944,25 @@ static hipError_t gather_dispatch(gk_ctx *c, const KS &k, const uint32_t *starts
 }
 
 hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n,
-                                      uint64_t *keys, uint64_t *table) {
+                                      uint64_t *keys, uint64_t *table, uint64_t table_bytes) {
     hipError_t e = init_tables();
     if (e != hipSuccess) return e;
+    KS k = pod(ks);
+    // the position-indexed 2-bit rows when they fit the table buffer (k <= 63)
+    static const bool enum_rows = std::getenv("GKM_KEY_TABLE_ENUM") != nullptr;  // (A/B: the W-word rows)
+    // (the rows, then the fix-up list of marker entries -- at most n -- in the same buffer)
+    const uint64_t rows_bytes = 16 * (((uint64_t)c->sba_len + kRowPos - 1) / kRowPos * kRowPos);
+    if (!enum_rows && ks.symbols <= 63 && rows_bytes + 4 * (n + 64) <= table_bytes) {
+        uint32_t *fix_idx = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(table) + rows_bytes);
+        uint32_t *fix_cnt = nullptr;
+        if (scratch(c, "rows_fix_cnt", 64, &fix_cnt) != hipSuccess) return hipErrorOutOfMemory;
+        if (ks.bits == 2 && ks.words == 2) e = row2_gather_w<2, 2>(c, k, starts, n, keys, table, fix_cnt, fix_idx);
+        else if (ks.bits == 4 && ks.words == 2) e = row2_gather_w<2, 4>(c, k, starts, n, keys, table, fix_cnt, fix_idx);
+        else if (ks.bits == 4 && ks.words == 3) e = row2_gather_w<3, 4>(c, k, starts, n, keys, table, fix_cnt, fix_idx);
+        else if (ks.bits == 4 && ks.words == 4) e = row2_gather_w<4, 4>(c, k, starts, n, keys, table, fix_cnt, fix_idx);
+        else return hipErrorNotSupported;
+        return e;
+    }
     // kb: exclusive prefix of the contigs' k-mer counts (kmers.py:837-861 counts)
     std::vector<uint32_t> kb(c->nseg);
     uint64_t acc = 0;
@@ -714,7 +977,6 @@ hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32
     if (scratch(c, "enc_kb", std::max<uint64_t>(c->nseg, 1), &d_kb) != hipSuccess) return hipErrorOutOfMemory;
     e = hipMemcpyAsync(d_kb, kb.data(), 4 * c->nseg, hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return e;
-    KS k = pod(ks);
     if (ks.bits == 2) {
         switch (ks.words) {
         case 2: e = table_gather_w<2, 2>(c, k, starts, n, keys, table, d_kb); break;

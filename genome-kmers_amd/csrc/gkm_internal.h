@@ -224,10 +224,10 @@ hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n,
 hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist);
 hipError_t launch_encode_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint64_t *keys);
 // keys of sorted starts that are a permutation of the whole enumeration (c->enum_sorted): every
-// k-mer's key in enumeration order into `table` (AoS, W words each), then one aligned row gather
-// per sorted start (gkm_encode.hip)
+// k-mer's key into `table` (table_bytes long), then one aligned row gather per sorted start: 2-bit
+// rows per sba position (k <= 63), else W-word rows in enumeration order (gkm_encode.hip)
 hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n,
-                                      uint64_t *keys, uint64_t *table);
+                                      uint64_t *keys, uint64_t *table, uint64_t table_bytes);
 // strand of each canonical k-mer: 1 if its reverse complement is the smaller (the key), else 0
 hipError_t launch_canon_strands(gk_ctx *c, const KeySpec &ks, const uint32_t *starts, uint64_t n, uint8_t *out);
 

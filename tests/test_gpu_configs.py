@@ -222,3 +222,32 @@ def test_small_chunks_key_ranges_concatenate(small_chunks):
         e.shard_sort_range(31, cuts[r], cuts[r + 1])
         parts.append(e.copy_starts())
     np.testing.assert_array_equal(np.concatenate(parts), want)
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-word keys of a sorted enumeration through the position-indexed 2-bit row table
+# (gkm_encode.hip key_rows2_kernel / row2_gather_kernel): every row dispatch (2-bit W 2; 4-bit
+# W 2, 3, 4), canonical and forward, windows with N runs / IUPAC letters (marker rows), several
+# contigs (rows across the '$' separators) and a contig shorter than 16 positions
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("k,alphabet,canonical", [
+    (33, b"ACGT", False), (63, b"ACGT", True), (40, b"ACGTACGTACGTRYKMSWBDHV", False),
+    (48, b"ACGTACGTACGTACGTN", True), (63, b"ACGTACGTACGTACGTACGTN", True), (63, b"ACGTACGTACGTNRY", False),
+    (24, b"ACGTACGTACGTACGTACGTRY", True)])
+def test_key_rows_vs_oracle(k, alphabet, canonical):
+    seqs = _genome(50 + k, [60_000, 25_000], alphabet=alphabet, rep_len=2000, copies=4, n_runs=3)
+    seqs.append(("tiny", "ACGTTGCA" * 9 + "AC"))  # 74 bases: k-mers near a contig end
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=k, max_kmer_len=k)
+    unsorted = km.kmer_sba_start_indices.copy()
+    km.sort(canonical=canonical) if canonical else km.sort()
+    words, bits, _ = km._engine.key_layout()
+    if canonical:
+        want = oracle.canonical_sort(sc.forward_sba, unsorted, k)
+        want_keys = oracle.canonical_keys(sc.forward_sba, want, k, bits)
+    else:
+        want = oracle.quicksort(sc.forward_sba, unsorted, k, k, break_ties=True)
+        spec = oracle.key_spec(km._engine.is_acgt(), k, k)
+        want_keys = oracle.encode_keys(sc.forward_sba, want, *spec)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), want_keys)

@@ -16,7 +16,7 @@ for rep in 1 2; do
       env:*) envs=("${lib#env:}") ;;
       *) export GKM_LIB=$lib ;;
     esac
-    timeout -k 10 300 env "${envs[@]}" python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/abm.json 2> gpurun_out/abm.err || { tail -20 gpurun_out/abm.err; exit 1; }
+    timeout -k 10 300 env "${envs[@]}" python bench.py --config ${CONFIG:-c3} --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline > gpurun_out/abm.json 2> gpurun_out/abm.err || { tail -20 gpurun_out/abm.err; exit 1; }
     python3 -c "import json; d=json.loads(open('gpurun_out/abm.json').read().strip().splitlines()[-1]); s=d['config']['stages_ms_per_step']; print('$lib', d['ms_per_step'], {k: s[k] for k in sorted(s) if s[k] > 1})" | tee -a gpurun_out/abm.txt
   done
 done

@@ -708,7 +708,10 @@ __global__ __launch_bounds__(256) void row2_gather_kernel(KS ks, const uint32_t 
                                                           const uint64_t *__restrict__ rows,
                                                           uint64_t *__restrict__ keys, uint32_t *__restrict__ fix_cnt,
                                                           uint32_t *__restrict__ fix_idx) {
-    constexpr int U = 4;
+#ifndef GKM_ROW_U
+#define GKM_ROW_U 4
+#endif
+    constexpr int U = GKM_ROW_U;  // rows in flight per lane (A/B knob)
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
     for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i0 < n + (U - 1) * stride; i0 += U * stride) {

@@ -328,11 +328,15 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                 if (fast) {
                     for (uint32_t g = t; g < TILE / 8; g += T) {
                         const uint32_t q0 = g * 8;
-                        const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - 4);
+                        // only the top 32 bits of each window are read (16 symbols: positions q0 .. q0 + 10,
+                        // q0 + k - 4 .. q0 + k + 6): 32-bit shifts per position instead of 64-bit ones
+                        // (the 64-bit form ran this pass VALU-bound at 5.0 ms for C5)
+                        const uint32_t tf = (uint32_t)(win32_at(s_code, q0) >> 32);
+                        const uint32_t tr = (uint32_t)(win32_at(s_code, q0 + a.symbols - 4) >> 32);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
-                            const uint32_t f7 = (uint32_t)(tf >> (57 - 2 * i)) & 0x7Fu;
-                            const uint32_t v = (uint32_t)(tr >> (56 - 2 * i)) & 0xFFu;  // symbols q0+k-4+i ..
+                            const uint32_t f7 = (tf >> (25 - 2 * i)) & 0x7Fu;
+                            const uint32_t v = (tr >> (24 - 2 * i)) & 0xFFu;  // symbols q0+k-4+i ..
                             const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
                             const uint32_t d = min(f7, (~rv & 0xFFu) >> 1);
                             if (l0_owned(d, a)) atomicAdd(&s_hist[d * NC], 1u);

@@ -700,9 +700,9 @@ __global__ __launch_bounds__(256) void key_rows2_kernel(const uint8_t *__restric
 
 // The gather proper is a small kernel (many waves, U rows in flight per lane). Each random 16-B row
 // costs a whole 128-B line of HBM reads (391 GB per C5 launch, profiles/r3/prof_c5_end2: 5.6 TB/s
-// with the key writes), and non-temporal row loads measured the same; the keys of marker rows -- about 5 % of C5's k-mers, the N
-// runs, sorted together -- are left to row2_fix_kernel through a list appended per wave (one atomic
-// per wave).  With the per-byte path inlined in the gather, its registers cut the waves in flight
+// with the key writes); non-temporal row loads measured the same.  The keys of marker rows --
+// about 5 % of C5's k-mers, the N runs, sorted together -- are left to row2_fix_kernel through a
+// list appended per wave (one atomic per wave).  With the per-byte path inlined in the gather, its registers cut the waves in flight
 // and the gather took 125 ms at C5 against 93 ms for the W-word rows.
 template <int W, int BITS>
 __global__ __launch_bounds__(256) void row2_gather_kernel(KS ks, const uint32_t *__restrict__ starts, uint64_t n,

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 
 #include "gkm_internal.h"
 #include "gkm_partition.h"
@@ -244,69 +245,121 @@ extern "C" int gk_device_count(int *count) {
 // gkm_partition.h): it relies on the LDS applying the same-address lanes of one wave instruction in
 // increasing lane order.  That is how gfx950 behaves (tools/lds_rank_probe.hip: no exception in
 // 4e10 lane-ranks), not an ISA guarantee, so it is checked once per device and process against a
-// ballot-match ground truth -- 256, 64, 16, 4 and 1 random digits, 4 items per trial,
-// every CU busy -- and a device where it does not hold is refused (a wrong order would otherwise
-// be silent).
+// ballot-match ground truth over every digit space the partitions rank in -- 1024, 512, 256, 128,
+// 64, 16, 4 and 1 digits (the wave kernels' 10 / 9 / 8 bits, the level passes' 8, L0's 7) with
+// per-wave counter arrays of 1024 words like the wave kernels', 8 items per trial, lanes sitting
+// out, every CU busy.  Where it does not hold, the partitions switch to ballot-match ranking
+// (rank_ballot): the same ranks from ballots alone.  The kernel checks that path as well.
 __global__ __launch_bounds__(256) void lds_rank_check_kernel(uint32_t trials, unsigned long long *bad) {
-    __shared__ uint32_t s_cnt[4][256];
+    __shared__ uint32_t s_cnt[4][1024];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t *cnt = s_cnt[wave];
     unsigned long long nb = 0;
     for (uint32_t t = 0; t < trials; ++t) {
-        const uint32_t dmask = 0xFFu >> (2 * (t % 5));  // 256, 64, 16, 4 and 1 digits
+        constexpr uint32_t kMasks[8] = {1023u, 511u, 255u, 127u, 63u, 15u, 3u, 0u};
+        const uint32_t dmask = kMasks[t & 7];
+        const bool ballot = (t >> 3) & 1;  // every other round of 8: the fallback ranking
 #pragma unroll
-        for (int u = 0; u < 4; ++u) cnt[u * 64 + lane] = 0;
-        uint32_t dd[4], got[4];
+        for (int u = 0; u < 16; ++u) cnt[u * 64 + lane] = 0;
+        uint32_t dd[8], got[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             uint32_t x = (blockIdx.x * 0x9E3779B9u) ^ (t * 0x85EBCA6Bu) ^ ((uint32_t)(i * 64 + lane) * 0xC2B2AE35u);
             x ^= x >> 15;
             x *= 0x2C1B3C6Du;
             x ^= x >> 12;
             dd[i] = x & dmask;
-            got[i] = rank_atomic(cnt, dd[i], ((x >> 20) & 7u) != 0);  // some lanes sit out
-            if (((x >> 20) & 7u) == 0) got[i] = ~0u;
+            const bool valid = ((x >> 20) & 7u) != 0;  // some lanes sit out
+            got[i] = ballot ? rank_ballot(cnt, dd[i], valid) : (valid ? atomicAdd(&cnt[dd[i]], 1u) : 0u);
+            if (!valid) got[i] = ~0u;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const bool valid = got[i] != ~0u;
             // ground truth: valid lanes with the same digit below this lane, and in earlier items
             uint32_t want = 0;
             for (int j = 0; j <= i; ++j) {
                 uint64_t m = __ballot(got[j] != ~0u);
 #pragma unroll
-                for (int b = 0; b < 8; ++b) {
+                for (int b = 0; b < 10; ++b) {
                     const uint64_t x = __ballot((dd[j] >> b) & 1u);
                     m &= ((dd[i] >> b) & 1u) ? x : ~x;
                 }
                 want += (uint32_t)__popcll(j < i ? m : (m & ((1ull << lane) - 1ull)));
             }
-            nb += valid && got[i] != want;
+            nb += (valid && got[i] != want) ? (ballot ? (1ull << 40) : 1ull) : 0ull;
         }
     }
     if (nb) atomicAdd(bad, nb);
 }
 
+namespace {
+struct RankState {
+    int checked = 0;  // 0 unchecked, 1 lane order holds, -1 it does not
+    int forced = 0;   // ballot-match forced by gk_rank_mode (tests)
+    int active = 0;   // ranking in use: 0 atomic, 1 ballot-match
+};
+std::mutex g_rank_mu;
+std::map<int, RankState> g_rank;  // per device (hipGetDeviceCount-sized by use)
+
+bool env_force_ballot() {
+    const char *v = std::getenv("GKM_RANK_BALLOT");
+    return v && *v && std::strcmp(v, "0") != 0;
+}
+
+hipError_t set_rank_mode_all(int ballot) {
+    hipError_t e = gkm::rank_mode_msd(ballot);
+    if (e == hipSuccess) e = gkm::rank_mode_sort(ballot);
+    return e;
+}
+}  // namespace
+
+// the check on the current device (once per process), then its ranking mode
 static int lds_rank_check(int device) {
-    static int state[64] = {0};  // per device: 0 unchecked, 1 holds, -1 does not
-    if (device < 0 || device >= 64) return GK_E_ARG;
-    if (state[device] != 0) return state[device] > 0 ? GK_OK : GK_E_UNSUPPORTED;
-    unsigned long long *d = nullptr, h = 0;
-    if (hipMalloc(&d, 8) != hipSuccess) return GK_E_HIP;
-    hipError_t e = hipMemset(d, 0, 8);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(lds_rank_check_kernel, dim3(2048), dim3(256), 0, 0, 40u, d);
-        e = hipGetLastError();
+    std::lock_guard<std::mutex> lock(g_rank_mu);
+    RankState &st = g_rank[device];
+    if (st.checked == 0) {
+        unsigned long long *d = nullptr, h = 0;
+        if (hipMalloc(&d, 8) != hipSuccess) return GK_E_HIP;
+        hipError_t e = hipMemset(d, 0, 8);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(lds_rank_check_kernel, dim3(2048), dim3(256), 0, 0, 48u, d);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+        hipFree(d);
+        if (e != hipSuccess) return GK_E_HIP;
+        if (h >> 40) {  // the ballot-match ranking itself is wrong: nothing on this device can sort
+            std::fprintf(stderr, "libgkm: device %d: ballot-match ranks differ from their ground truth (%llu)\n",
+                         device, h >> 40);
+            return GK_E_UNSUPPORTED;
+        }
+        st.checked = h == 0 ? 1 : -1;
+        if (h)
+            std::fprintf(stderr, "libgkm: device %d: a returning LDS atomic did not apply same-address lanes in "
+                                 "lane order (%llu of ~2.5e8 ranks differ); the partitions rank by ballots instead\n",
+                         device, h);
     }
-    if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
-    hipFree(d);
-    if (e != hipSuccess) return GK_E_HIP;
-    state[device] = h == 0 ? 1 : -1;
-    if (h)
-        std::fprintf(stderr, "libgkm: device %d: a returning LDS atomic did not apply same-address lanes in lane "
-                             "order (%llu of ~1e8 ranks differ); the stable partitions need it -- device refused\n",
-                     device, h);
-    return h == 0 ? GK_OK : GK_E_UNSUPPORTED;
+    const int want = (st.checked < 0 || st.forced || env_force_ballot()) ? 1 : 0;
+    if (hipError_t e = set_rank_mode_all(want); e != hipSuccess) return GK_E_HIP;
+    st.active = want;
+    return GK_OK;
+}
+
+extern "C" int gk_rank_mode(gk_ctx *c, int mode, int *active) {
+    if (!c || mode < -1 || mode > 1) return GK_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return GK_E_HIP;
+    std::lock_guard<std::mutex> lock(g_rank_mu);
+    RankState &st = g_rank[c->device];
+    if (mode >= 0) {
+        st.forced = mode == 1;
+        const int want = (st.forced || st.checked < 0 || env_force_ballot()) ? 1 : 0;
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return GK_E_HIP;  // no launch of the old mode in flight
+        if (set_rank_mode_all(want) != hipSuccess) return GK_E_HIP;
+        st.active = want;
+    }
+    if (active) *active = st.active;
+    return GK_OK;
 }
 
 extern "C" int gk_create(gk_ctx **out, int device) {
@@ -678,10 +731,44 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     return GK_OK;
 }
 
+namespace gkm {
+int quicksort_by_rank(uint32_t *A, uint64_t n, const uint32_t *rank_of_pos);  // gkm_qsort.cpp
+}
+
+// GK_SORT_QUICKSORT_ORDER, after the device sort: every start's dense group rank from the device's
+// group pass, then numba's quicksort on the host over the original start order `orig` with rank
+// comparisons (gkm_qsort.cpp); the result replaces the sorted starts.  Only members of a group
+// change places, so keys, head flags and unique counts stay valid.
+static int apply_quicksort_order(gk_ctx *c, std::vector<uint32_t> &orig) {
+    const uint64_t n = c->n;
+    uint64_t G = 0;
+    if (int rc = gk_unique_counts(c, &G)) return rc;
+    if (int rc = materialize_starts(c)) return rc;
+    std::vector<uint32_t> S(n), gs(G);
+    GK_TRY_HIP(c, hipMemcpyAsync(S.data(), c->vals[c->cur], 4 * n, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipMemcpyAsync(gs.data(), c->idx_b, 4 * G, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> rank(c->sba_len + 1, 0);
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint64_t e = g + 1 < G ? gs[g + 1] : n;
+        for (uint64_t i = gs[g]; i < e; ++i) rank[S[i]] = (uint32_t)g;
+    }
+    if (quicksort_by_rank(orig.data(), n, rank.data()) != 0)
+        return fail(c, GK_E_UNSUPPORTED, "numba quicksort stack limit (MAX_STACK = 100) exceeded");
+    GK_TRY_HIP(c, hipMemcpyAsync(c->vals[c->cur], orig.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    return GK_OK;
+}
+
 extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     if (!c) return GK_E_ARG;
-    if (flags & ~GK_SORT_CANONICAL) return fail(c, GK_E_ARG, "unknown gk_sort flags");
+    if (flags & ~(GK_SORT_CANONICAL | GK_SORT_QUICKSORT_ORDER)) return fail(c, GK_E_ARG, "unknown gk_sort flags");
     const bool canonical = (flags & GK_SORT_CANONICAL) != 0;
+    const bool qorder = (flags & GK_SORT_QUICKSORT_ORDER) != 0;
+    if (qorder && canonical)
+        return fail(c, GK_E_ARG, "the reference's quicksort tie order exists for forward k-mers only (no canonical sort)");
+    if (qorder && c->n > kQuicksortOrderMax)
+        return fail(c, GK_E_UNSUPPORTED, "the reference's quicksort tie order runs on the host: at most 2^28 k-mers");
     if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (max_kmer_len != 0 && max_kmer_len < c->min_k) return fail(c, GK_E_ARG, "max_kmer_len is less than min_kmer_len");
@@ -703,6 +790,13 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     c->enum_sorted = false;
     const bool from_enum = c->enumerated;
     int rc;
+    std::vector<uint32_t> orig;  // the start order the reference's quicksort starts from
+    if (qorder && c->n >= 2) {
+        if ((rc = materialize_starts(c))) return rc;
+        orig.resize(c->n);
+        GK_TRY_HIP(c, hipMemcpyAsync(orig.data(), c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    }
     if (c->n < 2) {
         rc = materialize_starts(c);
         if (rc != GK_OK) return rc;
@@ -738,6 +832,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     c->enumerated = false;
     c->sort_len = max_kmer_len;
     c->canonical = canonical;
+    if (qorder) return apply_quicksort_order(c, orig);
     return GK_OK;
 }
 

@@ -26,6 +26,7 @@ namespace gkm {
 constexpr int kRadixBits = 8;
 constexpr int kRadixBins = 256;
 constexpr int kMaxWords = 4;          // direct keys up to 256 bits
+constexpr uint64_t kQuicksortOrderMax = 1ull << 28;  // GK_SORT_QUICKSORT_ORDER: host quicksort bound
 constexpr int kEncodeTile = 4096;     // positions per encode tile
 constexpr int kSbaPad = 32768;        // '$' bytes after the sba (>= largest tile + max symbols)
 constexpr int kSortThreads = 256;     // radix pass workgroup
@@ -207,6 +208,10 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
 int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t digit_hi, uint64_t *n_kept);
 // width of the key-range ownership digits (gk_shard_histogram's bins: 1 << width)
 int range_own_bits(const KeySpec &ks);
+// partition ranking of each code object: lane-ordered LDS atomics (0) or ballot-match (1), set
+// by gk_create from lds_rank_check (gkm_partition.h: g_rank_ballot)
+hipError_t rank_mode_msd(int ballot);
+hipError_t rank_mode_sort(int ballot);
 // key / start buffers for n elements and `words` key words (gkm_capi.hip)
 int ensure_elems(gk_ctx *c, uint64_t n, int words);
 // key buffer b alone grown to `words` key words of elem_cap elements (contents not kept)

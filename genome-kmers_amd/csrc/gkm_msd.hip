@@ -1347,6 +1347,9 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
                                                       int skip, uint32_t small, const uint64_t *__restrict__ cpref,
                                                       const uint8_t *__restrict__ cnd) {
     constexpr int CAP = 64 * I;
+    // bit budget of the packed per-item words below: sub-bucket start (slot) in 10 bits, size in 11,
+    // rank in 11, and the slot in the low 10 bits of a composite rank-by-count value
+    static_assert(CAP <= 1024, "slot fields are 10 bits wide");
     constexpr int MINLIVE = I > 4 ? I / 2 + 1 : 1;  // items a bucket of the class always fills
     constexpr int RADIX = 1 << R, CPL = RADIX / 64;  // digits; counters per lane in the scan
     static_assert(CPL % 4 == 0, "16-byte counter groups");
@@ -2762,6 +2765,7 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
 }
 
 int msd_radix_bits() { return kGR; }
+hipError_t rank_mode_msd(int ballot) { return set_rank_ballot_here(ballot); }
 
 // L0 digit width of the key-range shards: 7 bits for 2-bit keys (as msd_sort), 8 otherwise
 static int range_width(const KeySpec &ks) { return ks.bits == 2 ? 7 : kGR; }

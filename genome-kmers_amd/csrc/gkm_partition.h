@@ -69,10 +69,42 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // stable rank.  Successive items of a wave accumulate in order (one wave's LDS operations complete
 // in order).  A ballot-match takes R + 1 ballots per item and the LDS-mask round trip five LDS
 // instructions (tools/lds_rank_probe.hip: 3.9 vs 0.88 T items/s chip-wide).  The lane order is a
-// hardware property, not an ISA guarantee: gk_create checks it once per process (gkm_capi.hip,
-// lds_rank_check) and refuses a device where it does not hold.
+// hardware property, not an ISA guarantee: gk_create checks it once per device and process
+// (gkm_capi.hip, lds_rank_check) over every digit width the partitions use, and where it does not
+// hold switches every partition to the ballot-match ranking below (g_rank_ballot), which relies
+// on nothing but ballots: the same ranks, slower.
+//
+// g_rank_ballot: one copy per code object (every .hip file that ranks sets its own, gk_create ->
+// rank_mode_*); read once per kernel into an SGPR, the test is one scalar branch per item.
+static __constant__ int g_rank_ballot = 0;
+
+// Ballot-match rank: the valid lanes with this lane's digit (digits of up to 10 bits) by 10
+// ballots, the rank among them by mbcnt, and one returning atomic per distinct digit, from the
+// lowest such lane (distinct addresses: lane order cannot matter), whose pre-add count is then
+// broadcast to its peers.
+__device__ __forceinline__ uint32_t rank_ballot(uint32_t *wc, uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 10; ++b) {
+        const uint64_t x = __ballot((d >> b) & 1u);
+        m &= ((d >> b) & 1u) ? x : ~x;
+    }
+    const uint32_t below = lanes_below(m);
+    uint32_t old = 0;
+    if (valid && below == 0) old = atomicAdd(&wc[d], (uint32_t)__popcll(m));
+    const int leader = m ? __builtin_ctzll(m) : 0;
+    old = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old);
+    return valid ? old + below : 0u;
+}
+
 __device__ __forceinline__ uint32_t rank_atomic(uint32_t *wc, uint32_t d, bool valid) {
+    if (__builtin_expect(g_rank_ballot != 0, 0)) return rank_ballot(wc, d, valid);
     return valid ? atomicAdd(&wc[d], 1u) : 0u;
+}
+
+// host: switch this code object's partitions to the ballot-match ranking (or back)
+static inline hipError_t set_rank_ballot_here(int on) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_rank_ballot), &on, sizeof(int));
 }
 
 // ranks of I items (items >= live hold no valid element: skipped, wave-uniform)

@@ -82,6 +82,8 @@ static hipError_t launch_pass(gk_ctx *c, int word, int shift, const uint32_t *do
 }
 
 // Sort (keys[cur], vals[cur]) by the low total_bits of the W-word keys; result in keys/vals[cur].
+hipError_t rank_mode_sort(int ballot) { return set_rank_ballot_here(ballot); }
+
 int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready) {
     const int D = (total_bits + 7) / 8;
     if (c->n < 2 || D == 0) return GK_OK;

@@ -55,10 +55,11 @@ EXPORTED = (
     "gk_profile_enable", "gk_profile_report", "gk_stream", "gk_shard_bucket_bits", "gk_shard_partition",
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range", "gk_shard_class_b", "gk_shard_class_b_copy",
-    "gk_shard_sort_range_b",
+    "gk_shard_sort_range_b", "gk_rank_mode", "gk_reference_random_bases",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
+SORT_QUICKSORT_ORDER = 2  # GK_SORT_QUICKSORT_ORDER
 
 
 class GkFilter(ctypes.Structure):
@@ -142,6 +143,8 @@ _SIGS = {
     "gk_fasta_close": ([_P], None),
     "gk_locate": ([_P, _U64P, ctypes.c_uint64, _U32P, _U32P], ctypes.c_int),
     "gk_copy_strands": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
+    "gk_rank_mode": ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "gk_reference_random_bases": ([_U8P, ctypes.c_uint64, ctypes.c_uint32], ctypes.c_int),
 }
 
 
@@ -231,6 +234,16 @@ def read_fasta(path, n_threads: int = 0):
     return sba, seg_starts, name_list, set(np.flatnonzero(bad).tolist())
 
 
+def reference_random_bases(n: int, seed: int) -> np.ndarray:
+    """The reference's profiling genome (profiling.get_random_seq after np.random.seed(seed)) as n
+    ASCII bytes, from libgkm's host MT19937 (gk_reference_random_bases)."""
+    out = np.empty(n, dtype=np.uint8)
+    rc = load_library().gk_reference_random_bases(_ptr(out, ctypes.c_uint8), n, int(seed) & 0xFFFFFFFF)
+    if rc != GK_OK:
+        raise GkError(rc, "gk_reference_random_bases failed")
+    return out
+
+
 def _ptr(arr: np.ndarray, ctype):
     return arr.ctypes.data_as(ctypes.POINTER(ctype))
 
@@ -267,6 +280,14 @@ class Engine:
             self.lib.gk_destroy(ctx)
             self.ctx = None
 
+    def rank_mode(self, mode: int = -1) -> int:
+        """Partition ranking on this engine's device (gk_rank_mode): mode -1 queries, 0 restores the
+        device's checked default, 1 forces the ballot-match fallback.  Returns 1 if ballot-match
+        ranking is in use afterwards."""
+        active = ctypes.c_int(0)
+        self._check(self.lib.gk_rank_mode(self.ctx, int(mode), ctypes.byref(active)))
+        return active.value
+
     # -----------------------------------------------------------------------------------------
     def _check(self, rc: int):
         if rc != GK_OK:
@@ -295,8 +316,8 @@ class Engine:
         self._check(self.lib.gk_set_start_indices(self.ctx, _ptr(arr, ctypes.c_uint32), arr.size, min_kmer_len))
         self.n = arr.size
 
-    def sort(self, max_kmer_len: int = None, canonical: bool = False):
-        flags = SORT_CANONICAL if canonical else 0
+    def sort(self, max_kmer_len: int = None, canonical: bool = False, quicksort_order: bool = False):
+        flags = (SORT_CANONICAL if canonical else 0) | (SORT_QUICKSORT_ORDER if quicksort_order else 0)
         self._check(self.lib.gk_sort(self.ctx, 0 if max_kmer_len is None else int(max_kmer_len), flags))
 
     def copy_strands(self) -> np.ndarray:

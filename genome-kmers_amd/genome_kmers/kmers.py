@@ -766,8 +766,8 @@ class Kmers:
             g["_is_initialized"] = self._is_initialized
             g["_is_set"] = self._is_set
             # a canonical order is not the reference's sort order: the file says "not sorted" to the
-            # reference's loader (kmers.py:1435-1472), which then re-sorts instead of trusting it,
-            # and keeps the canonical state in keys of its own, which only this build reads
+            # reference's loader (kmers.py:939-960, 1435-1472), which then treats the object as
+            # unsorted, and keeps the canonical state in keys of its own, which only this build reads
             g["_is_sorted"] = False if self._canonical else self._is_sorted
             s = self.kmer_sba_start_indices
             g["kmer_sba_start_indices"] = np.array([], dtype=np.uint32) if s is None else s
@@ -807,7 +807,9 @@ class Kmers:
             starts = None if s.shape == (0,) else s
             canonical = bool(g["_canonical"][()]) if "_canonical" in g else False
             if canonical:
-                self._is_sorted = bool(g["_canonical_sorted"][()])
+                # a canonical file written before the key existed: keep the stored flag
+                if "_canonical_sorted" in g:
+                    self._is_sorted = bool(g["_canonical_sorted"][()])
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="hdf5")
@@ -834,7 +836,7 @@ class Kmers:
             starts = db["kmer_sba_start_indices"]
             canonical = bool(db.get("_canonical", False))
             if canonical:
-                self._is_sorted = bool(db["_canonical_sorted"])
+                self._is_sorted = bool(db.get("_canonical_sorted", self._is_sorted))
         if seq_coll is None:
             seq_coll = SequenceCollection()
             seq_coll.load(load_file_path, format="shelve")
@@ -877,13 +879,17 @@ class Kmers:
         return bytes(self.seq_coll.forward_sba[start : start + kmer_len]).decode("utf-8")
 
     # ---- sort (kmers.py:1624-1731) -----------------------------------------------------------
-    def sort(self, *, canonical: bool = False):
+    def sort(self, *, canonical: bool = False, order: str = "stable"):
         """Sort the start indices by k-mer on the GPU (in place from the caller's point of view).
 
-        Tie order: equal k-mers come back in ascending start order -- the reference's
-        ``get_is_less_than_func(break_ties=True)`` order (kmers.py:1710-1711).  The reference's own
-        ``sort()`` uses ``break_ties=False`` and leaves equal k-mers in whatever order numba's
-        quicksort produces (kmers.py:1624-1652); no parallel sort reproduces that.  Sorted k-mers,
+        Tie order (``order="stable"``, the default): equal k-mers come back in ascending start
+        order -- the reference's ``get_is_less_than_func(break_ties=True)`` order
+        (kmers.py:1710-1711).  The reference's own ``sort()`` uses ``break_ties=False`` and leaves
+        equal k-mers in whatever order numba's quicksort produces (kmers.py:1624-1652); no parallel
+        sort reproduces that.  ``order="reference"`` gives exactly that order: the device sorts,
+        then numba's quicksort runs on the host over the original start order, comparing the
+        device's group ranks (libgkm GK_SORT_QUICKSORT_ORDER; host-bound, at most 2^28 k-mers, not
+        with canonical=True).  Sorted k-mers,
         encoded keys, group sizes, counts, histograms and the ``(kmer_num, group_size_yielded,
         group_size_total)`` tuples of ``get_kmers`` are identical either way, because ties only
         permute the members of a group inside the group's index range.  What can differ is WHICH
@@ -898,12 +904,17 @@ class Kmers:
         get_canonical_strands() tells which strand each sorted k-mer's canonical form came from.
         """
         self._check_forward()
+        if order not in ("stable", "reference"):
+            raise ValueError(f"order must be 'stable' or 'reference' (order = {order!r})")
+        if canonical and order == "reference":
+            raise ValueError("order='reference' is the reference's forward-strand quicksort order; the reference "
+                             "has no canonical k-mers")
         if canonical and (self.max_kmer_len is None or self.max_kmer_len != self.min_kmer_len):
             raise ValueError(f"canonical k-mers need min_kmer_len == max_kmer_len (min_kmer_len = "
                              f"{self.min_kmer_len}, max_kmer_len = {self.max_kmer_len})")
         self._sync_device()
         try:
-            self._engine.sort(self.max_kmer_len, canonical=canonical)
+            self._engine.sort(self.max_kmer_len, canonical=canonical, quicksort_order=order == "reference")
         except _native.GkError as e:
             if e.code == _native.GK_E_NO_BASES:
                 raise AssertionError(

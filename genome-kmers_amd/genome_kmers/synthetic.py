@@ -1,8 +1,10 @@
 """Synthetic genomes of BASELINE.json's configs, shared by bench.py and the
 config-scale parity tests.  There is no network and no FASTA on the GPU box, so every config is a
-seeded surrogate of stated shape.  The reference's own generator is ``profiling.get_random_seq``
-(``np.random.seed`` + ``randint(0, 4)`` over ``b"ATGC"``, profiling.py:12-24); these use numpy's
-PCG64 in chunks so a 3.1 Gb genome is made in seconds without a 25 GB int64 temporary.
+seeded surrogate of stated shape.  C3 is the reference's own profiling genome:
+``profiling.get_random_seq`` after ``np.random.seed(seed)`` (``np.random.choice`` over
+``["A", "T", "G", "C"]``, profiling.py:12-24), made by libgkm's host MT19937
+(``gk_reference_random_bases``: the same bytes as numpy's legacy RandomState, 3.1 Gb in seconds
+and without a 25 GB int64 temporary).  The other surrogates use numpy's PCG64 in chunks.
 
 Every function returns ``(sba, seg_starts)`` in the reference's SequenceCollection layout
 (contigs joined by '$', no trailing '$'; sequence_collection.py:663-726).
@@ -34,8 +36,11 @@ def random_bases(L: int, seed: int, lut: np.ndarray = np.frombuffer(b"ATGC", dty
 
 
 def c3_genome(L: int = 3_100_000_000, seed: int = 42):
-    """C3: one random contig of L bases (BASELINE.json configs[2])."""
-    return random_bases(L, seed), np.zeros(1, dtype=np.uint32)
+    """C3: one random contig of L bases (BASELINE.json configs[2]) -- the reference's profiling
+    genome for this seed (profiling.get_random_seq(L) after np.random.seed(seed))."""
+    from genome_kmers import _native
+
+    return _native.reference_random_bases(L, seed), np.zeros(1, dtype=np.uint32)
 
 
 def c2_surrogate(seed: int = 1, L: int = C2_LENGTH):

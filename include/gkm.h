@@ -94,6 +94,11 @@ typedef struct gk_filter {
  * IUPAC complement (sequence_collection.py:402-433).  Fixed length only (min_kmer_len ==
  * max_kmer_len); groups, counts and keys then refer to the canonical k-mers. */
 #define GK_SORT_CANONICAL 1u
+/* The reference's default tie order (Kmers.sort: numba quicksort, break_ties=False,
+ * kmers.py:1624-1652): the device sorts, then numba's quicksort runs on the host over the original
+ * start order comparing the device's group ranks (gkm_qsort.cpp) -- bit-exact with the reference,
+ * equal k-mers included.  Host-bound: at most 2^28 k-mers; not with GK_SORT_CANONICAL. */
+#define GK_SORT_QUICKSORT_ORDER 2u
 
 /* ---- lifetime ------------------------------------------------------------------------------ */
 int gk_create(gk_ctx **out, int device);
@@ -101,6 +106,13 @@ void gk_destroy(gk_ctx *ctx);
 const char *gk_last_error(gk_ctx *ctx);
 int gk_sync(gk_ctx *ctx);
 int gk_device_count(int *count);
+/* Partition ranking of the sort on ctx's device.  Every stable partition ranks an item by one
+ * returning LDS atomic, which relies on gfx950 applying same-address lanes in lane order;
+ * gk_create checks that on every device it opens and, where it does not hold (or GKM_RANK_BALLOT=1
+ * is set), switches to a ballot-match ranking: the same order, slower.  mode: -1 = query only,
+ * 0 = the device's checked default, 1 = ballot-match forced (tests).  *active (may be NULL):
+ * 1 if ballot-match ranking is in use afterwards, else 0. */
+int gk_rank_mode(gk_ctx *ctx, int mode, int *active);
 
 /* ---- input contract ------------------------------------------------------------------------- */
 /* sba: ASCII bases, contigs joined by '$' (36), no trailing '$'; seg_starts: ascending uint32. */
@@ -263,6 +275,12 @@ int gk_fasta_open(const char *path, int n_threads, gk_fasta **out, uint64_t *num
 int gk_fasta_fill(gk_fasta *f, uint8_t *sba, uint64_t sba_len, uint32_t *seg_starts, char *names,
                   uint8_t *bad_bytes);
 void gk_fasta_close(gk_fasta *f);
+
+/* ---- synthetic genomes (host) --------------------------------------------------------------
+ * The reference's profiling genome: profiling.get_random_seq(n) after np.random.seed(seed)
+ * (profiling.py:12-24) -- MT19937 init_genrand(seed), base i = "ATGC"[genrand_int32() & 3] --
+ * written as n ASCII bytes. */
+int gk_reference_random_bases(uint8_t *out, uint64_t n, uint32_t seed);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,9 @@
 The reference's sort (numba quicksort + compare_sba_kmers_lexicographically with validation,
 kmers.py:1624-1731), as restated in oracle/gk_oracle.c (gcc -O3, 1 thread -- the reference is
 single-threaded, kmers.py:1644-1648), timed on the first 1e8 and 3e8 bases of the C3 genome
-(numpy PCG64 seed 42, genome_kmers.synthetic.random_bases: the same stream as bench.py's C3), and
+(the reference's profiling genome, get_random_seq after np.random.seed(42):
+genome_kmers.synthetic.c3_genome, the same stream as bench.py's C3; its prefixes are the genome's
+first bases), and
 extrapolated to the full 3,099,999,970 31-mers two ways, both labelled as extrapolations:
 N log2 N from each prefix, and a power law fitted through the two prefixes (which carries the
 growth of cache misses from 1e8 to 3e8 keys).
@@ -50,10 +52,10 @@ def heartbeat(stop):
 
 
 def main():
-    out = Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "profiles" / "r3" / "cpu_baseline_prefixes.json"
+    out = Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "profiles" / "r4" / "cpu_baseline_prefixes.json"
     runs = []
     for L in (100_000_000, 300_000_000):
-        sba = synthetic.random_bases(L, 42)
+        sba, _ = synthetic.c3_genome(L, 42)
         n = L - K + 1
         starts = np.arange(n, dtype=np.uint32)
         print(f"[cpu baseline] {L:,} bases, {n:,} k-mers: sorting ...", file=sys.stderr, flush=True)
@@ -80,7 +82,8 @@ def main():
     power = round(t2 * (N_FULL / n2) ** a, 1)
     res = {
         "what": "numba-quicksort restatement of Kmers.sort with validate_kmers (oracle/gk_oracle.c, gcc -O3), "
-                "1 thread, on prefixes of the C3 genome (PCG64 seed 42), k = 31",
+                "1 thread, on prefixes of the C3 genome, k = 31",
+        "genome": "the reference's profiling genome: get_random_seq after np.random.seed(42) (MT19937)",
         "cpu_model": cpu_model(), "cores_on_box": os.cpu_count(), "threads_used": 1,
         "prefixes": runs,
         "full_workload": {

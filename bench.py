@@ -5,10 +5,9 @@ enumerate -> encode (2-bit keys) -> stable MSD radix sort -> unique k-mers + mul
 `value` is measured at the DEVICE boundary (the bench contract: inputs resident in HBM when the
 timed region starts); the step ends with the whole product resident in HBM -- sorted start
 indices, sorted keys, and per distinct k-mer its first sorted index and multiplicity.  The
-end-to-end boundary of BASELINE.md section 3 is reported beside it: `value_e2e` adds the H2D of
-the sba from pinned host memory, `value_e2e_pipelined` is a stream of genomes where the next sba's
-pinned H2D runs on its own stream during the current sort (one GPU), and the D2H of the sorted
-start indices is reported apart.
+end-to-end boundary of BASELINE.md section 3 is reported beside it: `value_e2e` is one wall-clock
+interval from the caller's pageable numpy sba on the host to the product in HBM (gk_set_sequence's
+2-bit packed transfer, then one step), and the D2H of the sorted start indices is reported apart.
 Timed with a barrier + device synchronisation on both sides, max over ranks.
 
 N = 1: the genome on one MI355X.  N > 1 (torch.distributed, one rank per GPU), total work fixed,
@@ -51,13 +50,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3",
+    ap.add_argument("--config", choices=("c3", "c4", "c5", "ref_profile"), default="c3",
                     help="c3: the headline (3.1 Gb single contig, k=31); c4: GRCh38-shaped surrogate (24 "
-                         "contigs, ~5%% N, diverged repeats), k=31; c5: the same genome, k=63, canonical")
+                         "contigs, ~5%% N, diverged repeats), k=31; c5: the same genome, k=63, canonical; "
+                         "ref_profile: the reference's own Kmers.sort profiling workload (tools/run_profiling.py "
+                         "kmers_sort 'large': 1e8 bases in 10 contigs, min_kmer_len=1, --max-kmer-len 20 or none)")
+    ap.add_argument("--max-kmer-len", default="20", help="ref_profile: max_kmer_len (an integer, or 'none')")
+    ap.add_argument("--ref-bases", type=int, default=100_000_000, help="ref_profile: total sequence length")
     ap.add_argument("--genome-len", type=int, default=None, help="c3 genome length (default 3.1e9)")
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=16_000_000, help="k-mers in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=4_000_000,
+                    help="k-mers in the CPU-baseline sample (starts spread over the whole genome: ~15 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU path even at N = 1 (exercises it on one GPU)")
@@ -90,7 +94,7 @@ def cpu_baseline(sba: np.ndarray, k: int, sample: int, n_full: int) -> dict:
       `sample` k-mers whose starts are spread evenly over the WHOLE genome (every comparison reads
       two windows anywhere in the 3.1 GB sba, as the full sort's do), and its N log2 N
       extrapolation to the full workload, labelled as such;
-      context: `sample` CONSECUTIVE k-mers (a ~16 MB window: mostly cache-resident, faster), and
+      context: `sample` CONSECUTIVE k-mers (a few-MB window: cache-resident, faster), and
       the 1e8 / 3e8-base prefix runs measured outside the bench's budget."""
     from genome_kmers import synthetic
     from oracle import oracle
@@ -142,8 +146,8 @@ def cpu_baseline(sba: np.ndarray, k: int, sample: int, n_full: int) -> dict:
             "c1": {"kmers": n1, "seconds": round(t1, 4), "kmers_per_s": round(n1 / t1, 1)},
             "c2": {"kmers": n2, "seconds": round(t2, 3), "kmers_per_s": round(n2 / t2, 1)},
             "consecutive_sample": {"kmers": nc, "seconds": round(tc, 2), "kmers_per_s": round(nc / tc, 1),
-                                   "note": "consecutive k-mers of a ~16 MB window: cache-resident, not the "
-                                           "full run's regime (context only)"},
+                                   "note": "consecutive k-mers of one window: cache-resident, not the full "
+                                           "run's regime (context only)"},
             "full_workload_extrapolated": {"kmers": n_full, "seconds": round(t_full, 1),
                                            "kmers_per_s": round(n_full / t_full, 1),
                                            "method": "spread-sample time x (N log2 N) / (n log2 n); extrapolated, "
@@ -185,8 +189,10 @@ def window_check(eng, sba: np.ndarray, k: int, canonical: bool, width: int = 204
 
 def transfer_times(torch, eng, sba, seg, log, reps: int = 3) -> dict:
     """The transfers either side of the device boundary, after the timed
-    steps: D2H of the sorted start indices into pinned host memory, then H2D of the sba from pinned
-    host memory through gk_set_sequence (which also runs the device alphabet check); best of reps."""
+    steps, best of reps: the D2H of the sorted start indices into pinned host memory; gk_set_sequence
+    from the caller's pageable numpy sba (the packed transfer: host packing + census, 2-bit H2D,
+    device unpack; gkm_xfer.hip) until the sba is resident; and, for context, a plain H2D of the
+    ASCII sba from pinned host memory (what one unpacked copy over the link costs)."""
     n = eng.n
     out = {}
     host = torch.empty(max(n, 1), dtype=torch.int32).pin_memory().numpy().view(np.uint32)
@@ -198,50 +204,50 @@ def transfer_times(torch, eng, sba, seg, log, reps: int = 3) -> dict:
     out["d2h_starts_ms"] = round(best * 1e3, 2)
     out["d2h_starts_gbs"] = round(4 * n / best / 1e9, 1)
     del host
-    pinned = torch.empty(len(sba), dtype=torch.uint8).pin_memory().numpy()
-    pinned[:] = sba
-    best = float("inf")
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        eng.set_sequence(pinned, seg)
-        eng.sync()
-        best = min(best, time.perf_counter() - t0)
-    out["h2d_pinned_ms"] = round(best * 1e3, 2)
-    out["h2d_pinned_gbs"] = round(len(sba) / best / 1e9, 1)
-    log(f"transfers: {out}")
-    return out
-
-
-def pipelined_e2e(torch, eng, sba, step, log, reps: int = 3) -> dict:
-    """End to end as a stream of genomes (one GPU): while step i sorts the resident sba, the next
-    genome's sba (here: a second copy of the same bytes, from pinned host memory) is copied H2D on a
-    separate stream into its own device buffer.  Wall time per step with both in flight; best of
-    reps.  The copy is the transfer BASELINE.md section 3 adds; it overlaps the sort instead of
-    preceding it."""
-    pinned = torch.empty(len(sba), dtype=torch.uint8).pin_memory()
-    pinned.numpy()[:] = sba
-    nxt = torch.empty(len(sba), dtype=torch.uint8, device="cuda")
-    side = torch.cuda.Stream()
     best = float("inf")
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        with torch.cuda.stream(side):
-            nxt.copy_(pinned, non_blocking=True)
+        eng.set_sequence(sba, seg)
+        eng.sync()
+        best = min(best, time.perf_counter() - t0)
+    out["set_sequence_ms"] = round(best * 1e3, 2)
+    out["set_sequence_gbs"] = round(len(sba) / best / 1e9, 1)
+    pinned = torch.empty(len(sba), dtype=torch.uint8).pin_memory()
+    pinned.numpy()[:] = sba
+    dev = torch.empty(len(sba), dtype=torch.uint8, device="cuda")
+    best = float("inf")
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.copy_(pinned, non_blocking=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    del dev, pinned
+    out["h2d_ascii_pinned_ms"] = round(best * 1e3, 2)
+    out["h2d_ascii_pinned_gbs"] = round(len(sba) / best / 1e9, 1)
+    log(f"transfers: {out}")
+    return out
+
+
+def end_to_end(torch, eng, sba, seg, step, log, reps: int = 3) -> dict:
+    """BASELINE.md section 3's end-to-end boundary, measured as one wall-clock interval: from the
+    caller's pageable numpy sba on the host to the whole product resident in HBM -- gk_set_sequence
+    (host packing, 2-bit H2D overlapped with it, device unpack) followed by one step, device
+    synchronised.  Best of reps."""
+    best, best_set = float("inf"), 0.0
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.set_sequence(sba, seg)
+        t1 = time.perf_counter()
         step()
         eng.sync()
-        side.synchronize()
-        best = min(best, time.perf_counter() - t0)
-    # the copy alone on the same buffers (how much of it the step hid)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(side):
-        nxt.copy_(pinned, non_blocking=True)
-    side.synchronize()
-    alone = time.perf_counter() - t0
-    del nxt, pinned
-    out = {"step_with_h2d_ms": round(best * 1e3, 2), "h2d_alone_ms": round(alone * 1e3, 2)}
-    log(f"pipelined end to end: {out}")
+        t2 = time.perf_counter()
+        if t2 - t0 < best:
+            best, best_set = t2 - t0, t1 - t0
+    out = {"e2e_ms": round(best * 1e3, 2), "set_sequence_host_ms": round(best_set * 1e3, 2)}
+    log(f"end to end: {out}")
     return out
 
 
@@ -261,6 +267,144 @@ def load_traffic(path: str, kernel: str):
         if not name.startswith("_") and "<" in name and name.startswith(want):
             return rec.get("hbm_bytes_max_launch"), f"{rel} ({t.get('_label', '')}; {t.get('_convention', '')})"
     return None, f"{rel}: no {kernel} record"
+
+
+def ref_profile_sba(total: int, contigs: int = 10, seed: int = 42):
+    """profiling.get_random_seq_list(total, contigs) after np.random.seed(seed) (profiling.py:30-60):
+    contigs of total // contigs bases (the last takes the rest), drawn one after another from the
+    same stream, joined by '$' as SequenceCollection does (sequence_collection.py:663-726)."""
+    from genome_kmers import _native
+
+    bases = _native.reference_random_bases(total, seed)
+    avg = total // contigs
+    cuts = [i * avg for i in range(contigs)] + [total]
+    sba = np.empty(total + contigs - 1, dtype=np.uint8)
+    seg = np.empty(contigs, dtype=np.uint32)
+    at = 0
+    for i in range(contigs):
+        piece = bases[cuts[i]:cuts[i + 1]]
+        seg[i] = at
+        sba[at:at + len(piece)] = piece
+        at += len(piece)
+        if i + 1 < contigs:
+            sba[at] = 36
+            at += 1
+    return sba, seg
+
+
+def order_check(eng, sba: np.ndarray, max_len, width: int = 2048) -> int:
+    """Self-check of a variable-length / suffix sort (no oracle): windows of the sorted starts are
+    non-decreasing by their k-mers -- bytes up to '$' (or the end), capped at max_len -- with equal
+    k-mers in ascending start order."""
+    n = eng.n
+    cap = max_len if max_len is not None else 1 << 62
+
+    def kmer(s):
+        w = 64
+        while True:
+            b = bytes(sba[s:s + min(w, cap)]).split(b"$")[0]
+            if len(b) < min(w, cap) or w >= cap or s + w >= len(sba):
+                return b
+            w *= 4
+
+    checked = 0
+    for off in sorted({0, max(n // 2 - width // 2, 0), max(n - width, 0)}):
+        w = eng.start_range(off, min(width, n - off)).tolist()
+        prev = kmer(w[0])
+        for a, b in zip(w, w[1:]):
+            cur = kmer(b)
+            if cur < prev or (cur == prev and b < a):
+                raise SystemExit(f"bench self-check: sorted order broken near index {off}")
+            prev = cur
+        checked += len(w)
+    return checked
+
+
+def run_ref_profile(args, torch, result_out, log):
+    """The reference's own profiled sort workload (tools/run_profiling.py:226-236, profiling.py:367-448):
+    Kmers(min_kmer_len=1, max_kmer_len=M).sort() over 1e8 bases in 10 contigs, seed 42.  A step is
+    enumerate + sort, the call the reference times (run_kmers_sort).  M = 20: bounded variable-length
+    keys (2-bit padded symbols + length, 45 bits) through the LSD onesweep; M = None (the Kmers
+    default): prefix doubling."""
+    from genome_kmers import _native
+    from oracle import oracle
+
+    M = None if str(args.max_kmer_len).lower() == "none" else int(args.max_kmer_len)
+    sba, seg = ref_profile_sba(args.ref_bases)
+    eng = _native.Engine(0)
+    eng.set_sequence(sba, seg)
+    eng.sync()
+    n = eng.enumerate(1)
+
+    def step():
+        eng.enumerate(1)
+        eng.sort(M)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.profile_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    report = eng.profile_report()
+    eng.profile_enable(False)
+    checked = order_check(eng, sba, M)
+    words, bits, _ = eng.key_layout()
+    # dominant kernel: the LSD onesweep pass (every radix_pass launch: keys W words + start in and out)
+    rp = report.get("radix_pass", {"count": 0, "total_ms": 0.0, "units": 0})
+    per_unit = 2 * (8 * max(words, 1) + 4)
+    avg_ms = rp["total_ms"] / max(rp["count"], 1)
+    units = rp["units"] / max(rp["count"], 1)
+    achieved = per_unit * units / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
+    cpu = None
+    if not args.no_cpu_baseline:
+        # DRAM regime: 2M starts spread over the whole sba (every position outside '$' is a start)
+        valid = np.flatnonzero(sba != 36).astype(np.uint32)
+        sample = valid[:: max(1, len(valid) // 2_000_000)]
+        t1 = time.perf_counter()
+        oracle.quicksort(sba, sample, 1, M)
+        tc = time.perf_counter() - t1
+        ns = len(sample)
+        t_full = tc * (n * np.log2(n)) / (ns * np.log2(ns))
+        cpu = {"value": ns / tc, "unit": "k-mers/s", "cores": 1, "kind": "port",
+               "sample": f"{ns:,} starts spread over the whole {len(sba):,}-byte sba, numba-quicksort restatement "
+                         f"of Kmers.sort (min_kmer_len=1, max_kmer_len={M}) with validate_kmers, gcc -O3, 1 thread; "
+                         f"{tc:.1f} s",
+               "cpu_model": _cpu_model(), "cores_on_box": os.cpu_count(),
+               "full_workload_extrapolated": {"kmers": n, "seconds": round(t_full, 1),
+                                              "kmers_per_s": round(n / t_full, 1),
+                                              "method": "sample time x (N log2 N) / (n log2 n); extrapolated, not "
+                                                        "measured"}}
+    line = {
+        "metric": f"Kmers.sort() k-mers/sec on the reference's profiling workload (run_profiling.py kmers_sort "
+                  f"'large': {args.ref_bases:,} bases, 10 contigs, min_kmer_len=1, max_kmer_len={M})",
+        "value": round(n * args.steps / dt, 1), "unit": "k-mers/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: profiling.get_random_seq_list(1e8, 10) after np.random.seed(42) (MT19937 stream, "
+                "gk_reference_random_bases)",
+        "boundary": "device: sba resident in HBM; step = enumerate + sort (the call the reference times); sorted "
+                    "starts and keys (M=20) / ranks (M=None) resident at the end",
+        "self_check": f"{checked:,} sorted k-mers in windows re-checked against the sba bytes",
+        "config": {"workload": f"ref_profile: {args.ref_bases:,} bases in 10 contigs, min_kmer_len=1, "
+                               f"max_kmer_len={M}", "kmers": n,
+                   "sort_path": "LSD onesweep over (2-bit padded, length) keys" if M is not None and bits else
+                                "prefix doubling (seed keys, then rank pairs)",
+                   "key_words": words, "key_bits": bits, "stages_ms_per_step": stages},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": f"onesweep_kernel (W = {max(words, 1)}; radix_pass: one stable 8-bit LSD pass with decoupled look-back)",
+                     "avg_launch_ms": round(avg_ms, 4), "launches_per_step": round(rp["count"] / args.steps, 2),
+                     "units_per_launch": int(units), "bytes_per_unit": per_unit},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), file=result_out, flush=True)
 
 
 def main():
@@ -288,6 +432,11 @@ def main():
 
     from genome_kmers import _native, synthetic
 
+    if args.config == "ref_profile":
+        if world != 1:
+            raise SystemExit("--config ref_profile runs on one GPU")
+        return run_ref_profile(args, torch, result_out,
+                               lambda m: print(f"[bench] {m}", file=sys.stderr, flush=True))
     cfg = args.config
     k = args.k or (63 if cfg == "c5" else 31)
     canonical = cfg == "c5"
@@ -375,12 +524,16 @@ def main():
         if int(t.item()) != n_units:
             raise SystemExit(f"bench self-check: ranks hold {int(t.item())} k-mers, expected {n_units}")
     boundary = transfer_times(torch, eng, sba, seg, log)
-    if dist is not None:
-        t = torch.tensor([boundary["h2d_pinned_ms"], boundary["d2h_starts_ms"]], dtype=torch.float64, device="cuda")
+    if dist is None:
+        e2e = end_to_end(torch, eng, sba, seg, step, log)
+        e2e_ms = e2e["e2e_ms"]
+    else:  # ranks: each loads the whole sba; the slowest transfer + the step (max over ranks)
+        t = torch.tensor([boundary["set_sequence_ms"], boundary["d2h_starts_ms"]], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        boundary["h2d_pinned_ms"], boundary["d2h_starts_ms"] = round(float(t[0]), 2), round(float(t[1]), 2)
-    value_e2e = n_units / ((ms_per_step + boundary["h2d_pinned_ms"]) * 1e-3)
-    pipe = pipelined_e2e(torch, eng, sba, step, log) if dist is None else None
+        boundary["set_sequence_ms"], boundary["d2h_starts_ms"] = round(float(t[0]), 2), round(float(t[1]), 2)
+        e2e = None
+        e2e_ms = ms_per_step + boundary["set_sequence_ms"]
+    value_e2e = n_units / (e2e_ms * 1e-3)
 
     # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4
     seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
@@ -440,12 +593,12 @@ def main():
     # BASELINE.md section 3, verbatim: the step's read roofline n * 105 B / t (device boundary and
     # end to end), and the total-traffic fraction n * 201 B / t -- a model of the whole step, beside
     # the dominant kernel's own byte model above
-    t_dev, t_e2e = ms_per_step * 1e-3, (ms_per_step + boundary["h2d_pinned_ms"]) * 1e-3
+    t_dev, t_e2e = ms_per_step * 1e-3, e2e_ms * 1e-3
     base = {"baseline_read_frac": round(n_units * BASELINE_READ_B / t_dev / (HBM_PEAK_GBS * 1e9), 4),
             "baseline_read_frac_e2e": round(n_units * BASELINE_READ_B / t_e2e / (HBM_PEAK_GBS * 1e9), 4),
             "baseline_total_frac": round(n_units * BASELINE_TOTAL_B / t_dev / (HBM_PEAK_GBS * 1e9), 4),
             "baseline_model": "BASELINE.md section 3: read 105 B, total 201 B per 31-mer (8-pass LSD model) / "
-                              "ms_per_step (device) or ms_per_step + h2d_pinned_ms (e2e) / 8 TB/s"}
+                              "ms_per_step (device) or e2e_ms (end to end) / 8 TB/s"}
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 **base,
@@ -467,15 +620,13 @@ def main():
                                                  + (" (canonical)" if canonical else "")}),
             "data": data,
             "boundary": "value: device (sba resident in HBM at the start; sorted starts, sorted keys, first index "
-                        "+ multiplicity of every distinct k-mer resident in HBM at the end); value_e2e adds the H2D "
-                        "of the sba from pinned host memory (BASELINE.md section 3); the D2H of the sorted starts "
-                        "is reported apart (d2h_starts_ms)",
-            "value_e2e": round(value_e2e, 1),
-            **({} if pipe is None else {
-                "value_e2e_pipelined": round(n_units / (pipe["step_with_h2d_ms"] * 1e-3), 1),
-                "e2e_pipelined": dict(pipe, note="a stream of genomes: the next sba's pinned H2D runs on its own "
-                                                 "stream during this step's sort (wall time per step, best of 3)")}),
-            "h2d_pinned_ms": boundary["h2d_pinned_ms"], "d2h_starts_ms": boundary["d2h_starts_ms"],
+                        "+ multiplicity of every distinct k-mer resident in HBM at the end); value_e2e: one wall-clock "
+                        "interval from the caller's pageable numpy sba on the host to that product in HBM "
+                        "(gk_set_sequence's packed transfer + one step; BASELINE.md section 3); the D2H of the "
+                        "sorted starts is reported apart (d2h_starts_ms)",
+            "value_e2e": round(value_e2e, 1), "e2e_ms": round(e2e_ms, 2),
+            **({} if e2e is None else {"e2e": e2e}),
+            "set_sequence_ms": boundary["set_sequence_ms"], "d2h_starts_ms": boundary["d2h_starts_ms"],
             "self_check": f"{checked:,} sorted k-mers in windows re-checked against the sba bytes",
             "config": {"workload": workload,
                        "genome_bases": L, "k": k, "kmers": n_units, "unique_kmers": n_unique,
@@ -483,7 +634,7 @@ def main():
                                        f"key-range shards x{world}: whole sba per rank, 32 KiB RCCL all-reduce, "
                                        "no k-mer exchange" if args.exchange == "range" else
                                        f"position-range shards x{world} + 1 RCCL all-to-all of the k-mers"),
-                       "h2d_sba_pageable_ms": round(h2d_ms, 2), "transfers": boundary,
+                       "first_set_sequence_ms": round(h2d_ms, 2), "transfers": boundary,
                        "stages_ms_per_step": stages},
             "roofline": roofline,
             "cpu_baseline": cpu,

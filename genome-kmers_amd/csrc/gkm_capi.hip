@@ -386,6 +386,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    xfer_release(c);
     void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
                     c->dhist, c->mask, c->hmask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
@@ -436,18 +437,27 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     const uint64_t padded = ((len + kEncodeTile - 1) / kEncodeTile) * kEncodeTile + kSbaPad;
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->sba), &c->sba_cap, padded));
     GK_TRY_HIP(c, hipMemsetAsync(c->sba + len, GK_DOLLAR, c->sba_cap - len, c->stream));
-    GK_TRY_HIP(c, hipMemcpyAsync(c->sba, sba, len, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->seg), &c->seg_cap, 4 * nseg));
     GK_TRY_HIP(c, hipMemcpyAsync(c->seg, seg_starts, 4 * nseg, hipMemcpyHostToDevice, c->stream));
     c->sba_len = len;
     c->nseg = nseg;
     c->hseg.assign(seg_starts, seg_starts + nseg);
     c->max_seg_len = max_len;
-    uint32_t *d_flags = reinterpret_cast<uint32_t *>(c->scalars + 8);
-    GK_TRY_HIP(c, launch_alphabet(c, d_flags));
-    uint32_t h[2] = {0, 0};
-    GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
-    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    uint32_t h[2] = {0, 0};  // alphabet classes seen (alphabet_kernel's bits), '$' count
+    if (len >= packed_transfer_min()) {
+        // 2-bit packed over the link, census on the host, unpacked into the resident sba on the
+        // device (gkm_xfer.hip); the stream orders the sort's kernels behind the last unpack, so
+        // only the census is waited for
+        uint64_t dollars = 0;
+        if (int rc = packed_transfer(c, sba, len, &h[0], &dollars)) return rc;
+        h[1] = (uint32_t)dollars;
+    } else {
+        GK_TRY_HIP(c, hipMemcpyAsync(c->sba, sba, len, hipMemcpyHostToDevice, c->stream));
+        uint32_t *d_flags = reinterpret_cast<uint32_t *>(c->scalars + 8);
+        GK_TRY_HIP(c, launch_alphabet(c, d_flags));
+        GK_TRY_HIP(c, hipMemcpyAsync(h, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    }
     c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = c->canonical = false;
     c->enum_sorted = false;
     c->pk_fresh = false;
@@ -455,6 +465,16 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;
     c->internal_dollar = internal || (uint64_t)h[1] != nseg - 1;
+    return GK_OK;
+}
+
+extern "C" int gk_copy_sequence(gk_ctx *c, uint8_t *dst, uint64_t len) {
+    if (!c) return GK_E_ARG;
+    if (!c->sba) return fail(c, GK_E_STATE, "no sequence loaded");
+    if (len != c->sba_len) return fail(c, GK_E_ARG, "len differs from the loaded sequence length");
+    GK_TRY_HIP(c, hipSetDevice(c->device));
+    GK_TRY_HIP(c, hipMemcpyAsync(dst, c->sba, len, hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     return GK_OK;
 }
 

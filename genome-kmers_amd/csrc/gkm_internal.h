@@ -150,6 +150,13 @@ struct gk_ctx {
     // named, grow-only scratch buffers (MSD sort tables etc.)
     std::map<std::string, std::pair<void *, uint64_t>> scratch;
 
+    // packed sba transfer (gkm_xfer.hip): pinned host + device staging slots, copy stream, events
+    uint8_t *xfer_host = nullptr, *xfer_dev = nullptr;
+    hipStream_t xfer_stream = nullptr;
+    std::vector<hipEvent_t> xfer_ev;
+    int xfer_slots = 0;
+    uint64_t xfer_slot_bytes = 0;
+
     // profiling
     bool profile = false;
     std::vector<gkm::Timer> timers;
@@ -221,6 +228,12 @@ void timer_end(gk_ctx *c, int slot);
 void timer_units(gk_ctx *c, int slot, uint64_t units);
 int fail(gk_ctx *c, int code, const std::string &msg);
 int hip_fail(gk_ctx *c, hipError_t e, const char *where);
+
+// packed sba transfer (gkm_xfer.hip): inputs of >= packed_transfer_min() bytes go 2-bit packed;
+// the alphabet census (class bits as alphabet_kernel's, '$' count) is taken on the host
+uint64_t packed_transfer_min();
+int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars);
+void xfer_release(gk_ctx *c);
 
 // encode
 hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags);

@@ -1557,6 +1557,67 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
     }
 }
 
+// TIMING EXPERIMENTS ONLY (GKM_EXP_WAVECOPY=1, wrong output): the wave kernel's memory traffic
+// without its ranking -- the same list walk, loads (compact entries unpacked) and software
+// pipelining, then keys, starts and head flags stored straight from registers in load order.
+// Its time is the floor of msd_wave_kernel's bucket-granular access pattern.
+template <int I, int MINW>
+__global__ __launch_bounds__(64, MINW) void msd_wave_copy_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
+                                                           uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                           const uint32_t *v1, uint8_t *__restrict__ heads,
+                                                           const uint64_t *__restrict__ cpref,
+                                                           const uint8_t *__restrict__ cnd) {
+    const int lane = threadIdx.x;
+    uint32_t idx = blockIdx.x, lend = count, lstep = gridDim.x;
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+        const uint32_t x = blockIdx.x & 7;
+        idx = (uint32_t)((uint64_t)count * x / 8) + (blockIdx.x >> 3);
+        lend = (uint32_t)((uint64_t)count * (x + 1) / 8);
+        lstep = gridDim.x >> 3;
+    }
+    if (idx >= lend) return;
+    uint2 e, en;
+    uint64_t pf, pfn;
+    uint64_t key[I], a[I];
+    uint32_t val[I], b[I];
+    wave_entry(list, cpref, idx, e, pf);
+    wave_load<I>(e, pf, lane, k0, k1, v0, v1, cnd, a, b);
+    en = e;
+    pfn = pf;
+    if (idx + lstep < lend) wave_entry(list, cpref, idx + lstep, en, pfn);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (;;) {
+        const uint64_t st = e.x;
+        const uint32_t len = e.y >> 8;
+        const int hi0 = (e.y >> 1) & 127;
+        const bool cmp = (pf & kCompact) != 0;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            key[i] = cmp ? compact_key(pf, hi0, B, b[i] & 0xFFu, (uint32_t)(a[i] >> 32)) : a[i];
+            val[i] = cmp ? (uint32_t)a[i] : b[i];
+        }
+        uint2 enn = en;
+        uint64_t pfnn = pfn;
+        if (idx + 2 * lstep < lend) wave_entry(list, cpref, idx + 2 * lstep, enn, pfnn);
+        wave_load<I>(en, pfn, lane, k0, k1, v0, v1, cnd, a, b);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t j = min((uint32_t)(i * 64 + lane), len - 1);
+            gmem(k0)[st + j] = key[i];
+            gmem(v0)[st + j] = val[i];
+            gmem(heads)[st + j] = 1;
+        }
+        idx += lstep;
+        if (idx >= lend) break;
+        e = en;
+        pf = pfn;
+        en = enn;
+        pfn = pfnn;
+    }
+}
+
+static bool exp_wave_copy() { return std::getenv("GKM_EXP_WAVECOPY") != nullptr; }
+
 // one round's lists, copied to device memory for the wave kernels
 __global__ void lists_store_kernel(Lists L, Lists *__restrict__ dst) { *dst = L; }
 
@@ -2599,6 +2660,12 @@ struct MsdDriver {
             wave(msd_wave_kernel<4, kWaveOcc4, true, kWaveR4>, msd_wave_kernel<4, kWaveOcc4, false, kWaveR4>);
             break;
         case 1:
+            if (exp_wave_copy()) {  // timing experiments only: wrong output
+                hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8>),
+                                   grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
+                break;
+            }
             wave(msd_wave_kernel<8, kWaveOcc8, true, kWaveR8>, msd_wave_kernel<8, kWaveOcc8, false, kWaveR8>);
             break;
         case 2:

@@ -136,6 +136,7 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready) {
         }
         GK_TRY_HIP(c, e);
         timer_end(c, slot);
+        timer_units(c, slot, c->n);
         c->cur ^= 1;
         ++pass;
     }

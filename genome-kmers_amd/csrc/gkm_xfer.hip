@@ -1,0 +1,312 @@
+// gkm_xfer.hip -- host -> device transfer of the sequence byte array, 2-bit packed (gk_set_sequence).
+//
+// The reference hands the hot path a uint8 ASCII sba (sequence_collection.py:531-576, 663-726):
+// 1 byte per base, 3.1 GB for a human-sized genome, ~56 ms over PCIe at 55 GB/s -- 40 % of the
+// end-to-end time of a C3 sort.  Nearly every base is A, C, G or T, so the transfer ships 2 bits
+// per base where it can:
+//   host    the sba is cut into 64 KiB blocks and chunks of kBlocksPerChunk blocks.  Worker threads
+//           (up to 16) take chunks in order and write each into a pinned staging slot: a header
+//           (per block: payload offset | raw flag), then per block either the 16 KiB of 2-bit
+//           codes (every byte A/C/G/T: AVX2 compare + pack, 32 bases per step) or the raw bytes
+//           (anything else: '$' separators, N runs, IUPAC letters).  The same pass takes the
+//           alphabet census the reference's check needs (sequence_collection.py:441-458, 694-697):
+//           classes seen and '$' count -- no device pass over the sba afterwards.
+//   link    the caller's thread copies each finished chunk H2D on a copy stream, in chunk order,
+//           header + payload only (C3: 0.78 GB instead of 3.1 GB).
+//   device  unpack_chunk_kernel expands the chunk into the resident ASCII sba (LDS table, 16-B
+//           loads, 64-B stores) on the context's stream; the sort kernels read the sba as before.
+// Packing, copies and unpacking overlap: slots are recycled once the device has unpacked them.
+// Inputs below GKM_PACK_MIN bytes (default 16 MiB) are copied as they are (gkm_capi.hip).
+#include <immintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "gkm_internal.h"
+
+namespace gkm {
+
+constexpr uint64_t kXBlock = 64 * 1024;  // bytes of sba per block
+constexpr uint32_t kRawFlag = 0x80000000u;
+constexpr uint64_t kHeaderBytes = 1024;  // per slot: uint32 per block (<= 256 blocks)
+
+// ---------------------------------------------------------------------------------------------
+// device
+// ---------------------------------------------------------------------------------------------
+// packed byte b (bases 4j..4j+3 at bits 2i) -> 4 ASCII bytes, A0 C1 G2 T3
+__global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__restrict__ slot,
+                                                           uint8_t *__restrict__ dst, uint64_t chunk_len) {
+    __shared__ uint32_t s_lut[256];
+    const int t = threadIdx.x;
+    {
+        constexpr uint32_t kAscii = 0x54474341u;  // "ACGT" little-endian
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w |= ((kAscii >> (8 * ((t >> (2 * i)) & 3))) & 0xFFu) << (8 * i);
+        s_lut[t] = w;
+    }
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * kXBlock;
+    const uint64_t blen = chunk_len - b0 < kXBlock ? chunk_len - b0 : kXBlock;
+    const uint32_t hdr = reinterpret_cast<const uint32_t *>(slot)[blockIdx.x];
+    const uint8_t *src = slot + (hdr & ~kRawFlag);
+    uint8_t *out = dst + b0;
+    if (hdr & kRawFlag) {  // raw bytes: a straight copy, 16 B per lane where whole
+        const uint64_t q = blen / 16;
+        for (uint64_t i = t; i < q; i += 256)
+            reinterpret_cast<uint4 *>(out)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        for (uint64_t i = q * 16 + t; i < blen; i += 256) out[i] = src[i];
+        return;
+    }
+    // 16 packed bytes -> 64 bases per lane step
+    const uint64_t groups = (blen + 63) / 64;
+    for (uint64_t g = t; g < groups; g += 256) {
+        const uint4 p = reinterpret_cast<const uint4 *>(src)[g];
+        const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
+        uint32_t o[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[4 * k + j] = s_lut[(pw[k] >> (8 * j)) & 0xFFu];
+        if ((g + 1) * 64 <= blen) {
+            uint4 *q = reinterpret_cast<uint4 *>(out + g * 64);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        } else {  // the sba's last, partial group
+            for (uint64_t i = g * 64; i < blen; ++i) out[i] = (uint8_t)(o[(i - g * 64) >> 2] >> (8 * (i & 3)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host packing
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+// reference alphabet classes, as the device check (gkm_encode.hip c_class): 0 A/C/G/T/'$',
+// 1 other IUPAC letter, 2 not allowed
+struct ClassTable {
+    uint8_t c[256];
+    ClassTable() {
+        for (int i = 0; i < 256; ++i) c[i] = 2;
+        for (const char *p = "ABCDGHKMNRSTVWY"; *p; ++p) c[(uint8_t)*p] = 1;
+        c['A'] = c['C'] = c['G'] = c['T'] = c[GK_DOLLAR] = 0;
+    }
+};
+const ClassTable kClass;
+
+struct Census {
+    uint32_t cls_or = 0;
+    uint64_t dollars = 0;
+};
+
+inline uint32_t code_of(uint8_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
+
+// scalar: 2-bit codes of n bases (n % 4 == 0 except at the sba's end), false at the first non-ACGT
+bool pack_scalar(const uint8_t *s, uint64_t n, uint8_t *d) {
+    for (uint64_t i = 0; i < n; i += 4) {
+        uint32_t v = 0;
+        for (int j = 0; j < 4; ++j) {
+            const uint8_t c = i + j < n ? s[i + j] : 'A';
+            if (c != 'A' && c != 'C' && c != 'G' && c != 'T') return false;
+            v |= code_of(c) << (2 * j);
+        }
+        d[i / 4] = (uint8_t)v;
+    }
+    return true;
+}
+
+// AVX2: 32 bases per step -- four compares for the alphabet, code = ((c ^ c >> 1) >> 1) & 3, then
+// two multiply-adds fold 4 codes into a byte
+__attribute__((target("avx2"))) bool pack_avx2(const uint8_t *s, uint64_t n, uint8_t *d) {
+    const __m256i A = _mm256_set1_epi8('A'), C = _mm256_set1_epi8('C'), G = _mm256_set1_epi8('G'),
+                  T = _mm256_set1_epi8('T'), three = _mm256_set1_epi8(3);
+    const __m256i w1 = _mm256_set1_epi16(0x0401);   // bytes (1, 4): c0 + 4 c1
+    const __m256i w2 = _mm256_set1_epi32(0x00100001);  // words (1, 16): (c0 + 4 c1) + 16 (c2 + 4 c3)
+    const __m256i pick = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                          0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    uint64_t i = 0;
+    for (; i + 32 <= n; i += 32) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+        const __m256i ok = _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(v, A), _mm256_cmpeq_epi8(v, C)),
+                                           _mm256_or_si256(_mm256_cmpeq_epi8(v, G), _mm256_cmpeq_epi8(v, T)));
+        if ((uint32_t)_mm256_movemask_epi8(ok) != 0xFFFFFFFFu) return false;
+        const __m256i x = _mm256_xor_si256(v, _mm256_srli_epi16(v, 1));
+        const __m256i code = _mm256_and_si256(_mm256_srli_epi16(x, 1), three);
+        const __m256i pair = _mm256_maddubs_epi16(code, w1);
+        const __m256i quad = _mm256_madd_epi16(pair, w2);  // one byte value per dword
+        const __m256i b = _mm256_shuffle_epi8(quad, pick);  // 4 bytes at the bottom of each lane
+        const uint32_t lo = (uint32_t)_mm256_extract_epi32(b, 0), hi = (uint32_t)_mm256_extract_epi32(b, 4);
+        std::memcpy(d + i / 4, &lo, 4);
+        std::memcpy(d + i / 4 + 4, &hi, 4);
+    }
+    return pack_scalar(s + i, n - i, d + i / 4);
+}
+
+bool have_avx2() {
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+
+// one chunk into a staging slot; returns the bytes used (header + payloads)
+uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen) {
+    const uint32_t nb = (uint32_t)((len + kXBlock - 1) / kXBlock);
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(slot);
+    uint64_t off = kHeaderBytes;
+    const bool avx2 = have_avx2();
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint8_t *s = src + (uint64_t)b * kXBlock;
+        const uint64_t blen = std::min<uint64_t>(kXBlock, len - (uint64_t)b * kXBlock);
+        uint8_t *d = slot + off;
+        if (avx2 ? pack_avx2(s, blen, d) : pack_scalar(s, blen, d)) {
+            hdr[b] = (uint32_t)off;
+            off += ((blen + 63) / 64) * 16;  // whole 16-byte groups (the unpack reads uint4)
+            cen.cls_or |= 1u;
+            continue;
+        }
+        std::memcpy(d, s, blen);
+        for (uint64_t i = 0; i < blen; ++i) {
+            cen.cls_or |= 1u << kClass.c[s[i]];
+            cen.dollars += s[i] == GK_DOLLAR;
+        }
+        hdr[b] = (uint32_t)off | kRawFlag;
+        off += (blen + 15) & ~15ull;
+    }
+    return off;
+}
+
+uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
+}
+
+}  // namespace
+
+uint64_t packed_transfer_min() { return env_u64("GKM_PACK_MIN", 16ull << 20); }
+
+// staging slots of the context (pinned host + device), grown on demand and kept for later calls
+static hipError_t xfer_slots(gk_ctx *c, int slots, uint64_t slot_bytes) {
+    if (c->xfer_slots >= slots && c->xfer_slot_bytes >= slot_bytes) return hipSuccess;
+    xfer_release(c);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->xfer_host), (size_t)slots * slot_bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(&c->xfer_dev, (size_t)slots * slot_bytes);
+    if (e != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&c->xfer_stream, hipStreamNonBlocking)) != hipSuccess) return e;
+    c->xfer_ev.resize(2 * slots);
+    for (auto &ev : c->xfer_ev)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    c->xfer_slots = slots;
+    c->xfer_slot_bytes = slot_bytes;
+    return hipSuccess;
+}
+
+void xfer_release(gk_ctx *c) {
+    if (c->xfer_stream) hipStreamSynchronize(c->xfer_stream);
+    for (auto &ev : c->xfer_ev)
+        if (ev) hipEventDestroy(ev);
+    c->xfer_ev.clear();
+    if (c->xfer_stream) hipStreamDestroy(c->xfer_stream);
+    if (c->xfer_host) hipHostFree(c->xfer_host);
+    if (c->xfer_dev) hipFree(c->xfer_dev);
+    c->xfer_stream = nullptr;
+    c->xfer_host = nullptr;
+    c->xfer_dev = nullptr;
+    c->xfer_slots = 0;
+    c->xfer_slot_bytes = 0;
+}
+
+// sba[0, len) -> c->sba through the packed pipeline; *cls_or / *dollars: the alphabet census
+int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars) {
+    const uint64_t bpc = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_PACK_BLOCKS", 128), 256));
+    const uint64_t chunk = bpc * kXBlock;
+    const uint64_t C = (len + chunk - 1) / chunk;
+    unsigned hw = std::thread::hardware_concurrency();
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_XFER_THREADS", std::min(16u, hw ? hw : 1u)), C));
+    const int S = (int)std::min<uint64_t>(C, std::max(2, 2 * T));
+    GK_TRY_HIP(c, xfer_slots(c, S, kHeaderBytes + chunk + 16));
+    hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
+
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int64_t> used(C, -1);  // bytes of a packed chunk, -1 while packing
+    uint64_t freed = std::min<uint64_t>(S, C);  // chunks < freed may use their slot
+    bool abort = false;
+    std::atomic<uint64_t> next{0};
+    std::atomic<uint32_t> cls{0};
+    std::atomic<uint64_t> dol{0};
+
+    auto worker = [&]() {
+        Census cen;
+        for (;;) {
+            const uint64_t k = next.fetch_add(1);
+            if (k >= C) break;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return abort || k < freed; });
+                if (abort) break;
+            }
+            const uint64_t at = k * chunk, m = std::min(chunk, len - at);
+            const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (k % S) * c->xfer_slot_bytes, cen);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                used[k] = (int64_t)u;
+            }
+            cv.notify_all();
+        }
+        cls.fetch_or(cen.cls_or);
+        dol.fetch_add(cen.dollars);
+    };
+    std::vector<std::thread> pool;
+    for (int i = 0; i < T; ++i) pool.emplace_back(worker);
+
+    hipError_t err = hipSuccess;
+    for (uint64_t k = 0; k < C && err == hipSuccess; ++k) {
+        int64_t u;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return used[k] >= 0; });
+            u = used[k];
+        }
+        const int s = (int)(k % S);
+        const uint64_t m = std::min(chunk, len - k * chunk);
+        uint8_t *ds = c->xfer_dev + (uint64_t)s * c->xfer_slot_bytes;
+        err = hipMemcpyAsync(ds, c->xfer_host + (uint64_t)s * c->xfer_slot_bytes, (size_t)u, hipMemcpyHostToDevice,
+                             c->xfer_stream);
+        if (err == hipSuccess) err = hipEventRecord(ev_copy[s], c->xfer_stream);
+        if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, ev_copy[s], 0);
+        if (err == hipSuccess) {
+            hipLaunchKernelGGL(unpack_chunk_kernel, dim3((unsigned)((m + kXBlock - 1) / kXBlock)), dim3(256), 0,
+                               c->stream, ds, c->sba + k * chunk, m);
+            err = hipGetLastError();
+        }
+        if (err == hipSuccess) err = hipEventRecord(ev_done[s], c->stream);
+        // the slot chunk k + 1 will take (chunk k + 1 - S's) is free once the device has unpacked it
+        if (err == hipSuccess && k + 1 >= (uint64_t)S && k + 1 < C) {
+            err = hipEventSynchronize(ev_done[(k + 1) % S]);
+            if (err == hipSuccess) {
+                std::lock_guard<std::mutex> lk(mu);
+                freed = k + 2;  // chunk k + 1 may now fill its slot
+            }
+            cv.notify_all();
+        }
+    }
+    if (err != hipSuccess) {
+        std::lock_guard<std::mutex> lk(mu);
+        abort = true;
+    }
+    cv.notify_all();
+    for (auto &th : pool) th.join();
+    if (err != hipSuccess) return hip_fail(c, err, "packed sba transfer");
+    *cls_or = cls.load();
+    *dollars = dol.load();
+    return GK_OK;
+}
+
+}  // namespace gkm

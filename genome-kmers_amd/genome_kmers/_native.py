@@ -56,6 +56,7 @@ EXPORTED = (
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range", "gk_shard_class_b", "gk_shard_class_b_copy",
     "gk_shard_sort_range_b", "gk_rank_mode", "gk_reference_random_bases",
+    "gk_copy_sequence",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
@@ -145,6 +146,7 @@ _SIGS = {
     "gk_copy_strands": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
     "gk_rank_mode": ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "gk_reference_random_bases": ([_U8P, ctypes.c_uint64, ctypes.c_uint32], ctypes.c_int),
+    "gk_copy_sequence": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
 }
 
 
@@ -238,7 +240,12 @@ def reference_random_bases(n: int, seed: int) -> np.ndarray:
     """The reference's profiling genome (profiling.get_random_seq after np.random.seed(seed)) as n
     ASCII bytes, from libgkm's host MT19937 (gk_reference_random_bases)."""
     out = np.empty(n, dtype=np.uint8)
-    rc = load_library().gk_reference_random_bases(_ptr(out, ctypes.c_uint8), n, int(seed) & 0xFFFFFFFF)
+    lib = load_library()
+    if os.environ.get("GKM_LIB") and not hasattr(lib, "gk_reference_random_bases"):
+        # an older build under A/B (tuning only): the in-tree library's generator
+        lib = ctypes.CDLL(str(Path(__file__).with_name("libgkm.so")))
+        lib.gk_reference_random_bases.argtypes = _SIGS["gk_reference_random_bases"][0]
+    rc = lib.gk_reference_random_bases(_ptr(out, ctypes.c_uint8), n, int(seed) & 0xFFFFFFFF)
     if rc != GK_OK:
         raise GkError(rc, "gk_reference_random_bases failed")
     return out
@@ -310,6 +317,12 @@ class Engine:
         self._check(self.lib.gk_enumerate(self.ctx, min_kmer_len, ctypes.byref(n)))
         self.n = n.value
         return self.n
+
+    def copy_sequence(self, length: int) -> np.ndarray:
+        """The device-resident sba (gk_copy_sequence)."""
+        out = np.empty(length, dtype=np.uint8)
+        self._check(self.lib.gk_copy_sequence(self.ctx, _ptr(out, ctypes.c_uint8), length))
+        return out
 
     def set_start_indices(self, starts: np.ndarray, min_kmer_len: int):
         arr = np.ascontiguousarray(starts, dtype=np.uint32)

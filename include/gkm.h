@@ -117,6 +117,11 @@ int gk_rank_mode(gk_ctx *ctx, int mode, int *active);
 /* ---- input contract ------------------------------------------------------------------------- */
 /* sba: ASCII bases, contigs joined by '$' (36), no trailing '$'; seg_starts: ascending uint32. */
 int gk_set_sequence(gk_ctx *ctx, const uint8_t *sba, uint64_t len, const uint32_t *seg_starts, uint64_t nseg);
+/* The transfer: inputs of >= 16 MiB (GKM_PACK_MIN) cross the link 2-bit packed wherever a 64 KiB
+ * block is pure A/C/G/T and raw elsewhere, packed by up to 16 host threads (AVX2) and unpacked
+ * into the resident ASCII sba on the device (gkm_xfer.hip); the alphabet check runs on the host
+ * during the packing.  gk_copy_sequence reads the resident sba back (len = the loaded length). */
+int gk_copy_sequence(gk_ctx *ctx, uint8_t *dst, uint64_t len);
 /* 1 if the loaded sba holds only {A,C,G,T,$} (2-bit keys), 0 otherwise (4-bit keys) */
 int gk_alphabet_is_acgt(gk_ctx *ctx, int *is_acgt);
 

@@ -94,6 +94,23 @@ __global__ __launch_bounds__(256) void rank_scatter_kernel(const uint32_t *__res
         R[vals[i]] = gstart[gid[i] - 1] + 1;
 }
 
+// Groups of the current order that may still split: more than one member, and members longer than
+// the h symbols the keys hold.  Members of a group share their first h symbols, so a group whose
+// first member's suffix (to '$' / the end) is at most h long holds equal k-mers and is final --
+// the '$'-terminated tails shared by several contigs, which no doubling round can separate.
+__global__ __launch_bounds__(256) void unresolved_groups_kernel(const uint32_t *__restrict__ vals,
+                                                                const uint32_t *__restrict__ gstart, uint64_t G,
+                                                                uint64_t n, const uint32_t *__restrict__ seg,
+                                                                uint32_t nseg, uint64_t L, uint64_t h,
+                                                                uint32_t *__restrict__ count) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = gstart[g], e = g + 1 < G ? gstart[g + 1] : n;
+        if (e - b < 2) continue;
+        const uint64_t p = vals[b];
+        if (seg_end_of(seg, nseg, L, p) - p + 1 > h) atomicAdd(count, 1u);
+    }
+}
+
 // key = rank[p] << 32 | (p + o <= seg_end(p) ? rank[p + o] : 0)
 __global__ __launch_bounds__(256) void pair_keys_kernel(const uint32_t *__restrict__ vals,
                                                         const uint32_t *__restrict__ R,
@@ -694,6 +711,16 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
         GK_TRY_HIP(c, select_flags(c, c->flags, n1, c->idx_b, &G));
         if (G == n1) break;                          // all distinct
         if (!bounded && h >= c->max_seg_len) break;  // every suffix ends within h symbols
+        {  // every tied group already holds equal k-mers (shared contig tails): done
+            uint32_t *d_cnt = reinterpret_cast<uint32_t *>(c->scalars + 20), cnt = 0;
+            GK_TRY_HIP(c, hipMemsetAsync(d_cnt, 0, 4, c->stream));
+            hipLaunchKernelGGL(unresolved_groups_kernel, dim3(grid_of(G)), dim3(256), 0, c->stream, c->vals[c->cur],
+                               c->idx_b, G, n1, c->seg, (uint32_t)c->nseg, L, h, d_cnt);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, c->stream));
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+            if (cnt == 0) break;
+        }
         GK_TRY_HIP(c, scan_flags_inclusive(c, c->flags, n1, c->idx_a));
         GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
         GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[c->cur], c->idx_a, c->idx_b, n1, c->ranks));

@@ -122,29 +122,38 @@ bool pack_scalar(const uint8_t *s, uint64_t n, uint8_t *d) {
     return true;
 }
 
-// AVX2: 32 bases per step -- four compares for the alphabet, code = ((c ^ c >> 1) >> 1) & 3, then
-// two multiply-adds fold 4 codes into a byte
+// AVX2: 64 bases -> 16 bytes per step.  Alphabet: four compares per 32 bytes; code =
+// ((c ^ c >> 1) >> 1) & 3 (A0 C1 G2 T3); two multiply-adds fold 4 codes into the low byte of a
+// dword, two saturating packs and one dword permute put the 16 bytes in order, one 16-byte store
+// (the staging slots are pinned memory: whole 16-byte stores).
+__attribute__((target("avx2"))) static inline __m256i avx2_codes(__m256i v) {
+    const __m256i x = _mm256_xor_si256(v, _mm256_srli_epi16(v, 1));
+    return _mm256_and_si256(_mm256_srli_epi16(x, 1), _mm256_set1_epi8(3));
+}
+
+__attribute__((target("avx2"))) static inline uint32_t avx2_acgt_mask(__m256i v) {
+    const __m256i ok = _mm256_or_si256(
+        _mm256_or_si256(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('A')), _mm256_cmpeq_epi8(v, _mm256_set1_epi8('C'))),
+        _mm256_or_si256(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('G')), _mm256_cmpeq_epi8(v, _mm256_set1_epi8('T'))));
+    return (uint32_t)_mm256_movemask_epi8(ok);
+}
+
 __attribute__((target("avx2"))) bool pack_avx2(const uint8_t *s, uint64_t n, uint8_t *d) {
-    const __m256i A = _mm256_set1_epi8('A'), C = _mm256_set1_epi8('C'), G = _mm256_set1_epi8('G'),
-                  T = _mm256_set1_epi8('T'), three = _mm256_set1_epi8(3);
-    const __m256i w1 = _mm256_set1_epi16(0x0401);   // bytes (1, 4): c0 + 4 c1
+    const __m256i w1 = _mm256_set1_epi16(0x0401);      // bytes (1, 4): c0 + 4 c1
     const __m256i w2 = _mm256_set1_epi32(0x00100001);  // words (1, 16): (c0 + 4 c1) + 16 (c2 + 4 c3)
-    const __m256i pick = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
-                                          0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const __m256i order = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
     uint64_t i = 0;
-    for (; i + 32 <= n; i += 32) {
-        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
-        const __m256i ok = _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(v, A), _mm256_cmpeq_epi8(v, C)),
-                                           _mm256_or_si256(_mm256_cmpeq_epi8(v, G), _mm256_cmpeq_epi8(v, T)));
-        if ((uint32_t)_mm256_movemask_epi8(ok) != 0xFFFFFFFFu) return false;
-        const __m256i x = _mm256_xor_si256(v, _mm256_srli_epi16(v, 1));
-        const __m256i code = _mm256_and_si256(_mm256_srli_epi16(x, 1), three);
-        const __m256i pair = _mm256_maddubs_epi16(code, w1);
-        const __m256i quad = _mm256_madd_epi16(pair, w2);  // one byte value per dword
-        const __m256i b = _mm256_shuffle_epi8(quad, pick);  // 4 bytes at the bottom of each lane
-        const uint32_t lo = (uint32_t)_mm256_extract_epi32(b, 0), hi = (uint32_t)_mm256_extract_epi32(b, 4);
-        std::memcpy(d + i / 4, &lo, 4);
-        std::memcpy(d + i / 4 + 4, &hi, 4);
+    for (; i + 64 <= n; i += 64) {
+        const __m256i v0 = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+        const __m256i v1 = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
+        if ((avx2_acgt_mask(v0) & avx2_acgt_mask(v1)) != 0xFFFFFFFFu) return false;
+        const __m256i q0 = _mm256_madd_epi16(_mm256_maddubs_epi16(avx2_codes(v0), w1), w2);
+        const __m256i q1 = _mm256_madd_epi16(_mm256_maddubs_epi16(avx2_codes(v1), w1), w2);
+        // per 128-bit lane: packus_epi32 -> (q0 lane, q1 lane) words; packus_epi16 -> their bytes
+        // (twice); dwords 0, 4, 1, 5 are then q0[0..3], q0[4..7], q1[0..3], q1[4..7]
+        const __m256i b = _mm256_packus_epi16(_mm256_packus_epi32(q0, q1), _mm256_setzero_si256());
+        const __m256i o = _mm256_permutevar8x32_epi32(b, order);
+        _mm_storeu_si128(reinterpret_cast<__m128i *>(d + i / 4), _mm256_castsi256_si128(o));
     }
     return pack_scalar(s + i, n - i, d + i / 4);
 }

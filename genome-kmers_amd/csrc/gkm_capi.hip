@@ -262,22 +262,24 @@ extern "C" int gk_device_count(int *count) {
 // gkm_partition.h): it relies on the LDS applying the same-address lanes of one wave instruction in
 // increasing lane order.  That is how gfx950 behaves (tools/lds_rank_probe.hip: no exception in
 // 4e10 lane-ranks), not an ISA guarantee, so it is checked once per device and process against a
-// ballot-match ground truth over every digit space the partitions rank in -- 1024, 512, 256, 128,
-// 64, 16, 4 and 1 digits (the wave kernels' 10 / 9 / 8 bits, the level passes' 8, L0's 7) with
-// per-wave counter arrays of 1024 words like the wave kernels', 8 items per trial, lanes sitting
-// out, every CU busy.  Where it does not hold, the partitions switch to ballot-match ranking
-// (rank_ballot): the same ranks from ballots alone.  The kernel checks that path as well.
+// ballot-match ground truth over every digit space the partitions rank in -- 2048, 1024, 512, 256,
+// 128, 64, 16, 4 and 1 digits (the wide L0's 11 bits, the wave kernels' 10 / 9 / 8, the level
+// passes' 8, L0's 7) with per-wave counter arrays of 2048 words, in both counter forms (u32 words,
+// and the u16 halves of rank_atomic16), 8 items per trial, lanes sitting out, every CU busy.  Where
+// it does not hold, the partitions switch to ballot-match ranking (rank_ballot): the same ranks
+// from ballots alone.  The kernel checks that path as well.
 __global__ __launch_bounds__(256) void lds_rank_check_kernel(uint32_t trials, unsigned long long *bad) {
-    __shared__ uint32_t s_cnt[4][1024];
+    __shared__ uint32_t s_cnt[4][2048];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t *cnt = s_cnt[wave];
     unsigned long long nb = 0;
     for (uint32_t t = 0; t < trials; ++t) {
-        constexpr uint32_t kMasks[8] = {1023u, 511u, 255u, 127u, 63u, 15u, 3u, 0u};
-        const uint32_t dmask = kMasks[t & 7];
-        const bool ballot = (t >> 3) & 1;  // every other round of 8: the fallback ranking
+        constexpr uint32_t kMasks[9] = {2047u, 1023u, 511u, 255u, 127u, 63u, 15u, 3u, 0u};
+        const uint32_t dmask = kMasks[t % 9];
+        const uint32_t form = (t / 9) & 3;  // 0 atomic u32, 1 ballot u32, 2 atomic u16, 3 ballot u16
+        const bool ballot = form & 1;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) cnt[u * 64 + lane] = 0;
+        for (int u = 0; u < 32; ++u) cnt[u * 64 + lane] = 0;
         uint32_t dd[8], got[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -287,7 +289,11 @@ __global__ __launch_bounds__(256) void lds_rank_check_kernel(uint32_t trials, un
             x ^= x >> 12;
             dd[i] = x & dmask;
             const bool valid = ((x >> 20) & 7u) != 0;  // some lanes sit out
-            got[i] = ballot ? rank_ballot(cnt, dd[i], valid) : (valid ? atomicAdd(&cnt[dd[i]], 1u) : 0u);
+            const uint32_t d = dd[i], sh = (d & 1u) << 4;
+            if (form == 0) got[i] = valid ? atomicAdd(&cnt[d], 1u) : 0u;
+            else if (form == 1) got[i] = rank_ballot<11, false>(cnt, d, valid);
+            else if (form == 2) got[i] = valid ? (atomicAdd(&cnt[d >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+            else got[i] = rank_ballot<11, true>(cnt, d, valid);
             if (!valid) got[i] = ~0u;
         }
 #pragma unroll
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(256) void lds_rank_check_kernel(uint32_t trials, un
             for (int j = 0; j <= i; ++j) {
                 uint64_t m = __ballot(got[j] != ~0u);
 #pragma unroll
-                for (int b = 0; b < 10; ++b) {
+                for (int b = 0; b < 11; ++b) {
                     const uint64_t x = __ballot((dd[j] >> b) & 1u);
                     m &= ((dd[i] >> b) & 1u) ? x : ~x;
                 }
@@ -340,7 +346,7 @@ static int lds_rank_check(int device) {
         if (hipMalloc(&d, 8) != hipSuccess) return GK_E_HIP;
         hipError_t e = hipMemset(d, 0, 8);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(lds_rank_check_kernel, dim3(2048), dim3(256), 0, 0, 48u, d);
+            hipLaunchKernelGGL(lds_rank_check_kernel, dim3(2048), dim3(256), 0, 0, 72u, d);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
@@ -354,7 +360,7 @@ static int lds_rank_check(int device) {
         st.checked = h == 0 ? 1 : -1;
         if (h)
             std::fprintf(stderr, "libgkm: device %d: a returning LDS atomic did not apply same-address lanes in "
-                                 "lane order (%llu of ~2.5e8 ranks differ); the partitions rank by ballots instead\n",
+                                 "lane order (%llu of ~1.9e8 ranks differ); the partitions rank by ballots instead\n",
                          device, h);
     }
     const int want = (st.checked < 0 || st.forced || env_force_ballot()) ? 1 : 0;

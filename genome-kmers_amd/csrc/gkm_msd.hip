@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "gkm_canon.h"
 #include "gkm_internal.h"
@@ -30,13 +31,17 @@ namespace gkm {
 constexpr int kGR = 8;                  // global digit bits
 constexpr int kGRadix = 1 << kGR;
 constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
+// wide L0 (msd0_wide_kernel): 11-bit digits over the same 18,432-position tile, 512 threads x 36
+constexpr int kWideL0 = 11, kWT = 512, kWI = 36;
 constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk (GKM_TEST_CHUNK_TILES overrides: tests only)
 constexpr int kBT = 512, kBI = 8, kBR = 8;    // block-local: 512 threads x 8 keys, 8-bit digit
-constexpr int kBlockMax = kBT * kBI;    // 4096
-// local finishing classes by bucket size: one wave x 4 or 8 keys (msd_wave_kernel), 256 threads x
-// 4 or 16 keys (msd_local_kernel)
-constexpr int kLocal = 5;                // 4 = tiny (<= kTiny elements: one thread per bucket)
+constexpr int kBT2 = 1024;                    // big block-local: 1024 threads x 8 keys
+constexpr int kBlockMax = kBT2 * kBI;   // 8192: larger buckets take another global level
+// local finishing classes by bucket size: one wave x 4, 8 or 16 keys (msd_wave_kernel), 512
+// threads x 8 keys (msd_local_kernel, <= 4096), 4 = tiny (<= kTiny elements: one thread per
+// bucket), 5 = 1024 threads x 8 keys (<= 8192: the buckets an 11-bit L0 + one level leave at C3)
+constexpr int kLocal = 6;
 constexpr int kTiny = 8;
 constexpr int kSmall = 24;
 // waves per SIMD the wave-local kernels' registers are capped for (msd_wave_kernel<I, W, .>); the
@@ -542,6 +547,147 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     }
 }
 
+// Wide L0 partition (R = 10 or 11 bits; 2-bit keys of one word, forward, no profile): the
+// position-staged, software-pipelined scheme of msd0_pipe_kernel with a digit space the 7-bit one
+// cannot hold -- per-wave u16 counters, two per word (rank_atomic16), K = RADIX / T digits per
+// thread in the scan, K tile offsets per thread.  With the level pass behind it, 11 + 8 bits leave
+// the C3 buckets at ~5.9 K keys, finished in one block-local round (three passes instead of
+// four global ones plus the wave-local round).
+template <int T, int I, int R, bool ND>
+__global__ __launch_bounds__(T) void msd0_wide_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
+                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                      uint32_t ntiles, uint64_t sink, NextDigits nd) {
+    constexpr int TILE = T * I;
+    static_assert(TILE < 65536, "tile positions are staged as u16");
+    constexpr int RADIX = 1 << R;
+    constexpr int NW = T / 64;
+    constexpr int K = RADIX / T;  // digits per thread in the scan
+    static_assert(RADIX % T == 0 && K >= 1, "whole digits per thread");
+    static_assert(I * 64 < 65536, "per-wave counts fit 16 bits");
+    constexpr int G_TOP = 1, G_SCAN = 2;
+    constexpr int G_RANK = I - G_TOP - G_SCAN - 2 > 0 ? I - G_TOP - G_SCAN - 2 : 0;
+    using P = L0Pack<2, TILE>;
+    __shared__ uint16_t s_pos[2][TILE + 2];          // positions in digit order (slot TILE: sink)
+    __shared__ uint64_t s_code[2][P::kCodeWords];   // this tile's and the staged tile's codes
+    __shared__ uint32_t s_dol[P::kGroups];
+    __shared__ uint32_t s_wc[NW * RADIX / 2];        // per-wave u16 digit counters
+    __shared__ uint32_t s_toff[2][RADIX];
+    __shared__ uint32_t s_start[RADIX + 1];
+    __shared__ uint32_t s_wsum[NW];
+    uint16_t *const s_wc16 = reinterpret_cast<uint16_t *>(s_wc);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < TILE + 2; i += T) s_pos[1][i] = 0;
+    lds_barrier();
+    const TileWalk walk(ntiles);
+    uint64_t rr[L0Units<2, TILE, T>::kPer];
+    uint32_t toff[K];
+    auto load = [&](uint32_t t) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) toff[k] = tile_off[(uint64_t)t * RADIX + tid * K + k];
+        l0_load<2, TILE, T>(a, a.lo + (uint64_t)t * TILE, rr);
+    };
+    uint32_t pcnt = 0;
+    uint64_t pP0 = 0;
+    int b = 0;
+    auto store_group = [&](int g) {
+        const uint32_t s = min((uint32_t)(tid + g * T), pcnt - 1);
+        const uint32_t p = s_pos[b ^ 1][s];
+        const uint64_t key = l0_key<2>(s_code[b ^ 1], p, a.total_bits);
+        const uint64_t o = pcnt ? (uint64_t)(s_toff[b ^ 1][dg_of(key, d0)] + s) : sink;
+        kout[o] = key;
+        vout[o] = (uint32_t)(pP0 + p);
+        if (ND) nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (walk.first < walk.end) load(walk.first);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        uint32_t *wc = s_wc + wave * (RADIX / 2);
+#pragma unroll
+        for (int u = 0; u < RADIX / 2 / 64; ++u) wc[u * 64 + lane] = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) s_toff[b][tid * K + k] = toff[k];
+        l0_pack<2, TILE, T>(rr, s_code[b], s_dol, nullptr, 0, a.pk_code != nullptr);
+        load(min(t + walk.step, walk.end - 1));
+#pragma unroll
+        for (int g = 0; g < G_TOP; ++g) store_group(g);
+        lds_barrier();  // packed codes visible
+        const uint64_t P0 = a.lo + (uint64_t)t * TILE;
+        uint32_t anystop = 0;
+#pragma unroll
+        for (int j = 0; j < (P::kGroups + 63) / 64; ++j)
+            anystop |= s_dol[min((uint32_t)(j * 64 + lane), (uint32_t)P::kGroups - 1)];
+        const bool clean = __ballot(anystop != 0) == 0 && P0 + TILE <= a.hi;
+        uint32_t dr[I];  // per item: digit | rank << R, all ones when not valid
+        uint32_t p0 = wave * (I * 64) + lane;
+        asm volatile("" : "+v"(p0));
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t p = p0 + i * 64;
+            const bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
+            const uint32_t dig = dg_of(l0_key<2>(s_code[b], p, a.total_bits), d0);
+            const uint32_t rk = rank_atomic16<R>(wc, dig, valid);
+            dr[i] = valid ? dig | (rk << R) : ~0u;
+            if (i < G_RANK) store_group(G_TOP + i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();  // ranks final
+        // per-digit totals over the waves -> per-wave exclusive prefixes (u16), block scan of the
+        // digit totals (thread tid owns digits tid K .. tid K + K - 1)
+        uint32_t tot[K], sum = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int d = tid * K + k;
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t v = s_wc16[w * RADIX + d];
+                s_wc16[w * RADIX + d] = (uint16_t)run;
+                run += v;
+            }
+            tot[k] = run;
+            sum += run;
+        }
+        const uint32_t incl = wave_incl_scan(sum);
+        if (lane == 63) s_wsum[wave] = incl;
+#pragma unroll
+        for (int g = 0; g < G_SCAN; ++g) store_group(G_TOP + G_RANK + g);
+        lds_barrier();
+        {
+            uint32_t pre = 0;
+            for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+            uint32_t run = pre + incl - sum;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int d = tid * K + k;
+                s_start[d] = run;
+                s_toff[b][d] -= run;
+                run += tot[k];
+            }
+            if (tid == T - 1) s_start[RADIX] = run;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const bool valid = dr[i] != ~0u;
+            const uint32_t dg = dr[i] & (RADIX - 1);
+            const uint32_t sl = valid ? s_start[dg] + s_wc16[wave * RADIX + dg] + (dr[i] >> R) : (uint32_t)TILE;
+            s_pos[b][sl] = (uint16_t)(p0 + i * 64);
+        }
+        const uint32_t cnt = s_start[RADIX];
+#pragma unroll
+        for (int g = G_TOP + G_RANK + G_SCAN; g < I; ++g) store_group(g);
+        pcnt = cnt;
+        pP0 = P0;
+        lds_barrier();  // staging complete; counters, codes and the previous staging read
+        b ^= 1;
+    }
+    if (walk.first < walk.end) {
+#pragma unroll
+        for (int g = 0; g < I; ++g) store_group(g);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Key-range shard select (gk_shard_sort_range)
 // ---------------------------------------------------------------------------------------------
@@ -780,12 +926,18 @@ __global__ __launch_bounds__(256) void pack2_kernel(const uint8_t *__restrict__ 
 // column-wise segmented exclusive scan of per-tile digit histograms -> per-tile digit offsets
 // (one thread per digit: blockDim = RADIX)
 // ---------------------------------------------------------------------------------------------
+// Column scans of per-tile digit histograms.  Threads per block: min(RADIX, 1024); wider digit
+// spaces (the wide L0's 2048) take blockIdx.y for the digit block (chunk sums, tile apply) or
+// several consecutive digits per thread (the bucket scan).
 template <int RADIX>
-__global__ __launch_bounds__(RADIX) void chunk_sum_kernel(const uint32_t *__restrict__ tile_hist,
+constexpr int scan_threads() { return RADIX < 1024 ? RADIX : 1024; }
+
+template <int RADIX>
+__global__ __launch_bounds__(scan_threads<RADIX>()) void chunk_sum_kernel(const uint32_t *__restrict__ tile_hist,
                                                           const uint32_t *__restrict__ c_first,
                                                           const uint32_t *__restrict__ c_ntiles,
                                                           uint32_t *__restrict__ chunk_hist) {
-    const int d = threadIdx.x;
+    const int d = blockIdx.y * scan_threads<RADIX>() + threadIdx.x;
     const uint64_t f = c_first[blockIdx.x];
     const uint32_t nt = c_ntiles[blockIdx.x];
     uint32_t acc = 0;
@@ -803,22 +955,29 @@ __global__ __launch_bounds__(RADIX) void chunk_sum_kernel(const uint32_t *__rest
 
 // one block per bucket: chunk bases within the bucket, digit bases, digit counts
 template <int RADIX>
-__global__ __launch_bounds__(RADIX) void seg_scan_kernel(uint32_t *__restrict__ chunk_hist,
+__global__ __launch_bounds__(scan_threads<RADIX>()) void seg_scan_kernel(uint32_t *__restrict__ chunk_hist,
                                                          const uint32_t *__restrict__ s_cfirst,
                                                          const uint32_t *__restrict__ s_nchunks,
                                                          const uint32_t *__restrict__ s_start,
                                                          uint32_t *__restrict__ seg_base, uint32_t *__restrict__ seg_cnt) {
-    __shared__ uint32_t s_wsum[RADIX / 64];
-    const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
+    constexpr int TH = scan_threads<RADIX>(), DPT = RADIX / TH;  // DPT consecutive digits per thread
+    __shared__ uint32_t s_wsum[TH / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint64_t cf = s_cfirst[blockIdx.x];
     const uint32_t nc = s_nchunks[blockIdx.x];
-    uint32_t run = 0;
-    for (uint32_t i = 0; i < nc; ++i) {
-        const uint32_t v = chunk_hist[(cf + i) * RADIX + d];
-        chunk_hist[(cf + i) * RADIX + d] = run;
-        run += v;
+    uint32_t run[DPT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = t * DPT + k;
+        run[k] = 0;
+        for (uint32_t i = 0; i < nc; ++i) {
+            const uint32_t v = chunk_hist[(cf + i) * RADIX + d];
+            chunk_hist[(cf + i) * RADIX + d] = run[k];
+            run[k] += v;
+        }
+        sum += run[k];
     }
-    uint32_t incl = run;
+    uint32_t incl = sum;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(incl, off);
@@ -828,18 +987,23 @@ __global__ __launch_bounds__(RADIX) void seg_scan_kernel(uint32_t *__restrict__ 
     __syncthreads();
     uint32_t pre = 0;
     for (int w = 0; w < wave; ++w) pre += s_wsum[w];
-    const uint32_t base = s_start[blockIdx.x] + pre + incl - run;
-    seg_base[(uint64_t)blockIdx.x * RADIX + d] = base;
-    seg_cnt[(uint64_t)blockIdx.x * RADIX + d] = run;
-    for (uint32_t c = 0; c < nc; ++c) chunk_hist[(cf + c) * RADIX + d] += base;
+    uint32_t base = s_start[blockIdx.x] + pre + incl - sum;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = t * DPT + k;
+        seg_base[(uint64_t)blockIdx.x * RADIX + d] = base;
+        seg_cnt[(uint64_t)blockIdx.x * RADIX + d] = run[k];
+        for (uint32_t c = 0; c < nc; ++c) chunk_hist[(cf + c) * RADIX + d] += base;
+        base += run[k];
+    }
 }
 
 template <int RADIX>
-__global__ __launch_bounds__(RADIX) void tile_apply_kernel(uint32_t *__restrict__ tile_hist,
+__global__ __launch_bounds__(scan_threads<RADIX>()) void tile_apply_kernel(uint32_t *__restrict__ tile_hist,
                                                            const uint32_t *__restrict__ c_first,
                                                            const uint32_t *__restrict__ c_ntiles,
                                                            const uint32_t *__restrict__ chunk_base) {
-    const int d = threadIdx.x;
+    const int d = blockIdx.y * scan_threads<RADIX>() + threadIdx.x;
     const uint64_t f = c_first[blockIdx.x];
     const uint32_t nt = c_ntiles[blockIdx.x];
     uint32_t run = chunk_base[(uint64_t)blockIdx.x * RADIX + d];
@@ -874,7 +1038,7 @@ __device__ __forceinline__ uint32_t wave_append(bool flag, uint32_t *counter, in
 }
 
 // list counters (device, one array): next global level, done, then the local classes
-enum { kCtrBig = 0, kCtrDone = 1, kCtrLoc = 2, kLists = kCtrLoc + kLocal, kCtrN = 8 };
+enum { kCtrBig = 0, kCtrDone = 1, kCtrLoc = 2, kLists = kCtrLoc + kLocal, kCtrN = 8 + 2 };
 
 struct Lists {
     uint32_t *nb_start, *nb_len;                 // buckets for the next global level
@@ -899,7 +1063,7 @@ __device__ __forceinline__ uint64_t compact_key(uint64_t pref, int hi, int B, ui
 
 // local class of a bucket of <= kBlockMax elements
 __host__ __device__ constexpr uint32_t local_cap(int cls) {
-    return cls == 0 ? 256 : cls == 1 ? 512 : cls == 2 ? 1024 : cls == 3 ? 4096 : kTiny;
+    return cls == 0 ? 256 : cls == 1 ? 512 : cls == 2 ? 1024 : cls == 3 ? 4096 : cls == 5 ? 8192 : kTiny;
 }
 
 // list of a live sub-bucket of `size` elements (kCtr* index)
@@ -907,7 +1071,8 @@ __device__ __forceinline__ int list_of(uint32_t size, int hi, int B, bool allow_
     if (hi >= B) return kCtrDone;
     if (size > (uint32_t)kBlockMax && allow_big) return kCtrBig;
     if (size <= (uint32_t)kTiny) return kCtrLoc + 4;
-    return kCtrLoc + (size <= local_cap(0) ? 0 : size <= local_cap(1) ? 1 : size <= local_cap(2) ? 2 : 3);
+    return kCtrLoc + (size <= local_cap(0) ? 0 : size <= local_cap(1) ? 1 : size <= local_cap(2) ? 2
+                      : size <= local_cap(3) ? 3 : 5);
 }
 
 // entry `at` of list l for a sub-bucket
@@ -2000,14 +2165,15 @@ static int pack_sequence(gk_ctx *c, const uint64_t **code, const uint32_t **dol)
     return GK_OK;
 }
 
-static const char *kLocPrefName[kLocal] = {"locp0", "locp1", "locp2", "locp3", "locp4"};
+static const char *kLocPrefName[kLocal] = {"locp0", "locp1", "locp2", "locp3", "locp4", "locp5"};
 static const char *kLocName[kLocal][2] = {{"loc0a", "loc0b"}, {"loc1a", "loc1b"}, {"loc2a", "loc2b"},
-                                          {"loc3a", "loc3b"}, {"loc4a", "loc4b"}};
+                                          {"loc3a", "loc3b"}, {"loc4a", "loc4b"}, {"loc5a", "loc5b"}};
 static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_r"},
                                            {"msd_local_wave8", "msd_local_wave8_r"},
                                            {"msd_local_wave16", "msd_local_wave16_r"},
                                            {"msd_local_block16", "msd_local_block16_r"},
-                                           {"msd_local_tiny", "msd_local_tiny_r"}};
+                                           {"msd_local_tiny", "msd_local_tiny_r"},
+                                           {"msd_local_block32", "msd_local_block32_r"}};
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
 static const char *kPassNamesC[] = {"msd_pass_l0c", "msd_pass_l1c", "msd_pass_l2c", "msd_pass_l3c",
@@ -2061,6 +2227,15 @@ struct MsdDriver {
         if (const char *e = std::getenv("GKM_TEST_CHUNK_TILES")) ctiles = (uint32_t)std::max(1, std::atoi(e));
     }
 
+    // the whole sort of forward 2-bit one-word keys (msd_sort's phase 0): an 11-bit L0
+    // (msd0_wide_kernel) when GKM_WIDE_L0=1 (A/B), so that 11 + 8 bits leave C3-sized buckets for
+    // one block-local round
+    void enable_wide_l0() {
+        const char *e = std::getenv("GKM_WIDE_L0");  // (read per sort: tests flip it)
+        const bool want = e && *e && std::strcmp(e, "0") != 0;
+        if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8) wsched[0] = kWideL0;
+    }
+
     // level digit widths "w0,w1,w2,..." (the last one repeats).  Default 7,8,8,...: for 2-bit
     // keys a 7-bit L0 is ~10% faster than an 8-bit one (longer runs per tile), and after 23 bits
     // the C3 buckets (~370) fit the one-wave finishing kernel; 4-bit keys keep an 8-bit L0.
@@ -2083,9 +2258,9 @@ struct MsdDriver {
     Lists lists(int g, int bigsel) {
         // prefixes are recorded by classify (generation 0); re-listed entries carry full keys
         return Lists{big_start[bigsel], big_len[bigsel], dn_start, dn_len, dn_par,
-                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g], loc[4][g]}, big_pref[bigsel],
+                     {loc[0][g], loc[1][g], loc[2][g], loc[3][g], loc[4][g], loc[5][g]}, big_pref[bigsel],
                      {g ? nullptr : loc_pref[0], g ? nullptr : loc_pref[1], g ? nullptr : loc_pref[2],
-                      g ? nullptr : loc_pref[3], g ? nullptr : loc_pref[4]}};
+                      g ? nullptr : loc_pref[3], g ? nullptr : loc_pref[4], g ? nullptr : loc_pref[5]}};
     }
 
     int init(uint64_t n_) {
@@ -2121,11 +2296,12 @@ struct MsdDriver {
     template <int RADIX>
     void scan_launch(uint64_t C, const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start,
                      uint64_t nseg) {
-        hipLaunchKernelGGL(chunk_sum_kernel<RADIX>, dim3((unsigned)C), dim3(RADIX), 0, c->stream, tile_hist, c_first,
-                           c_ntiles, chunk_hist);
-        hipLaunchKernelGGL(seg_scan_kernel<RADIX>, dim3((unsigned)nseg), dim3(RADIX), 0, c->stream, chunk_hist,
+        constexpr int TH = scan_threads<RADIX>();
+        hipLaunchKernelGGL(chunk_sum_kernel<RADIX>, dim3((unsigned)C, RADIX / TH), dim3(TH), 0, c->stream, tile_hist,
+                           c_first, c_ntiles, chunk_hist);
+        hipLaunchKernelGGL(seg_scan_kernel<RADIX>, dim3((unsigned)nseg), dim3(TH), 0, c->stream, chunk_hist,
                            s_cfirst, s_nchunks, s_start, seg_base, seg_cnt);
-        hipLaunchKernelGGL(tile_apply_kernel<RADIX>, dim3((unsigned)C), dim3(RADIX), 0, c->stream, tile_hist,
+        hipLaunchKernelGGL(tile_apply_kernel<RADIX>, dim3((unsigned)C, RADIX / TH), dim3(TH), 0, c->stream, tile_hist,
                            c_first, c_ntiles, chunk_hist);
     }
 
@@ -2134,6 +2310,7 @@ struct MsdDriver {
         timer_begin(c, "msd_scan", &slot);
         if (R == 8) scan_launch<256>(C, s_cfirst, s_nchunks, s_start, nseg);
         else if (R == 7) scan_launch<128>(C, s_cfirst, s_nchunks, s_start, nseg);
+        else if (R == kWideL0) scan_launch<1 << kWideL0>(C, s_cfirst, s_nchunks, s_start, nseg);
         else scan_launch<64>(C, s_cfirst, s_nchunks, s_start, nseg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
@@ -2142,12 +2319,13 @@ struct MsdDriver {
 
     // tile / chunk tables: device buffers sized for T tiles, C chunks, nseg buckets
     int tables(uint64_t T, uint64_t C, uint64_t nseg) {
-        GK_TRY_HIP(c, scratch(c, "tile_hist", T * kGRadix, &tile_hist));
-        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * kGRadix, &chunk_hist));
+        const uint64_t rad = std::max(kGRadix, 1 << wsched[0]);  // the wide L0's digits
+        GK_TRY_HIP(c, scratch(c, "tile_hist", T * rad, &tile_hist));
+        GK_TRY_HIP(c, scratch(c, "chunk_hist", C * rad, &chunk_hist));
         GK_TRY_HIP(c, scratch(c, "c_first", C, &c_first));
         GK_TRY_HIP(c, scratch(c, "c_ntiles", C, &c_ntiles));
-        GK_TRY_HIP(c, scratch(c, "seg_base", nseg * kGRadix, &seg_base));
-        GK_TRY_HIP(c, scratch(c, "seg_cnt", nseg * kGRadix, &seg_cnt));
+        GK_TRY_HIP(c, scratch(c, "seg_base", nseg * rad, &seg_base));
+        GK_TRY_HIP(c, scratch(c, "seg_cnt", nseg * rad, &seg_cnt));
         return GK_OK;
     }
 
@@ -2210,6 +2388,26 @@ struct MsdDriver {
     template <bool CANON>
     void l0_dispatch_c(bool count, int w0, bool nd_, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout,
                        uint32_t *vout, uint32_t nt, uint64_t sink, const NextDigits &ndg) {
+        if (ks.bits == 2 && !CANON && w0 == kWideL0) {  // enable_wide_l0: forward 2-bit one-word sorts
+            if (count) {
+                static int per_cu = 0;
+                if (!per_cu &&
+                    (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         &per_cu, (const void *)msd0_count_kernel<2, kPT / 4, kP0I * 4, kWideL0, false>, kPT / 4,
+                         0) != hipSuccess ||
+                     per_cu < 1))
+                    per_cu = 1;
+                hipLaunchKernelGGL((msd0_count_kernel<2, kPT / 4, kP0I * 4, kWideL0, false>),
+                                   dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kPT / 4), 0, c->stream, a, d0,
+                                   tile_hist, nt0);
+            } else if (nd_)
+                hipLaunchKernelGGL((msd0_wide_kernel<kWT, kWI, kWideL0, true>), dim3(pgrid), dim3(kWT), 0, c->stream,
+                                   a, d0, tile_hist, kout, vout, nt, sink, ndg);
+            else
+                hipLaunchKernelGGL((msd0_wide_kernel<kWT, kWI, kWideL0, false>), dim3(pgrid), dim3(kWT), 0,
+                                   c->stream, a, d0, tile_hist, kout, vout, nt, sink, ndg);
+            return;
+        }
         if (ks.bits == 2 && w0 == 7) {
             if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else l0_launch<2, 7, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
@@ -2409,8 +2607,8 @@ struct MsdDriver {
         if (rc != GK_OK) return rc;
         GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
         // the next level's digit bytes, unless this level's sub-buckets will most likely all be
-        // local (mean under kBlockMax / 8); a next level then counts from the keys
-        nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax / 8;
+        // local (mean under kBlockMax); a next level then counts from the keys
+        nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax;
         // compact output when this level's sub-buckets will most likely all be finished locally
         // and the key bits below the next 8-bit digit fit a u32: (low bits, start) as one u64 and
         // the digit byte -- 9 B per element out instead of 12 -- and the finishing kernels read 9 B
@@ -2677,6 +2875,11 @@ struct MsdDriver {
                                cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
                                (uint32_t)kSmall, wkeys, ci);  // the block class keeps kSmall: 96 measured slower (A/B)
             break;
+        case 5:
+            hipLaunchKernelGGL((msd_local_kernel<kBT2, kBI, kBR>),
+                               grid((const void *)msd_local_kernel<kBT2, kBI, kBR>, kBT2), dim3(kBT2), 0, c->stream,
+                               lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, (uint32_t)kSmall, wkeys, ci);
+            break;
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
                                v1, heads, wkeys, ci, B);
@@ -2766,6 +2969,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     const int nphase = (ks.symbols + spw - 1) / spw;
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
+    if (nphase == 1) d.enable_wide_l0();
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);

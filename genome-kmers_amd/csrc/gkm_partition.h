@@ -78,20 +78,28 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // rank_mode_*); read once per kernel into an SGPR, the test is one scalar branch per item.
 static __constant__ int g_rank_ballot = 0;
 
-// Ballot-match rank: the valid lanes with this lane's digit (digits of up to 10 bits) by 10
+// Ballot-match rank: the valid lanes with this lane's digit (digits of up to DB bits) by DB
 // ballots, the rank among them by mbcnt, and one returning atomic per distinct digit, from the
 // lowest such lane (distinct addresses: lane order cannot matter), whose pre-add count is then
-// broadcast to its peers.
+// broadcast to its peers.  P16: the counters are u16 halves of u32 words (rank_atomic16).
+template <int DB = 10, bool P16 = false>
 __device__ __forceinline__ uint32_t rank_ballot(uint32_t *wc, uint32_t d, bool valid) {
     uint64_t m = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 10; ++b) {
+    for (int b = 0; b < DB; ++b) {
         const uint64_t x = __ballot((d >> b) & 1u);
         m &= ((d >> b) & 1u) ? x : ~x;
     }
     const uint32_t below = lanes_below(m);
     uint32_t old = 0;
-    if (valid && below == 0) old = atomicAdd(&wc[d], (uint32_t)__popcll(m));
+    if (valid && below == 0) {
+        if (P16) {
+            const uint32_t sh = (d & 1u) << 4;
+            old = (atomicAdd(&wc[d >> 1], (uint32_t)__popcll(m) << sh) >> sh) & 0xFFFFu;
+        } else {
+            old = atomicAdd(&wc[d], (uint32_t)__popcll(m));
+        }
+    }
     const int leader = m ? __builtin_ctzll(m) : 0;
     old = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old);
     return valid ? old + below : 0u;
@@ -100,6 +108,18 @@ __device__ __forceinline__ uint32_t rank_ballot(uint32_t *wc, uint32_t d, bool v
 __device__ __forceinline__ uint32_t rank_atomic(uint32_t *wc, uint32_t d, bool valid) {
     if (__builtin_expect(g_rank_ballot != 0, 0)) return rank_ballot(wc, d, valid);
     return valid ? atomicAdd(&wc[d], 1u) : 0u;
+}
+
+// The same rank with 16-bit counters, two digits per u32 word (digit d: half d & 1 of word d >> 1),
+// for digit spaces whose per-wave u32 counters would not fit the LDS (2^11 digits x 16 waves).
+// Counts stay below 2^16 (a wave ranks at most 64 I items), so an add never carries into the
+// other half; the lane-order property is the same one (same-address lanes of one instruction,
+// whatever they add), checked by lds_rank_check in this form too.
+template <int DB = 11>
+__device__ __forceinline__ uint32_t rank_atomic16(uint32_t *wc, uint32_t d, bool valid) {
+    if (__builtin_expect(g_rank_ballot != 0, 0)) return rank_ballot<DB, true>(wc, d, valid);
+    const uint32_t sh = (d & 1u) << 4;
+    return valid ? (atomicAdd(&wc[d >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
 }
 
 // host: switch this code object's partitions to the ballot-match ranking (or back)

@@ -739,3 +739,30 @@ def test_split_keys_with_homopolymers(k, canonical):
             b[a:a + k + 40] = bytes([letter]) * (k + 40)
         out.append((name, b.decode()))
     _split_keys_check(out, k, canonical)
+
+
+# the 11-bit L0 (msd0_wide_kernel, GKM_WIDE_L0=1) with its 1024-thread block-local finishing class:
+# random, repeat-heavy and multi-contig inputs, bit-exact against the oracle
+@pytest.mark.parametrize("case", ["random", "block32", "repeats", "contigs", "homopolymer"])
+def test_wide_l0_vs_oracle(case, monkeypatch):
+    monkeypatch.setenv("GKM_WIDE_L0", "1")
+    rng = np.random.default_rng(21)
+    if case == "random":
+        seqs = random_genome(rng, [1_500_000])
+    elif case == "block32":  # ~5.9 K k-mers per 11-bit L0 bucket: the 1024-thread block class
+        seqs = random_genome(rng, [12_000_000])
+    elif case == "repeats":
+        rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 9000).astype(np.uint8)
+        seqs = random_genome(rng, [600_000, 300_000], repeat=rep, copies=9)
+    elif case == "contigs":
+        seqs = random_genome(rng, [40_000, 31, 250_000, 32, 99_999, 64])
+    else:
+        seqs = [("a", "A" * 40_000 + "C" * 9_000), ("b", "AC" * 30_000)]
+    oracle_check(seqs, 31, 31)
+
+
+@pytest.mark.parametrize("k", [12, 20, 32])
+def test_wide_l0_k_sweep_vs_oracle(k, monkeypatch):
+    monkeypatch.setenv("GKM_WIDE_L0", "1")
+    rng = np.random.default_rng(k)
+    oracle_check(random_genome(rng, [700_000, 12_345]), k, k)

@@ -107,6 +107,15 @@ __global__ __launch_bounds__(256) void alphabet_kernel(const uint8_t *__restrict
     }
 }
 
+hipError_t launch_alphabet_range(gk_ctx *c, const uint8_t *p, uint64_t len, uint32_t *d_flags) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    const uint64_t chunks = len / 16 + 1;
+    const int grid = (int)std::min<uint64_t>((chunks + 255) / 256, 2048);
+    hipLaunchKernelGGL(alphabet_kernel, dim3(grid), dim3(256), 0, c->stream, p, len, d_flags);
+    return hipGetLastError();
+}
+
 hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags) {
     hipError_t e = init_tables();
     if (e != hipSuccess) return e;

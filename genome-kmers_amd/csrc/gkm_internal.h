@@ -152,7 +152,7 @@ struct gk_ctx {
 
     // packed sba transfer (gkm_xfer.hip): pinned host + device staging slots, copy stream, events
     uint8_t *xfer_host = nullptr, *xfer_dev = nullptr;
-    hipStream_t xfer_stream = nullptr;
+    hipStream_t xfer_stream = nullptr, xfer_raw_stream = nullptr;
     std::vector<hipEvent_t> xfer_ev;
     int xfer_slots = 0;
     uint64_t xfer_slot_bytes = 0;
@@ -237,6 +237,8 @@ void xfer_release(gk_ctx *c);
 
 // encode
 hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags);
+// the same census over [p, p + len) of the resident sba, accumulated into d_flags (not zeroed)
+hipError_t launch_alphabet_range(gk_ctx *c, const uint8_t *p, uint64_t len, uint32_t *d_flags);
 hipError_t launch_enumerate(gk_ctx *c, uint32_t min_k, uint32_t *out);
 hipError_t launch_validate_starts(gk_ctx *c, const uint32_t *starts, uint64_t n, uint32_t min_k, uint32_t *d_bad);
 hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys, uint32_t *vals, uint32_t *hist);

@@ -36,7 +36,9 @@ constexpr int kWideL0 = 11, kWT = 512, kWI = 36;
 constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk (GKM_TEST_CHUNK_TILES overrides: tests only)
 constexpr int kBT = 512, kBI = 8, kBR = 8;    // block-local: 512 threads x 8 keys, 8-bit digit
-constexpr int kBT2 = 1024;                    // big block-local: 1024 threads x 8 keys
+constexpr int kBT2 = 1024, kBR2 = 10;         // big block-local: 1024 threads x 8 keys, 10-bit digit
+                                              // (~5.9 K keys over 1024 digits: sub-buckets of ~6,
+                                              // finished by rank-by-count, few re-listed)
 constexpr int kBlockMax = kBT2 * kBI;   // 8192: larger buckets take another global level
 // local finishing classes by bucket size: one wave x 4, 8 or 16 keys (msd_wave_kernel), 512
 // threads x 8 keys (msd_local_kernel, <= 4096), 4 = tiny (<= kTiny elements: one thread per
@@ -2875,11 +2877,22 @@ struct MsdDriver {
                                cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip,
                                (uint32_t)kSmall, wkeys, ci);  // the block class keeps kSmall: 96 measured slower (A/B)
             break;
-        case 5:
-            hipLaunchKernelGGL((msd_local_kernel<kBT2, kBI, kBR>),
-                               grid((const void *)msd_local_kernel<kBT2, kBI, kBR>, kBT2), dim3(kBT2), 0, c->stream,
-                               lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, (uint32_t)kSmall, wkeys, ci);
+        case 5: {
+            // (A/B: GKM_BLOCK32_T512=1 -- 512 threads x 16 keys: half the per-wave counters to
+            // zero and scan per bucket, half the waves)
+            static const bool t512 = std::getenv("GKM_BLOCK32_T512") != nullptr;
+            if (t512)
+                hipLaunchKernelGGL((msd_local_kernel<kBT, 2 * kBI, kBR2>),
+                                   grid((const void *)msd_local_kernel<kBT, 2 * kBI, kBR2>, kBT), dim3(kBT), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, (uint32_t)kSmall,
+                                   wkeys, ci);
+            else
+                hipLaunchKernelGGL((msd_local_kernel<kBT2, kBI, kBR2>),
+                                   grid((const void *)msd_local_kernel<kBT2, kBI, kBR2>, kBT2), dim3(kBT2), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, nl, ctr, skip, (uint32_t)kSmall,
+                                   wkeys, ci);
             break;
+        }
         default:
             hipLaunchKernelGGL(msd_tiny_kernel, dim3((cnt + 255) / 256), dim3(256), 0, c->stream, lst, cnt, k0, v0, k1,
                                v1, heads, wkeys, ci, B);

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -35,6 +36,7 @@ namespace gkm {
 constexpr uint64_t kXBlock = 64 * 1024;  // bytes of sba per block
 constexpr uint32_t kRawFlag = 0x80000000u;
 constexpr uint64_t kHeaderBytes = 1024;  // per slot: uint32 per block (<= 256 blocks)
+constexpr int kRawDepth = 4;             // raw chunk copies in flight (pinned sources)
 
 // ---------------------------------------------------------------------------------------------
 // device
@@ -208,7 +210,9 @@ static hipError_t xfer_slots(gk_ctx *c, int slots, uint64_t slot_bytes) {
     e = hipMalloc(&c->xfer_dev, (size_t)slots * slot_bytes);
     if (e != hipSuccess) return e;
     if ((e = hipStreamCreateWithFlags(&c->xfer_stream, hipStreamNonBlocking)) != hipSuccess) return e;
-    c->xfer_ev.resize(2 * slots);
+    if ((e = hipStreamCreateWithFlags(&c->xfer_raw_stream, hipStreamNonBlocking)) != hipSuccess) return e;
+    // per slot: copy landed, slot unpacked; then kRawDepth raw-copy events
+    c->xfer_ev.resize(2 * slots + kRawDepth);
     for (auto &ev : c->xfer_ev)
         if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
     c->xfer_slots = slots;
@@ -218,20 +222,42 @@ static hipError_t xfer_slots(gk_ctx *c, int slots, uint64_t slot_bytes) {
 
 void xfer_release(gk_ctx *c) {
     if (c->xfer_stream) hipStreamSynchronize(c->xfer_stream);
+    if (c->xfer_raw_stream) hipStreamSynchronize(c->xfer_raw_stream);
     for (auto &ev : c->xfer_ev)
         if (ev) hipEventDestroy(ev);
     c->xfer_ev.clear();
     if (c->xfer_stream) hipStreamDestroy(c->xfer_stream);
+    if (c->xfer_raw_stream) hipStreamDestroy(c->xfer_raw_stream);
     if (c->xfer_host) hipHostFree(c->xfer_host);
     if (c->xfer_dev) hipFree(c->xfer_dev);
-    c->xfer_stream = nullptr;
+    c->xfer_stream = c->xfer_raw_stream = nullptr;
     c->xfer_host = nullptr;
     c->xfer_dev = nullptr;
     c->xfer_slots = 0;
     c->xfer_slot_bytes = 0;
 }
 
-// sba[0, len) -> c->sba through the packed pipeline; *cls_or / *dollars: the alphabet census
+// is p (page-locked) host memory the DMA engines can read directly?
+static bool host_pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // a pageable pointer reports an error on some runtimes: clear it
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// sba[0, len) -> c->sba.  Chunks are independent (each writes its own range of the resident sba),
+// so they are issued in whatever order they are ready:
+//   packed  worker threads claim chunks from the front, pack each into a free staging slot and
+//           queue it; the caller's thread copies queued slots H2D (xfer_stream) and unpacks them on
+//           the context's stream, and recycles a slot once its unpack has run;
+//   raw     when the caller's buffer is pinned, the caller's thread also claims chunks from the
+//           back and DMAs them as they are, straight into the resident sba (xfer_raw_stream, at
+//           most kRawDepth in flight) -- the link carries raw bytes while the CPUs pack, and the
+//           two ends meet where packing and copying balance; raw chunks get their alphabet census
+//           on the device (launch_alphabet_range).
+// *cls_or / *dollars: the census (host part + device part).
 int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars) {
     const uint64_t bpc = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_PACK_BLOCKS", 128), 256));
     const uint64_t chunk = bpc * kXBlock;
@@ -239,33 +265,47 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     unsigned hw = std::thread::hardware_concurrency();
     const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_XFER_THREADS", std::min(16u, hw ? hw : 1u)), C));
     const int S = (int)std::min<uint64_t>(C, std::max(2, 2 * T));
+    const bool hybrid = env_u64("GKM_XFER_HYBRID", 1) != 0 && host_pinned(sba);
     GK_TRY_HIP(c, xfer_slots(c, S, kHeaderBytes + chunk + 16));
     hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
+    hipEvent_t *ev_raw = c->xfer_ev.data() + 2 * S;
+    uint32_t *d_census = reinterpret_cast<uint32_t *>(c->scalars + 24);
+    if (hybrid) GK_TRY_HIP(c, hipMemsetAsync(d_census, 0, 8, c->stream));
+    // the copy streams write the resident sba and the staging slots outside the context's stream:
+    // everything queued before (an earlier sort reading the sba, an earlier transfer's unpacks)
+    // has to be done first
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
 
     std::mutex mu;
     std::condition_variable cv;
-    std::vector<int64_t> used(C, -1);  // bytes of a packed chunk, -1 while packing
-    uint64_t freed = std::min<uint64_t>(S, C);  // chunks < freed may use their slot
+    uint64_t front = 0, back = C;            // unclaimed chunks: [front, back)
+    std::vector<int> free_slots;             // slots ready to be packed into
+    std::vector<std::pair<uint64_t, int>> ready;  // (chunk, slot) packed, not yet issued
+    std::vector<uint64_t> used(S, 0);        // bytes of the packed chunk in each slot
     bool abort = false;
-    std::atomic<uint64_t> next{0};
+    for (int i = 0; i < S; ++i) free_slots.push_back(i);
     std::atomic<uint32_t> cls{0};
     std::atomic<uint64_t> dol{0};
 
     auto worker = [&]() {
         Census cen;
         for (;;) {
-            const uint64_t k = next.fetch_add(1);
-            if (k >= C) break;
+            uint64_t k;
+            int slot;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return abort || k < freed; });
-                if (abort) break;
+                cv.wait(lk, [&] { return abort || front >= back || !free_slots.empty(); });
+                if (abort || front >= back) break;
+                k = front++;
+                slot = free_slots.back();
+                free_slots.pop_back();
             }
             const uint64_t at = k * chunk, m = std::min(chunk, len - at);
-            const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (k % S) * c->xfer_slot_bytes, cen);
+            const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (uint64_t)slot * c->xfer_slot_bytes, cen);
             {
                 std::lock_guard<std::mutex> lk(mu);
-                used[k] = (int64_t)u;
+                used[slot] = u;
+                ready.emplace_back(k, slot);
             }
             cv.notify_all();
         }
@@ -276,45 +316,100 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     for (int i = 0; i < T; ++i) pool.emplace_back(worker);
 
     hipError_t err = hipSuccess;
-    for (uint64_t k = 0; k < C && err == hipSuccess; ++k) {
-        int64_t u;
+    std::vector<int> inflight;           // slots issued, unpack not yet known to have run
+    std::vector<char> raw_busy(kRawDepth, 0);
+    uint64_t issued = 0, raw_chunks = 0;  // chunks handed to the device (packed + raw)
+    while (err == hipSuccess && issued < C) {
+        bool progress = false;
+        std::vector<std::pair<uint64_t, int>> batch;
         {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return used[k] >= 0; });
-            u = used[k];
+            std::lock_guard<std::mutex> lk(mu);
+            batch.swap(ready);
         }
-        const int s = (int)(k % S);
-        const uint64_t m = std::min(chunk, len - k * chunk);
-        uint8_t *ds = c->xfer_dev + (uint64_t)s * c->xfer_slot_bytes;
-        err = hipMemcpyAsync(ds, c->xfer_host + (uint64_t)s * c->xfer_slot_bytes, (size_t)u, hipMemcpyHostToDevice,
-                             c->xfer_stream);
-        if (err == hipSuccess) err = hipEventRecord(ev_copy[s], c->xfer_stream);
-        if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, ev_copy[s], 0);
-        if (err == hipSuccess) {
-            hipLaunchKernelGGL(unpack_chunk_kernel, dim3((unsigned)((m + kXBlock - 1) / kXBlock)), dim3(256), 0,
-                               c->stream, ds, c->sba + k * chunk, m);
-            err = hipGetLastError();
-        }
-        if (err == hipSuccess) err = hipEventRecord(ev_done[s], c->stream);
-        // the slot chunk k + 1 will take (chunk k + 1 - S's) is free once the device has unpacked it
-        if (err == hipSuccess && k + 1 >= (uint64_t)S && k + 1 < C) {
-            err = hipEventSynchronize(ev_done[(k + 1) % S]);
+        for (auto &kr : batch) {  // packed chunks: copy, then unpack on the context's stream
+            const uint64_t k = kr.first;
+            const int s = kr.second;
+            const uint64_t m = std::min(chunk, len - k * chunk);
+            uint8_t *ds = c->xfer_dev + (uint64_t)s * c->xfer_slot_bytes;
+            err = hipMemcpyAsync(ds, c->xfer_host + (uint64_t)s * c->xfer_slot_bytes, (size_t)used[s],
+                                 hipMemcpyHostToDevice, c->xfer_stream);
+            if (err == hipSuccess) err = hipEventRecord(ev_copy[s], c->xfer_stream);
+            if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, ev_copy[s], 0);
             if (err == hipSuccess) {
-                std::lock_guard<std::mutex> lk(mu);
-                freed = k + 2;  // chunk k + 1 may now fill its slot
+                hipLaunchKernelGGL(unpack_chunk_kernel, dim3((unsigned)((m + kXBlock - 1) / kXBlock)), dim3(256), 0,
+                                   c->stream, ds, c->sba + k * chunk, m);
+                err = hipGetLastError();
             }
-            cv.notify_all();
+            if (err == hipSuccess) err = hipEventRecord(ev_done[s], c->stream);
+            if (err != hipSuccess) break;
+            inflight.push_back(s);
+            ++issued;
+            progress = true;
+        }
+        // recycle slots whose unpack has run
+        for (size_t i = 0; i < inflight.size() && err == hipSuccess;) {
+            const hipError_t q = hipEventQuery(ev_done[inflight[i]]);
+            if (q == hipSuccess) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    free_slots.push_back(inflight[i]);
+                }
+                cv.notify_all();
+                inflight[i] = inflight.back();
+                inflight.pop_back();
+                progress = true;
+            } else if (q == hipErrorNotReady) {
+                ++i;
+            } else {
+                err = q;
+            }
+        }
+        // raw chunks from the back while the raw copy queue has room
+        for (int r = 0; hybrid && r < kRawDepth && err == hipSuccess; ++r) {
+            if (raw_busy[r]) {
+                const hipError_t q = hipEventQuery(ev_raw[r]);
+                if (q == hipErrorNotReady) continue;
+                if (q != hipSuccess) {
+                    err = q;
+                    break;
+                }
+                raw_busy[r] = 0;
+            }
+            uint64_t k;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (front >= back) break;
+                k = --back;
+            }
+            const uint64_t at = k * chunk, m = std::min(chunk, len - at);
+            err = hipMemcpyAsync(c->sba + at, sba + at, (size_t)m, hipMemcpyHostToDevice, c->xfer_raw_stream);
+            if (err == hipSuccess) err = hipEventRecord(ev_raw[r], c->xfer_raw_stream);
+            if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, ev_raw[r], 0);
+            if (err == hipSuccess) err = launch_alphabet_range(c, c->sba + at, m, d_census);
+            raw_busy[r] = 1;
+            ++issued;
+            ++raw_chunks;
+            progress = true;
+        }
+        if (!progress && issued < C) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait_for(lk, std::chrono::microseconds(50), [&] { return !ready.empty(); });
         }
     }
-    if (err != hipSuccess) {
+    {
         std::lock_guard<std::mutex> lk(mu);
-        abort = true;
+        if (err != hipSuccess) abort = true;
     }
     cv.notify_all();
     for (auto &th : pool) th.join();
     if (err != hipSuccess) return hip_fail(c, err, "packed sba transfer");
-    *cls_or = cls.load();
-    *dollars = dol.load();
+    uint32_t cen[2] = {0, 0};
+    if (hybrid && raw_chunks) {  // the device census of the raw chunks (waits for them to land)
+        GK_TRY_HIP(c, hipMemcpyAsync(cen, d_census, 8, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    *cls_or = cls.load() | cen[0];
+    *dollars = dol.load() + cen[1];
     return GK_OK;
 }
 

@@ -122,3 +122,59 @@ def test_default_threshold_large_input():
     eng.set_sequence(sba, np.zeros(1, dtype=np.uint32))
     np.testing.assert_array_equal(eng.copy_sequence(len(sba)), sba)
     assert not eng.is_acgt()
+
+
+def pinned_copy(a):
+    import torch
+
+    t = torch.empty(len(a), dtype=torch.uint8).pin_memory()
+    t.numpy()[:] = a
+    return t  # keep the tensor alive: its numpy view is the pinned buffer
+
+
+@pytest.mark.parametrize("runs,iupac", [(0, 0), (3, 5)])
+@pytest.mark.parametrize("blocks,threads", [(1, 1), (2, 4)])
+def test_pinned_source_hybrid_transfer(runs, iupac, blocks, threads, monkeypatch):
+    # a pinned source: chunks go packed from the front and raw (DMA, device census) from the back
+    rng = np.random.default_rng(17 + runs)
+    sba, seg = genome(rng, 40 * B + 1234, contigs=4, n_runs=runs, iupac=iupac)
+    t = pinned_copy(sba)
+    packed = load(t.numpy(), seg, monkeypatch, True, blocks, threads)
+    np.testing.assert_array_equal(packed.copy_sequence(len(sba)), sba)
+    plain = load(sba, seg, monkeypatch, False)
+    assert packed.is_acgt() == plain.is_acgt()
+    outs = []
+    for eng in (packed, plain):
+        n = eng.enumerate(15)
+        eng.sort(15)
+        outs.append(eng.copy_starts(np.empty(n, dtype=np.uint32)))
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("where", [0, 20 * B + 3, 40 * B - 1])
+def test_pinned_source_rejects_bad_bytes_anywhere(where, monkeypatch):
+    rng = np.random.default_rng(where)
+    sba, seg = genome(rng, 40 * B)
+    sba[where] = ord("x")
+    t = pinned_copy(sba)
+    with pytest.raises(_native.GkError) as ei:
+        load(t.numpy(), seg, monkeypatch, True, 1, 2)
+    assert ei.value.code == _native.GK_E_ALPHABET
+
+
+def test_set_sequence_waits_for_an_earlier_sort(monkeypatch):
+    # a new sequence must not overwrite the resident one under a sort still queued on the stream
+    rng = np.random.default_rng(3)
+    a, seg = genome(rng, 30 * B)
+    b, _ = genome(rng, 30 * B)
+    eng = load(a, seg, monkeypatch, True)
+    n = eng.enumerate(21)
+    eng.sort(21)
+    monkeypatch.setenv("GKM_PACK_MIN", "0")
+    eng.set_sequence(b, seg)
+    monkeypatch.delenv("GKM_PACK_MIN")
+    np.testing.assert_array_equal(eng.copy_sequence(len(b)), b)
+    n = eng.enumerate(21)
+    eng.sort(21)
+    want = oracle.quicksort(b, oracle.enumerate_starts(b, seg, 21), 21, 21, break_ties=True)
+    np.testing.assert_array_equal(eng.copy_starts(np.empty(n, dtype=np.uint32)), want)

@@ -1783,6 +1783,72 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_copy_kernel(const uint2 *__
     }
 }
 
+// TIMING EXPERIMENTS ONLY (GKM_EXP_WAVECOPY=2): the copy-only variant with the loads issued two
+// buckets ahead instead of one -- does more memory in flight per wave move the floor?
+template <int I, int MINW>
+__global__ __launch_bounds__(64, MINW) void msd_wave_copy2_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
+                                                            uint64_t *k0, uint32_t *v0, const uint64_t *k1,
+                                                            const uint32_t *v1, uint8_t *__restrict__ heads,
+                                                            const uint64_t *__restrict__ cpref,
+                                                            const uint8_t *__restrict__ cnd) {
+    const int lane = threadIdx.x;
+    uint32_t idx = blockIdx.x, lend = count, lstep = gridDim.x;
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+        const uint32_t x = blockIdx.x & 7;
+        idx = (uint32_t)((uint64_t)count * x / 8) + (blockIdx.x >> 3);
+        lend = (uint32_t)((uint64_t)count * (x + 1) / 8);
+        lstep = gridDim.x >> 3;
+    }
+    if (idx >= lend) return;
+    uint2 e0, e1, e2;
+    uint64_t p0, p1, p2;
+    uint64_t a0[I], a1[I];
+    uint32_t b0[I], b1[I];
+    wave_entry(list, cpref, idx, e0, p0);
+    e1 = e0; p1 = p0;
+    if (idx + lstep < lend) wave_entry(list, cpref, idx + lstep, e1, p1);
+    wave_load<I>(e0, p0, lane, k0, k1, v0, v1, cnd, a0, b0);
+    wave_load<I>(e1, p1, lane, k0, k1, v0, v1, cnd, a1, b1);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    for (;;) {
+        const uint64_t st = e0.x;
+        const uint32_t len = e0.y >> 8;
+        const int hi0 = (e0.y >> 1) & 127;
+        const bool cmp = (p0 & kCompact) != 0;
+        uint64_t key[I];
+        uint32_t val[I];
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            key[i] = cmp ? compact_key(p0, hi0, B, b0[i] & 0xFFu, (uint32_t)(a0[i] >> 32)) : a0[i];
+            val[i] = cmp ? (uint32_t)a0[i] : b0[i];
+        }
+        e2 = e1; p2 = p1;
+        if (idx + 2 * lstep < lend) wave_entry(list, cpref, idx + 2 * lstep, e2, p2);
+        wave_load<I>(e2, p2, lane, k0, k1, v0, v1, cnd, a0, b0);  // two buckets ahead
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint32_t j = min((uint32_t)(i * 64 + lane), len - 1);
+            gmem(k0)[st + j] = key[i];
+            gmem(v0)[st + j] = val[i];
+            gmem(heads)[st + j] = 1;
+        }
+        idx += lstep;
+        if (idx >= lend) break;
+        // rotate: bucket 1 becomes current (its loads were issued a bucket ago)
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const uint64_t ta = a0[i];
+            a0[i] = a1[i];
+            a1[i] = ta;
+            const uint32_t tb = b0[i];
+            b0[i] = b1[i];
+            b1[i] = tb;
+        }
+        e0 = e1; p0 = p1;
+        e1 = e2; p1 = p2;
+    }
+}
+
 static bool exp_wave_copy() { return std::getenv("GKM_EXP_WAVECOPY") != nullptr; }
 
 // one round's lists, copied to device memory for the wave kernels
@@ -2860,6 +2926,12 @@ struct MsdDriver {
             wave(msd_wave_kernel<4, kWaveOcc4, true, kWaveR4>, msd_wave_kernel<4, kWaveOcc4, false, kWaveR4>);
             break;
         case 1:
+            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '2') {  // timing only
+                hipLaunchKernelGGL((msd_wave_copy2_kernel<8, kWaveOcc8>),
+                                   grid((const void *)msd_wave_copy2_kernel<8, kWaveOcc8>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
+                break;
+            }
             if (exp_wave_copy()) {  // timing experiments only: wrong output
                 hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8>),
                                    grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8>, 64), dim3(64), 0,

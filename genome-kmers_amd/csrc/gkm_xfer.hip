@@ -18,6 +18,10 @@
 // Packing, copies and unpacking overlap: slots are recycled once the device has unpacked them.
 // Inputs below GKM_PACK_MIN bytes (default 16 MiB) are copied as they are (gkm_capi.hip).
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
+
+#include <cstdio>
 
 #include <algorithm>
 #include <atomic>
@@ -155,7 +159,9 @@ __attribute__((target("avx2"))) bool pack_avx2(const uint8_t *s, uint64_t n, uin
         // (twice); dwords 0, 4, 1, 5 are then q0[0..3], q0[4..7], q1[0..3], q1[4..7]
         const __m256i b = _mm256_packus_epi16(_mm256_packus_epi32(q0, q1), _mm256_setzero_si256());
         const __m256i o = _mm256_permutevar8x32_epi32(b, order);
-        _mm_storeu_si128(reinterpret_cast<__m128i *>(d + i / 4), _mm256_castsi256_si128(o));
+        // d is 16-byte aligned (slot payloads start at multiples of 16): a streaming store, the
+        // staging slot is written once here and next read by the DMA engine, not by this core
+        _mm_stream_si128(reinterpret_cast<__m128i *>(d + i / 4), _mm256_castsi256_si128(o));
     }
     return pack_scalar(s + i, n - i, d + i / 4);
 }
@@ -190,6 +196,41 @@ uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen
         off += (blen + 15) & ~15ull;
     }
     return off;
+}
+
+// CPUs of the calling thread's NUMA node (within the process's affinity mask), for pinning the
+// packing threads next to the memory they read (GKM_XFER_NUMA=1); empty when unknown
+std::vector<int> caller_node_cpus() {
+    std::vector<int> out;
+    const int cpu = sched_getcpu();
+    if (cpu < 0) return out;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
+    for (int node = 0; node < 64; ++node) {
+        char path[96];
+        std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+        FILE *f = std::fopen(path, "r");
+        if (!f) continue;
+        char buf[4096] = {0};
+        const size_t got = std::fread(buf, 1, sizeof buf - 1, f);
+        std::fclose(f);
+        buf[got] = 0;
+        std::vector<int> cpus;
+        for (char *q = buf; *q;) {  // "a-b,c,d-e"
+            char *end;
+            const long a = std::strtol(q, &end, 10);
+            if (end == q) break;
+            long b = a;
+            if (*end == '-') b = std::strtol(end + 1, &end, 10);
+            for (long x = a; x <= b && x < CPU_SETSIZE; ++x)
+                if (CPU_ISSET((int)x, &allowed)) cpus.push_back((int)x);
+            q = end;
+            while (*q == ',' || *q == '\n') ++q;
+        }
+        if (std::find(cpus.begin(), cpus.end(), cpu) != cpus.end()) return cpus;
+    }
+    return out;
 }
 
 uint64_t env_u64(const char *name, uint64_t dflt) {
@@ -265,7 +306,10 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     unsigned hw = std::thread::hardware_concurrency();
     const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_XFER_THREADS", std::min(16u, hw ? hw : 1u)), C));
     const int S = (int)std::min<uint64_t>(C, std::max(2, 2 * T));
-    const bool hybrid = env_u64("GKM_XFER_HYBRID", 1) != 0 && host_pinned(sba);
+    // raw DMA from the back of a pinned source (GKM_XFER_HYBRID=1): measured slower than packing
+    // alone (3.1 Gb from pinned memory: 24.8-27.4 against 21.0-21.6 ms, profiles/r4/xfer_threads_numa.txt)
+    // -- the packing is bound by host memory bandwidth, which the DMA reads share
+    const bool hybrid = env_u64("GKM_XFER_HYBRID", 0) != 0 && host_pinned(sba);
     GK_TRY_HIP(c, xfer_slots(c, S, kHeaderBytes + chunk + 16));
     hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
     hipEvent_t *ev_raw = c->xfer_ev.data() + 2 * S;
@@ -302,6 +346,7 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             }
             const uint64_t at = k * chunk, m = std::min(chunk, len - at);
             const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (uint64_t)slot * c->xfer_slot_bytes, cen);
+            _mm_sfence();  // the chunk's streaming stores are globally visible before it is queued
             {
                 std::lock_guard<std::mutex> lk(mu);
                 used[slot] = u;
@@ -313,7 +358,16 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
         dol.fetch_add(cen.dollars);
     };
     std::vector<std::thread> pool;
-    for (int i = 0; i < T; ++i) pool.emplace_back(worker);
+    const std::vector<int> near = env_u64("GKM_XFER_NUMA", 0) ? caller_node_cpus() : std::vector<int>{};
+    for (int i = 0; i < T; ++i) {
+        pool.emplace_back(worker);
+        if (!near.empty()) {  // the packing threads next to the caller (and the sba it allocated)
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            for (int x : near) CPU_SET(x, &set);
+            pthread_setaffinity_np(pool.back().native_handle(), sizeof set, &set);
+        }
+    }
 
     hipError_t err = hipSuccess;
     std::vector<int> inflight;           // slots issued, unpack not yet known to have run

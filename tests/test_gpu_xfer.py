@@ -134,8 +134,11 @@ def pinned_copy(a):
 
 @pytest.mark.parametrize("runs,iupac", [(0, 0), (3, 5)])
 @pytest.mark.parametrize("blocks,threads", [(1, 1), (2, 4)])
-def test_pinned_source_hybrid_transfer(runs, iupac, blocks, threads, monkeypatch):
-    # a pinned source: chunks go packed from the front and raw (DMA, device census) from the back
+@pytest.mark.parametrize("hybrid", ["0", "1"])
+def test_pinned_source_hybrid_transfer(runs, iupac, blocks, threads, hybrid, monkeypatch):
+    # a pinned source; GKM_XFER_HYBRID=1: chunks go packed from the front and raw (DMA, device
+    # census) from the back
+    monkeypatch.setenv("GKM_XFER_HYBRID", hybrid)
     rng = np.random.default_rng(17 + runs)
     sba, seg = genome(rng, 40 * B + 1234, contigs=4, n_runs=runs, iupac=iupac)
     t = pinned_copy(sba)
@@ -153,6 +156,7 @@ def test_pinned_source_hybrid_transfer(runs, iupac, blocks, threads, monkeypatch
 
 @pytest.mark.parametrize("where", [0, 20 * B + 3, 40 * B - 1])
 def test_pinned_source_rejects_bad_bytes_anywhere(where, monkeypatch):
+    monkeypatch.setenv("GKM_XFER_HYBRID", "1")  # the device census of raw chunks must catch it too
     rng = np.random.default_rng(where)
     sba, seg = genome(rng, 40 * B)
     sba[where] = ord("x")

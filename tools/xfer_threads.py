@@ -20,9 +20,11 @@ pinned = torch.empty(len(sba), dtype=torch.uint8).pin_memory()
 pinned.numpy()[:] = sba
 eng = _native.Engine()
 out = {}
+numa = os.environ.get("XFER_NUMA_AB") == "1"  # also each count with GKM_XFER_NUMA=1
 for src_name, src in (("pageable", sba), ("pinned", pinned.numpy())):
-    for t in sys.argv[1:] or ["1", "4", "8", "16", "32"]:
-        os.environ["GKM_XFER_THREADS"] = t
+    for t in [f"{a}{b}" for a in (sys.argv[1:] or ["1", "4", "8", "16", "32"]) for b in (("", "n") if numa else ("",))]:
+        os.environ["GKM_XFER_NUMA"] = "1" if t.endswith("n") else "0"
+        os.environ["GKM_XFER_THREADS"] = t.rstrip("n")
         best = 1e9
         for _ in range(3):
             t0 = time.perf_counter()

@@ -557,8 +557,10 @@ def main():
     seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
 
     range_mode = dist is not None and args.exchange == "range"
-    # the last global level was compact: the wave-local round reads 9 B per element, not 12
+    # the last global level was compact: the wave-local round reads 9 B per element, not 12; a
+    # packed-pair level before it wrote 10 B (+ digit byte) per element, which the compact level reads
     compact_in = any(n.startswith("msd_pass_l") and n.endswith("c") for n in report)
+    pairs_in = any(n.startswith("msd_pass_l") and n.endswith("p") for n in report)
 
     def stage_bytes(name, v):
         u = v.get("units", 0)
@@ -569,7 +571,10 @@ def main():
         if name == "msd_pass_l0" and not range_mode:
             return seq_bytes * v["count"] + 13 * u  # sequence bytes in, (key, start, next digit) out
         if name.startswith("msd_pass_l") and name.endswith("c"):
-            return 21 * u  # compact level: (key, start) in, (low bits | start) + next digit out
+            # compact level: (key, start) -- or a packed pair, 10 B -- in, (low bits | start) + next digit out
+            return (19 if pairs_in else 21) * u
+        if name.startswith("msd_pass_l") and name.endswith("p"):
+            return 23 * u  # packed-pair level: (key, start) in, pair (10 B) + next digit out
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out
         if name.startswith("msd_local"):
@@ -604,7 +609,11 @@ def main():
     if dom in kinds:
         kdesc, what = kinds[dom]
     elif dom and dom.endswith("c"):
-        kdesc, what = "msd_pipe_kernel<1024,11,8,4>", "the compact last level's stable 8-bit partition"
+        kdesc, what = (("msd_pipe_kernel<1024,11,8,4,true,0,true>", "the compact last level's stable 8-bit partition "
+                        "(packed-pair input)") if pairs_in else
+                       ("msd_pipe_kernel<1024,11,8,4>", "the compact last level's stable 8-bit partition"))
+    elif dom and dom.endswith("p"):
+        kdesc, what = "msd_pipe_kernel<1024,11,8,5>", "one stable 8-bit MSD partition pass writing packed pairs"
     else:
         kdesc, what = "msd_pipe_kernel<1024,11,8,0>", "one stable 8-bit MSD partition pass"
     avg_ms = rp["total_ms"] / max(rp["count"], 1)

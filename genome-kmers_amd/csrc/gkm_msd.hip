@@ -1180,6 +1180,48 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
 // workgroup walking such a bucket alone took 3 ms per C4 rank
 static unsigned bucket_split(uint64_t nbuckets) { return nbuckets <= 4096 ? 32u : nbuckets <= 65536 ? 4u : 1u; }
 
+// (key, start) of packed-pair elements (a MODE 5 level's output, gkm_partition.h) in place, for
+// the buckets a packed-pair level's output goes to that do not read pairs: the next level when it
+// is not compact, and the local finishing classes.  Bucket j: start bst[j], length blen[j], sorted
+// key bits bpref[j] (the top hi of B); gridDim.y workgroups per bucket.
+__global__ __launch_bounds__(256) void expand_pair_kernel(const uint32_t *__restrict__ bst,
+                                                          const uint32_t *__restrict__ blen,
+                                                          const uint64_t *__restrict__ bpref, int hi, int B, int shi,
+                                                          uint64_t *__restrict__ kio, const uint16_t *__restrict__ in16,
+                                                          uint32_t *__restrict__ vout) {
+    const uint64_t st = bst[blockIdx.x];
+    const uint32_t len = blen[blockIdx.x];
+    const uint64_t top = (bpref[blockIdx.x] & ~kCompact) << (B - hi);
+    for (uint32_t e = blockIdx.y * 256 + threadIdx.x; e < len; e += gridDim.y * 256) {
+        uint64_t key;
+        uint32_t val;
+        unpack_pair(kio[st + e], in16[st + e], shi, key, val);
+        kio[st + e] = top | key;
+        vout[st + e] = val;
+    }
+}
+
+// the same over local-list entries [first, first + count) (entry: start, len << 8 | hi << 1 | parity;
+// prefixes in pref[]) -- the local buckets a packed-pair level's classify listed
+__global__ __launch_bounds__(256) void expand_pair_list_kernel(const uint2 *__restrict__ list,
+                                                               const uint64_t *__restrict__ pref, uint32_t first,
+                                                               int B, int shi, uint64_t *__restrict__ kio,
+                                                               const uint16_t *__restrict__ in16,
+                                                               uint32_t *__restrict__ vout) {
+    const uint2 en = list[first + blockIdx.x];
+    const uint64_t st = en.x;
+    const uint32_t len = en.y >> 8;
+    const int hi = (en.y >> 1) & 127;
+    const uint64_t top = (pref[first + blockIdx.x] & ~kCompact) << (B - hi);
+    for (uint32_t e = threadIdx.x; e < len; e += 256) {
+        uint64_t key;
+        uint32_t val;
+        unpack_pair(kio[st + e], in16[st + e], shi, key, val);
+        kio[st + e] = top | key;
+        vout[st + e] = val;
+    }
+}
+
 // keys of compact elements (gridDim.y workgroups per bucket): prefix | digit | low bits
 __global__ __launch_bounds__(256) void expand_compact_kernel(const uint32_t *__restrict__ bst,
                                                              const uint32_t *__restrict__ blen,
@@ -2244,6 +2286,8 @@ static const char *kLocTimer[kLocal][2] = {{"msd_local_wave4", "msd_local_wave4_
                                            {"msd_local_block32", "msd_local_block32_r"}};
 static const char *kPassNames[] = {"msd_pass_l0", "msd_pass_l1", "msd_pass_l2", "msd_pass_l3",
                                    "msd_pass_l4", "msd_pass_l5", "msd_pass_l6", "msd_pass_l7"};
+static const char *kPassNamesP[] = {"msd_pass_l0p", "msd_pass_l1p", "msd_pass_l2p", "msd_pass_l3p",
+                                    "msd_pass_l4p", "msd_pass_l5p", "msd_pass_l6p", "msd_pass_l7p"};  // packed pairs
 static const char *kPassNamesC[] = {"msd_pass_l0c", "msd_pass_l1c", "msd_pass_l2c", "msd_pass_l3c",
                                     "msd_pass_l4c", "msd_pass_l5c", "msd_pass_l6c", "msd_pass_l7c"};  // compact
 
@@ -2274,6 +2318,12 @@ struct MsdDriver {
     bool compact_now = false;
     int compact_hi = 0;
     bool nd_ready = false, nd_next = true;
+    // packed-pair levels (MODE 5): the level before a compact one writes 10-byte (key bits below
+    // the sorted ones, start) pairs + the digit byte instead of 12-byte (key, start) + digit; the
+    // compact level reads them (IN79).  allow_c79: msd_sort's own levels (GKM_NO_PAIRS=1: off)
+    bool allow_c79 = false, c79_in = false, c79_out = false;
+    int c79_shi = 0;
+    uint16_t *lo16 = nullptr;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
     uint64_t nloc[kLocal] = {0}, loc_elems[kLocal] = {0}, ndone = 0, big_elems = 0;
     uint32_t nbig = 0;
@@ -2639,7 +2689,21 @@ struct MsdDriver {
             const int rem = B - hi - R;  // 9..40: key bits below this level's digit
             NextDigits ndg{dig_at(B, hi + R, 8), nd};
             ndg.lowmask = (uint32_t)((1ull << (rem - 8)) - 1);
-            hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 4, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
+            if (c79_in)  // the previous level wrote packed pairs
+                hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 4, true, 0, true>), dim3(pgrid), dim3(kPT), 0,
+                                   c->stream, t_start, t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out],
+                                   c->vals[out], (uint32_t)T, n, ndg, lo16, c79_shi);
+            else
+                hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 4, true>), dim3(pgrid), dim3(kPT), 0, c->stream,
+                                   t_start, t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out],
+                                   c->vals[out], (uint32_t)T, n, ndg);
+            return;
+        }
+        if (c79_out) {  // packed pairs for the compact level behind this one
+            NextDigits ndg{dig_at(B, hi + R, nw), nd};
+            ndg.out16 = lo16;
+            ndg.pshi = c79_shi;
+            hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 5, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
                                t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
                                (uint32_t)T, n, ndg);
             return;
@@ -2683,12 +2747,49 @@ struct MsdDriver {
         const int rem = B - hi - width(level);
         compact_now = phase == 0 && !nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
         compact_hi = hi + width(level);
-        timer_begin(c, compact_now ? kPassNamesC[level & 7] : kPassNames[level & 7], &slot);
+        // packed pairs out: the next level is most likely compact (its sub-buckets local, its
+        // remaining bits <= 40) and this level's remaining key bits and the start fit 80 bits
+        const uint64_t next_mean = nseg ? (big_elems / nseg >> width(level)) >> width(level + 1) : 0;
+        const int rem2 = rem - width(level + 1);
+        const bool force = std::getenv("GKM_TEST_PAIRS") != nullptr;  // tests: whenever the bits fit (read per level)
+        c79_out = allow_c79 && !c79_in && phase == 0 && !compact_now && rem >= 33 && rem <= 48 && !no_compact() &&
+                  (force || (nd_next && next_mean < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 &&
+                             width(level + 2) == 8 && width(level + 1) == 8));
+        if (c79_out) {
+            c79_shi = 64 - rem;
+            GK_TRY_HIP(c, scratch(c, "msd_lo16", n + 64, &lo16));
+        }
+        // packed pairs in, but not a compact level after all: back to (key, start) first
+        if (c79_in && !compact_now) {
+            hipLaunchKernelGGL(expand_pair_kernel, dim3((unsigned)nseg, bucket_split(nseg)), dim3(256), 0, c->stream,
+                               big_start[cur_big], big_len[cur_big], big_pref[cur_big], hi, B, c79_shi,
+                               const_cast<uint64_t *>(kin), lo16, const_cast<uint32_t *>(vin));
+            GK_TRY_HIP(c, hipGetLastError());
+            c79_in = false;
+        }
+        timer_begin(c, compact_now ? kPassNamesC[level & 7] : c79_out ? kPassNamesP[level & 7] : kPassNames[level & 7],
+                    &slot);
         timer_units(c, slot, big_elems);
         level_dispatch(level, hi, t_start, t_count, T, kin, vin, out, false);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
-        nd_ready = nd_next || compact_now;  // a compact level wrote the next 8-bit digit
+        // a compact or packed-pair level wrote the next 8-bit digit too (the next count must not
+        // read keys: pairs hold them shifted)
+        nd_ready = nd_next || compact_now || c79_out;
+        c79_in = c79_out;  // the next level's input format
+        return GK_OK;
+    }
+
+    // after a packed-pair level's classify: its local buckets (entries [before[k], nloc[k]) of the
+    // generation-0 lists) back to (key, start) for the finishing kernels
+    int expand_pair_locals(const uint64_t (&before)[kLocal], int out) {
+        for (int k = 0; k < kLocal; ++k) {
+            if (nloc[k] <= before[k]) continue;
+            hipLaunchKernelGGL(expand_pair_list_kernel, dim3((unsigned)(nloc[k] - before[k])), dim3(256), 0,
+                               c->stream, loc[k][0], loc_pref[k], (uint32_t)before[k], B, c79_shi, c->keys[out], lo16,
+                               c->vals[out]);
+            GK_TRY_HIP(c, hipGetLastError());
+        }
         return GK_OK;
     }
 
@@ -2857,6 +2958,7 @@ struct MsdDriver {
     // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
     // key bits are sorted
     int levels(int level, int hi, int in) {
+        c79_in = false;
         while (nbig > 0) {
             const int out = in ^ 1;
             uint32_t *ntl, *nch, *tfirst, *cfirst;
@@ -2881,10 +2983,13 @@ struct MsdDriver {
                             c->vals[in], out);
             if (rc != GK_OK) return rc;
             cur_big ^= 1;
+            uint64_t before[kLocal];
+            for (int k = 0; k < kLocal; ++k) before[k] = nloc[k];
             rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big, nullptr, nullptr, 1,
                           big_pref[cur_big ^ 1], width(level), compact_now ? 1 : 0);
+            if (rc == GK_OK && c79_out) rc = expand_pair_locals(before, out);
             if (rc == GK_OK) rc = expand_big(out);
-            if (rc == GK_OK) rc = drop_uniform(level, out);
+            if (rc == GK_OK && !c79_out) rc = drop_uniform(level, out);  // (pairs: keys not comparable)
             if (rc != GK_OK) return rc;
             ++level;
             hi += width(level - 1);
@@ -3055,6 +3160,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
     if (nphase == 1) d.enable_wide_l0();
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);

@@ -488,7 +488,18 @@ struct NextDigits {
     // MODE 4 (a compact level, gkm_msd.hip): kout[] gets the key bits below the next digit
     // (lowmask) in the high half and the start in the low half; vout[] is not written
     uint32_t lowmask = 0;
+    // MODE 5 (a packed-pair level, gkm_msd.hip): the rem = 64 - pshi key bits below the sorted ones
+    // and the start in 80 bits -- kout[] = low key bits << pshi | start >> (32 - pshi), out16[] =
+    // the start's low 32 - pshi bits; vout[] is not written
+    uint16_t *out16 = nullptr;
+    int pshi = 0;
 };
+
+// a packed-pair element (MODE 5's output) -> (key bits below the sorted ones, start)
+__device__ __forceinline__ void unpack_pair(uint64_t a, uint32_t b16, int shi, uint64_t &key, uint32_t &val) {
+    key = a >> shi;
+    val = ((uint32_t)(a & ((1ull << shi) - 1)) << (32 - shi)) | b16;
+}
 
 template <int T, int I, int R, int MODE, bool ND>
 __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys, const uint32_t *s_vals,
@@ -502,6 +513,11 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     if (MODE == 4) {  // compact: (low key bits << 32 | start) in the key array, the next digit byte
         kout[o] = ((uint64_t)((uint32_t)k & nd.lowmask) << 32) | v;
         nd.out[o] = (uint8_t)dg_of(k, nd.d);
+    } else if (MODE == 5) {  // packed pair: 10 bytes (+ the next digit byte) instead of 12
+        const int shi = nd.pshi;
+        kout[o] = ((k & ((1ull << (64 - shi)) - 1)) << shi) | (v >> (32 - shi));
+        nd.out16[o] = (uint16_t)(v & ((1u << (32 - shi)) - 1));
+        nd.out[o] = (uint8_t)dg_of(k, nd.d);
     } else if (MODE != 1 || o == 0xFFFFFFFFu) {
         kout[o] = k;
         vout[o] = v;
@@ -509,13 +525,18 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     }
 }
 
-template <int T, int I, int R = 8, int MODE = 0, bool ND = false, int PRE_ = 0>
+// IN79: the input is packed pairs (a MODE 5 level's output: kin[] + in16[], key bits below the
+// sorted ones); only a compact (MODE 4) or packed-pair output, which never store the sorted bits,
+// may read it
+template <int T, int I, int R = 8, int MODE = 0, bool ND = false, int PRE_ = 0, bool IN79 = false>
 __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict__ t_start,
                                                      const uint32_t *__restrict__ t_count, Dig dl,
                                                      const uint32_t *__restrict__ tile_off,
                                                      const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                     uint32_t ntiles, uint64_t sink, NextDigits nd = {}) {
+                                                     uint32_t ntiles, uint64_t sink, NextDigits nd = {},
+                                                     const uint16_t *__restrict__ in16 = nullptr, int in_shi = 0) {
+    static_assert(!IN79 || MODE == 4 || MODE == 5, "packed-pair input keeps only the unsorted key bits");
     using SM = PipeSmem<T, I>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -542,8 +563,13 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint64_t e = b + min(q0 + i * 64, m - 1);
-            key[i] = kin[e];
-            val[i] = vin[e];
+            if (IN79) {
+                key[i] = kin[e];  // packed pair: unpacked at the item's first use (the rank loop)
+                val[i] = in16[e];
+            } else {
+                key[i] = kin[e];
+                val[i] = vin[e];
+            }
         }
     };
     uint32_t pcnt = 0;  // staged elements of the previous tile (0: none -> stores go to the sink)
@@ -564,6 +590,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
+            if (IN79) unpack_pair(key[i], val[i], in_shi, key[i], val[i]);  // (at the item's first use)
             dig[i] = dg_of(key[i], dl);
             rank[i] = rank_atomic(wc, dig[i], valid[i]);
             if (PRE + i < I) pipe_store<T, I, R, MODE, ND>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);

@@ -20,6 +20,8 @@
 #include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <cstdio>
 
@@ -200,10 +202,10 @@ uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen
 
 // CPUs of the calling thread's NUMA node (within the process's affinity mask), for pinning the
 // packing threads next to the memory they read (GKM_XFER_NUMA=1); empty when unknown
-std::vector<int> caller_node_cpus() {
+// the CPUs (within this process's affinity) of NUMA node `want`, or of the node holding CPU `cpu`
+// when want < 0
+static std::vector<int> node_cpus(int want, int cpu) {
     std::vector<int> out;
-    const int cpu = sched_getcpu();
-    if (cpu < 0) return out;
     cpu_set_t allowed;
     CPU_ZERO(&allowed);
     if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
@@ -228,9 +230,34 @@ std::vector<int> caller_node_cpus() {
             q = end;
             while (*q == ',' || *q == '\n') ++q;
         }
-        if (std::find(cpus.begin(), cpus.end(), cpu) != cpus.end()) return cpus;
+        if (want >= 0 ? node == want : std::find(cpus.begin(), cpus.end(), cpu) != cpus.end()) return cpus;
     }
     return out;
+}
+
+std::vector<int> caller_node_cpus() {
+    const int cpu = sched_getcpu();
+    return cpu < 0 ? std::vector<int>{} : node_cpus(-1, cpu);
+}
+
+// NUMA node of the page holding p (get_mempolicy with MPOL_F_NODE | MPOL_F_ADDR), -1 if unknown
+static int page_node(const void *p) {
+    int node = -1;
+    if (syscall(SYS_get_mempolicy, &node, nullptr, 0UL, const_cast<void *>(p), 3UL) != 0) return -1;
+    return node;
+}
+
+// the node holding most of [p, p + len) (17 sampled pages), -1 if unknown
+static int buffer_node(const uint8_t *p, uint64_t len) {
+    int votes[64] = {0};
+    for (int i = 0; i <= 16; ++i) {
+        const int nd = page_node(p + (len ? (len - 1) * i / 16 : 0));
+        if (nd >= 0 && nd < 64) ++votes[nd];
+    }
+    int best = -1;
+    for (int nd = 0; nd < 64; ++nd)
+        if (votes[nd] && (best < 0 || votes[nd] > votes[best])) best = nd;
+    return best;
 }
 
 uint64_t env_u64(const char *name, uint64_t dflt) {
@@ -358,7 +385,14 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
         dol.fetch_add(cen.dollars);
     };
     std::vector<std::thread> pool;
-    const std::vector<int> near = env_u64("GKM_XFER_NUMA", 0) ? caller_node_cpus() : std::vector<int>{};
+    // GKM_XFER_NUMA: 1 = the packing threads on the caller's node, 2 = on the node holding the source
+    const uint64_t numa = env_u64("GKM_XFER_NUMA", 0);
+    const std::vector<int> near = numa == 1   ? caller_node_cpus()
+                                  : numa == 2 ? [&] {
+                                        const int nd = buffer_node(sba, len);
+                                        return nd < 0 ? std::vector<int>{} : node_cpus(nd, -1);
+                                    }()
+                                              : std::vector<int>{};
     for (int i = 0; i < T; ++i) {
         pool.emplace_back(worker);
         if (!near.empty()) {  // the packing threads next to the caller (and the sba it allocated)

@@ -4,6 +4,8 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "packed_pair or wide_l0" --timeout 200 --timeout-method thread > gpurun_out/gpu_pairs.log 2>&1 || { tail -40 gpurun_out/gpu_pairs.log; exit 1; }
 tail -2 gpurun_out/gpu_pairs.log
+timeout -k 10 300 python -u tools/xfer_numa2.py > gpurun_out/xfer_numa2.txt 2>&1 || { tail -20 gpurun_out/xfer_numa2.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/xfer_numa2.txt
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
 for rep in 1 2 3; do

@@ -15,7 +15,7 @@ def main(path):
         avg = {c: sum(v) / len(v) for c, v in d.items()}
         rows.append((avg.get("SQ_WAVE_CYCLES", 0), k, avg, len(next(iter(d.values())))))
     for wc, k, avg, n in sorted(rows, reverse=True)[:14]:
-        fr = {c.replace("SQ_", "").lower(): (v / wc if "CYCLES" in c or "WAIT" in c or "ACTIVE" in c else v)
+        fr = {c.replace("SQ_", "").lower(): (v / wc if ("CYCLES" in c or "WAIT" in c or "ACTIVE" in c) and not c.startswith("SQ_LDS") else v)
               for c, v in avg.items() if c != "SQ_WAVE_CYCLES" and wc}
         txt = "  ".join(f"{c}={v:.3g}" for c, v in sorted(fr.items()))
         print(f"{k[:48]:48s} n={n:<3d} wave_cycles={wc:.3g}  {txt}")

@@ -381,8 +381,16 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
 // PROF (timing builds, GKM_L0_PROF): the first and the last wave of each workgroup add the clock
 // ticks of every phase of the tile loop to a.prof[wave != 0][phase]
 constexpr int kL0Phases = 9;
-constexpr int kP0I = 18;                 // L0 tile: kPT threads x kP0I positions
-constexpr int kP0Tile = kPT * kP0I;      // 22,528 (< 65,536: positions staged as u16)
+#ifndef GKM_L0_T
+#define GKM_L0_T 1024
+#endif
+#ifndef GKM_L0_I
+#define GKM_L0_I 18
+#endif
+// (tuning overrides, tools/build_variant.sh: GKM_L0_T threads x GKM_L0_I positions per tile)
+constexpr int kP0T = GKM_L0_T;           // L0 tile: kP0T threads x kP0I positions
+constexpr int kP0I = GKM_L0_I;
+constexpr int kP0Tile = kP0T * kP0I;     // 18,432 (< 65,536: positions staged as u16)
 
 template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
@@ -2351,7 +2359,9 @@ struct MsdDriver {
     void enable_wide_l0() {
         const char *e = std::getenv("GKM_WIDE_L0");  // (read per sort: tests flip it)
         const bool want = e && *e && std::strcmp(e, "0") != 0;
-        if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8) wsched[0] = kWideL0;
+        // (its tiles are the 7-bit L0's: tile shapes overridden for tuning keep it off)
+        if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8 && kWT * kWI == kP0Tile)
+            wsched[0] = kWideL0;
     }
 
     // level digit widths "w0,w1,w2,..." (the last one repeats).  Default 7,8,8,...: for 2-bit
@@ -2457,24 +2467,24 @@ struct MsdDriver {
         // bytes in flight; GKM_L0_COUNT_1024=1 runs them for A/B)
         static const bool count1024 = std::getenv("GKM_L0_COUNT_1024") != nullptr;
         if (count && count1024)
-            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT, kP0I, R, CANON>),
-                               dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kPT), 0, c->stream, a, d0, tile_hist, nt0);
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kP0T, kP0I, R, CANON>),
+                               dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kP0T), 0, c->stream, a, d0, tile_hist, nt0);
         else if (count) {
             static int per_cu = 0;  // resident workgroups (the grid is persistent)
             if (!per_cu &&
                 (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                     &per_cu, (const void *)msd0_count_kernel<BITS, kPT / 4, kP0I * 4, R, CANON>, kPT / 4, 0) !=
+                     &per_cu, (const void *)msd0_count_kernel<BITS, kP0T / 4, kP0I * 4, R, CANON>, kP0T / 4, 0) !=
                      hipSuccess ||
                  per_cu < 1))
                 per_cu = 1;
-            hipLaunchKernelGGL((msd0_count_kernel<BITS, kPT / 4, kP0I * 4, R, CANON>),
-                               dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kPT / 4), 0, c->stream, a, d0,
+            hipLaunchKernelGGL((msd0_count_kernel<BITS, kP0T / 4, kP0I * 4, R, CANON>),
+                               dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kP0T / 4), 0, c->stream, a, d0,
                                tile_hist, nt0);
         }
         else if (BITS == 2 && R == 7 && !CANON && l0_prof())
             l0_prof_launch<ND>(a, d0, kout, vout, nt, sink, ndg);
         else
-            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kPT, kP0I, R, ND, CANON>), dim3(pgrid), dim3(kPT), 0, c->stream,
+            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kP0T, kP0I, R, ND, CANON>), dim3(pgrid), dim3(kP0T), 0, c->stream,
                                a, d0, tile_hist, kout, vout, nt, sink, ndg);
     }
 
@@ -2486,7 +2496,7 @@ struct MsdDriver {
         if (scratch(c, "l0_prof", 2 * kL0Phases, &pr) != hipSuccess) return;
         hipMemsetAsync(pr, 0, 16 * kL0Phases, c->stream);
         a.prof = pr;
-        hipLaunchKernelGGL((msd0_pipe_kernel<2, kPT, kP0I, 7, ND, false, true>), dim3(pgrid), dim3(kPT), 0, c->stream,
+        hipLaunchKernelGGL((msd0_pipe_kernel<2, kP0T, kP0I, 7, ND, false, true>), dim3(pgrid), dim3(kP0T), 0, c->stream,
                            a, d0, tile_hist, kout, vout, nt, sink, ndg);
         unsigned long long h[2 * kL0Phases];
         hipMemcpyAsync(h, pr, 16 * kL0Phases, hipMemcpyDeviceToHost, c->stream);
@@ -2511,12 +2521,12 @@ struct MsdDriver {
                 static int per_cu = 0;
                 if (!per_cu &&
                     (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                         &per_cu, (const void *)msd0_count_kernel<2, kPT / 4, kP0I * 4, kWideL0, false>, kPT / 4,
+                         &per_cu, (const void *)msd0_count_kernel<2, 256, kWT * kWI / 256, kWideL0, false>, 256,
                          0) != hipSuccess ||
                      per_cu < 1))
                     per_cu = 1;
-                hipLaunchKernelGGL((msd0_count_kernel<2, kPT / 4, kP0I * 4, kWideL0, false>),
-                                   dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kPT / 4), 0, c->stream, a, d0,
+                hipLaunchKernelGGL((msd0_count_kernel<2, 256, kWT * kWI / 256, kWideL0, false>),
+                                   dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(256), 0, c->stream, a, d0,
                                    tile_hist, nt0);
             } else if (nd_)
                 hipLaunchKernelGGL((msd0_wide_kernel<kWT, kWI, kWideL0, true>), dim3(pgrid), dim3(kWT), 0, c->stream,

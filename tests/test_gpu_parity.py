@@ -773,13 +773,14 @@ def test_wide_l0_k_sweep_vs_oracle(k, monkeypatch):
 # buckets the pair level sends to the finishing classes and a next level that is not compact get
 # (key, start) back first (expand_pair_*).  At test sizes GKM_TEST_PAIRS=1 makes every level whose
 # remaining bits fit write pairs; the low-entropy input keeps buckets big for several levels.
-@pytest.mark.parametrize("level_bits", ["8", "8,6", "7,8,8"])
-def test_packed_pair_levels_vs_oracle(level_bits, monkeypatch):
+@pytest.mark.parametrize("level_bits,k", [("8", 31), ("8,6", 31), ("7,8,8", 31), ("7,8,8", 24), ("8", 32)])
+def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
+    # k = 24 / 32: 33 / 48 key bits left behind the pair level (the two ends of its range)
     monkeypatch.setenv("GKM_TEST_PAIRS", "1")
     monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(31)
     seqs = random_genome(rng, [1_600_000, 800_000], alphabet=b"AC")
     seqs.append(("mixed", random_genome(rng, [300_000])[0][1]))
-    km, sc, want = oracle_check(seqs, 31, 31)
-    spec = oracle.key_spec(True, 31, 31)
+    km, sc, want = oracle_check(seqs, k, k)
+    spec = oracle.key_spec(True, k, k)
     np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))

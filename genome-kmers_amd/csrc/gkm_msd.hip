@@ -130,12 +130,17 @@ __device__ __forceinline__ void l0_load(const L0Args &a, uint64_t P0, uint64_t (
     static_assert(U::kPer >= 2, "the packed path keeps a code word and a stop word");
     // every element of r is written on both paths (a path that leaves some unwritten made the
     // compiler keep r in scratch memory at kPer = 3)
-    if (BITS == 2 && a.pk_code) {  // pre-packed: thread g < kGroups holds group g's words
-        const uint64_t g = (P0 >> 5) + min((uint32_t)threadIdx.x, (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
-        r[0] = a.pk_code[g];
-        r[1] = a.pk_dol[g];
+    if (BITS == 2 && a.pk_code) {  // pre-packed: thread t holds the words of groups t, t + T, ...
+        constexpr int kPairs = U::kPer / 2;
+        static_assert(kPairs * T >= L0Pack<BITS, TILE>::kGroups, "every packed group has a register pair");
 #pragma unroll
-        for (int j = 2; j < U::kPer; ++j) r[j] = 0;
+        for (int j = 0; j < kPairs; ++j) {
+            const uint64_t g = (P0 >> 5) + min((uint32_t)(threadIdx.x + j * T), (uint32_t)L0Pack<BITS, TILE>::kGroups - 1);
+            r[2 * j] = a.pk_code[g];
+            r[2 * j + 1] = a.pk_dol[g];
+        }
+#pragma unroll
+        for (int j = 2 * kPairs; j < U::kPer; ++j) r[j] = 0;
     } else {
         const uint64_t *s8 = reinterpret_cast<const uint64_t *>(a.sba + P0);
 #pragma unroll
@@ -161,9 +166,13 @@ __device__ __forceinline__ void l0_pack(const uint64_t (&r)[L0Units<BITS, TILE, 
     using P = L0Pack<BITS, TILE>;
     constexpr uint64_t kOnes = 0x0101010101010101ull;
     if (BITS == 2 && packed) {
-        if (threadIdx.x < (uint32_t)P::kGroups) {
-            s_code[threadIdx.x] = r[0];
-            s_dol[threadIdx.x] = (uint32_t)r[1];
+#pragma unroll
+        for (int j = 0; j < U::kPer / 2; ++j) {
+            const uint32_t g = threadIdx.x + j * T;
+            if (g < (uint32_t)P::kGroups) {
+                s_code[g] = r[2 * j];
+                s_dol[g] = (uint32_t)r[2 * j + 1];
+            }
         }
         if (threadIdx.x == 0) s_code[P::kCodeWords - 1] = 0;
         return;
@@ -709,9 +718,16 @@ __global__ __launch_bounds__(T) void msd0_wide_kernel(L0Args a, Dig d0, const ui
 //                  a row store to consecutive addresses from tile_off[t]
 // Stable: tiles, waves, rows and lanes follow positions.  The kept k-mers then go through the
 // ordinary MSD levels as one bucket (the store pass writes their L0 digit bytes, so the first
-// level counts 1 byte per k-mer).
-constexpr int kST = 512, kSI = 8, kSTile = kST * kSI;  // 4096 positions per tile, 512 per wave
-constexpr int kSW = kST / 64;                          // waves per tile
+// level counts 1 byte per k-mer).  A tile is kSR rounds of 4096 positions (512 per wave per round):
+// one load of the tile's bytes (or packed words) per kSR rounds keeps more bytes in flight per
+// workgroup than one 4096-position tile did.
+#ifndef GKM_SEL_ROUNDS
+#define GKM_SEL_ROUNDS 1
+#endif
+constexpr int kST = 512, kSI = 8, kSR = GKM_SEL_ROUNDS;  // threads, rows of 64 positions per wave per round, rounds
+constexpr int kSRound = kST * kSI;                       // 4096 positions per round
+constexpr int kSTile = kSRound * kSR;                    // positions per tile
+constexpr int kSW = kST / 64;                            // waves per tile
 
 // MODE 0 / 1 are the two passes above.  MODE 2 is a single pass: workgroup w walks its own chunk of
 // tpw consecutive tiles and appends its kept k-mers at a running offset into its own region of
@@ -736,7 +752,7 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
     __shared__ uint32_t s_dol[P::kGroups];
     __shared__ uint8_t s_lut4[256];
     __shared__ uint16_t s_spos[kStage];
-    __shared__ uint32_t s_wtot[kSW];
+    __shared__ uint32_t s_wtot[2][kSW];  // per round parity (a round's barrier orders the reuse)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 256) s_lut4[tid] = c_code4_msd[tid];
     // tiles of this workgroup: a strided walk (MODE 0 / 1) or a chunk (MODE 2)
@@ -748,7 +764,6 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
     uint64_t rr[L0Units<BITS, kSTile, kST>::kPer];
     if (tfirst < tend) l0_load<BITS, kSTile, kST>(a, a.lo + (uint64_t)tfirst * kSTile, rr);
     for (uint32_t t = tfirst; t < tend; t += tstep) {
-        const uint64_t wslot = (uint64_t)t * kSW + wave;
         const uint64_t P0 = a.lo + (uint64_t)t * kSTile;
         __syncthreads();  // the LUT; the previous tile's codes and wave totals have been read
         l0_pack<BITS, kSTile, kST>(rr, s_code, s_dol, s_lut4, a.acgt_only, a.pk_code != nullptr);
@@ -757,13 +772,13 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
         if (t + tstep < tend) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)tstep * kSTile, rr);
         // MODE 2: the wave's output offset from the kept counts of the tile's waves (block-uniform
         // call: both paths below reach it)
-        auto chunk_offset = [&](uint32_t wcount) -> uint64_t {
-            if (lane == 0) s_wtot[wave] = wcount;
+        auto chunk_offset = [&](uint32_t wcount, int r) -> uint64_t {
+            if (lane == 0) s_wtot[r & 1][wave] = wcount;
             __syncthreads();
             uint32_t pre = 0, tot = 0;
 #pragma unroll
             for (int w = 0; w < kSW; ++w) {
-                const uint32_t v = s_wtot[w];
+                const uint32_t v = s_wtot[r & 1][w];
                 pre += w < wave ? v : 0u;
                 tot += v;
             }
@@ -778,97 +793,102 @@ __global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint
         // in position order, so their per-wave counts and offsets agree.
         if constexpr (BITS == 2 && CANON) {
             if (STORE) win = false;
-            const uint32_t anystop = tid < P::kGroups ? s_dol[tid] : 0u;
+            uint32_t anystop = 0;
+            for (int j = tid; j < P::kGroups; j += kST) anystop |= s_dol[j];
             win = win && __syncthreads_or(anystop != 0) == 0 && P0 + kSTile <= a.hi && d0.mask == 0x7Fu &&
                   (int)d0.shift == a.total_bits - 7 && a.symbols >= (a.own_bits + 1) / 2 && a.own_bits <= a.total_bits;
         }
-        if (BITS == 2 && win) {
-            // 8 consecutive positions per thread (Win8)
-            const uint32_t q0 = tid * 8;
-            Win8 win8{};
-            uint32_t keepm = 0;
-            if constexpr (!CANON) {
-                win8 = win8_load(s_code, s_dol, q0);
-                uint32_t dig[8];
-                keepm = win8_keep(win8, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
-            } else {  // the smaller of the forward and reverse-complement top own_bits bits
-                // (msd0_count_kernel): the reverse complement's first ns symbols are the complement
-                // of the k-mer's last ns symbols, reversed
-                const int ob = a.own_bits, ns = (ob + 1) >> 1;
-                const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - ns);
-                const uint32_t om = (1u << ob) - 1;
+        for (int r = 0; r < kSR; ++r) {
+            const uint32_t R0 = r * kSRound;                       // the round's first tile position
+            const uint64_t wslot = ((uint64_t)t * kSR + r) * kSW + wave;
+            if (BITS == 2 && win) {
+                // 8 consecutive positions per thread (Win8)
+                const uint32_t q0 = R0 + tid * 8;
+                Win8 win8{};
+                uint32_t keepm = 0;
+                if constexpr (!CANON) {
+                    win8 = win8_load(s_code, s_dol, q0);
+                    uint32_t dig[8];
+                    keepm = win8_keep(win8, a, d0, (int64_t)a.hi - (int64_t)(P0 + q0), s_dol, q0, dig);
+                } else {  // the smaller of the forward and reverse-complement top own_bits bits
+                    // (msd0_count_kernel): the reverse complement's first ns symbols are the complement
+                    // of the k-mer's last ns symbols, reversed
+                    const int ob = a.own_bits, ns = (ob + 1) >> 1;
+                    const uint64_t tf = win32_at(s_code, q0), tr = win32_at(s_code, q0 + a.symbols - ns);
+                    const uint32_t om = (1u << ob) - 1;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t f = (uint32_t)(tf >> (64 - ob - 2 * i)) & om;
+                        const uint32_t v = (uint32_t)(tr >> (64 - 2 * ns - 2 * i)) & ((1u << (2 * ns)) - 1);
+                        const uint32_t r = (uint32_t)(__builtin_bitreverse64(~(uint64_t)v) >> (64 - 2 * ns));
+                        // bitreverse flips each pair's bit order too: swap the bits of every pair back
+                        const uint32_t rr = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
+                        keepm |= (l0_owned(min(f, rr >> (2 * ns - ob)), a) ? 1u : 0u) << i;
+                    }
+                }
+                const uint32_t cnt = (uint32_t)__popc(keepm);
+                const uint32_t incl = wave_incl_scan(cnt);
+                const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+                if (!STORE) {
+                    if (lane == 63) wave_cnt[wslot] = incl;
+                    continue;
+                }
+                const uint64_t o = MODE == 2 ? chunk_offset(total, r) : (uint64_t)wave_off[wslot];
+                // stage the wave's kept positions in position order, then store the k-mers as one
+                // coalesced run
+                uint16_t *sp = s_spos + wave * kSlots;
+                uint32_t j = incl - cnt;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    const uint32_t f = (uint32_t)(tf >> (64 - ob - 2 * i)) & om;
-                    const uint32_t v = (uint32_t)(tr >> (64 - 2 * ns - 2 * i)) & ((1u << (2 * ns)) - 1);
-                    const uint32_t r = (uint32_t)(__builtin_bitreverse64(~(uint64_t)v) >> (64 - 2 * ns));
-                    // bitreverse flips each pair's bit order too: swap the bits of every pair back
-                    const uint32_t rr = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
-                    keepm |= (l0_owned(min(f, rr >> (2 * ns - ob)), a) ? 1u : 0u) << i;
+                    const uint32_t kp = (keepm >> i) & 1u;
+                    sp[kp ? j : 512u + (uint32_t)lane] = (uint16_t)(q0 + i);  // (tile positions < 65,536)
+                    j += kp;
                 }
-            }
-            const uint32_t cnt = (uint32_t)__popc(keepm);
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            if (!STORE) {
-                if (lane == 63) wave_cnt[wslot] = incl;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                for (uint32_t e = lane; e < total; e += 64) {
+                    const uint32_t p = sp[e];
+                    const uint64_t k = CANON ? l0_key_of<2, true>(s_code, p, a.total_bits, a.symbols)
+                                             : l0_key<2>(s_code, p, a.total_bits);
+                    kout[o + e] = k;
+                    vout[o + e] = (uint32_t)(P0 + p);
+                    nd_out[o + e] = (uint8_t)dg_of(k, d0);
+                }
                 continue;
             }
-            const uint64_t o = MODE == 2 ? chunk_offset(total) : (uint64_t)wave_off[wslot];
-            // stage the wave's kept positions in position order, then store the k-mers as one
-            // coalesced run
-            uint16_t *sp = s_spos + wave * kSlots;
-            uint32_t j = incl - cnt;
+            {
+                // one ballot per row of 64 positions
+                const uint32_t wbase = R0 + wave * (kSI * 64);
+                uint64_t key[kSI];
+                uint32_t at[kSI];
+                uint32_t keepm = 0, kept = 0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t kp = (keepm >> i) & 1u;
-                sp[kp ? j : 512u + (uint32_t)lane] = (uint16_t)(q0 + i);
-                j += kp;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-            for (uint32_t e = lane; e < total; e += 64) {
-                const uint32_t p = sp[e];
-                const uint64_t k = CANON ? l0_key_of<2, true>(s_code, p, a.total_bits, a.symbols)
-                                         : l0_key<2>(s_code, p, a.total_bits);
-                kout[o + e] = k;
-                vout[o + e] = (uint32_t)(P0 + p);
-                nd_out[o + e] = (uint8_t)dg_of(k, d0);
-            }
-            continue;
-        }
-        {
-            // one ballot per row of 64 positions
-            const uint32_t wbase = wave * (kSI * 64);
-            uint64_t key[kSI];
-            uint32_t at[kSI];
-            uint32_t keepm = 0, kept = 0;
+                for (int i = 0; i < kSI; ++i) {
+                    const uint32_t p = wbase + i * 64 + lane;
+                    key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
+                    const bool keep = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned_key(key[i], a);
+                    const uint64_t m = __ballot(keep);
+                    at[i] = kept + lanes_below(m);
+                    kept += (uint32_t)__popcll(m);
+                    keepm |= (keep ? 1u : 0u) << i;
+                }
+                if (!STORE) {
+                    if (lane == 0) wave_cnt[wslot] = kept;
+                    continue;
+                }
+                const uint64_t base = MODE == 2 ? chunk_offset(kept, r) : (uint64_t)wave_off[wslot];
 #pragma unroll
-            for (int i = 0; i < kSI; ++i) {
-                const uint32_t p = wbase + i * 64 + lane;
-                key[i] = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
-                const bool keep = l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned_key(key[i], a);
-                const uint64_t m = __ballot(keep);
-                at[i] = kept + lanes_below(m);
-                kept += (uint32_t)__popcll(m);
-                keepm |= (keep ? 1u : 0u) << i;
-            }
-            if (!STORE) {
-                if (lane == 0) wave_cnt[wslot] = kept;
-                continue;
-            }
-            const uint64_t base = MODE == 2 ? chunk_offset(kept) : (uint64_t)wave_off[wslot];
-#pragma unroll
-            for (int i = 0; i < kSI; ++i) {
-                if ((keepm >> i) & 1u) {
-                    const uint64_t o = base + at[i];
-                    kout[o] = key[i];
-                    vout[o] = (uint32_t)(P0 + wbase + i * 64 + lane);
-                    nd_out[o] = (uint8_t)dg_of(key[i], d0);
+                for (int i = 0; i < kSI; ++i) {
+                    if ((keepm >> i) & 1u) {
+                        const uint64_t o = base + at[i];
+                        kout[o] = key[i];
+                        vout[o] = (uint32_t)(P0 + wbase + i * 64 + lane);
+                        nd_out[o] = (uint8_t)dg_of(key[i], d0);
+                    }
                 }
             }
-        }
+        }  // rounds
     }
     if (MODE == 2 && tid == 0 && blockIdx.x * tpw < ntiles) wave_cnt[blockIdx.x] = (uint32_t)run;
 }
@@ -895,7 +915,7 @@ __global__ __launch_bounds__(kST) void own_hist_kernel(L0Args a, uint32_t ntiles
         __syncthreads();
         if (t + gridDim.x < ntiles) l0_load<BITS, kSTile, kST>(a, P0 + (uint64_t)gridDim.x * kSTile, rr);
 #pragma unroll
-        for (int i = 0; i < kSI; ++i) {
+        for (int i = 0; i < kSI * kSR; ++i) {
             const uint32_t p = i * kST + tid;
             const uint64_t key = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
             if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi) atomicAdd(&s_hist[(uint32_t)(key >> osh)], 1u);
@@ -3306,7 +3326,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     GK_TRY_HIP(c, msd_tables());
     const uint64_t L = c->sba_len;
     const uint32_t ntiles = (uint32_t)std::max<uint64_t>((L + kSTile - 1) / kSTile, 1);
-    const uint64_t nw = (uint64_t)ntiles * kSW;
+    const uint64_t nw = (uint64_t)ntiles * kSR * kSW;
     L0Args a{c->sba, 0, L, ks.symbols, d.B, ks.acgt_only};
     a.own_lo = digit_lo;
     a.own_span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;

@@ -3,13 +3,7 @@
 # packed-pair tests at k = 24 / 32 -> gpurun_out/
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "packed_pair" --timeout 200 --timeout-method thread > gpurun_out/gpu_pairs.log 2>&1 || { tail -40 gpurun_out/gpu_pairs.log; exit 1; }
-tail -1 gpurun_out/gpu_pairs.log
-for rep in 1 2; do
-  for v in "GKM_X=0" "GKM_PACK=1"; do
-    timeout -k 10 300 env $v python -u tools/exp_stages.py --label "$v" > gpurun_out/pack_one.json 2>&1 && tail -1 gpurun_out/pack_one.json | tee -a gpurun_out/pack_ab.txt || { tail -5 gpurun_out/pack_one.json; exit 1; }
-  done
-done
+rm -f gpurun_out/pack_ab.txt
 for v in "GKM_X=0" "GKM_PACK=1"; do
   env $v timeout -k 10 400 python -u tools/range_emulate.py --config c3 --worlds 8 --reps 2 > gpurun_out/sel_one.txt 2>&1 || { tail -20 gpurun_out/sel_one.txt; exit 1; }
   python3 - "$v" >> gpurun_out/pack_ab.txt <<'PY'

@@ -166,6 +166,8 @@ def main():
             gather_bytes = (4 * len(rest_all) + 12 * len(runs_all)) if mixed else 0
             coll = collective_ms(world, measured, gather_bytes, mixed)
             for r in range(world):
+                print(f"# world {world}: rank {r}", file=sys.stderr, flush=True)  # progress (long runs)
+
                 def rank(last, r=r):
                     e.profile_enable(last)
                     h, _ = e.shard_histogram(pb[r], pb[r + 1], k, canonical=canonical)  # the rank's share

@@ -2278,6 +2278,13 @@ static bool l0_prof() {
     return v;
 }
 
+// tuning only (A/B runs): GKM_COUNT_ONE_PER_TILE=1 counts digit bytes with one workgroup per tile
+// (the persistent count is the default)
+static bool count_persist() {
+    static const bool v = std::getenv("GKM_COUNT_ONE_PER_TILE") == nullptr;
+    return v;
+}
+
 static bool use_pack() {
     static const bool on = std::getenv("GKM_PACK") != nullptr;
     return on;
@@ -2707,7 +2714,16 @@ struct MsdDriver {
     void level_launch(int hi, int nw, const uint32_t *t_start, const uint32_t *t_count, uint64_t T,
                       const uint64_t *kin, const uint32_t *vin, int out, bool count) {
         if (count) {
-            if (nd_ready)  // the previous pass wrote this level's digits
+            if (nd_ready && count_persist()) {  // the previous pass wrote this level's digits
+                static int per_cu = 0;  // resident workgroups (the grid is persistent)
+                if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                    &per_cu, (const void *)msd_count_nd_persist_kernel<R>, 256, 0) != hipSuccess ||
+                                per_cu < 1))
+                    per_cu = 1;
+                const unsigned g = (unsigned)std::min<uint64_t>(T, (uint64_t)cus * per_cu);
+                hipLaunchKernelGGL(msd_count_nd_persist_kernel<R>, dim3(std::max(g, 1u)), dim3(256), 0, c->stream,
+                                   t_start, t_count, nd, tile_hist, (uint32_t)T);
+            } else if (nd_ready)
                 hipLaunchKernelGGL(msd_count_nd_kernel<R>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start,
                                    t_count, nd, tile_hist);
             else

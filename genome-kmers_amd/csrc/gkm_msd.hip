@@ -336,11 +336,12 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
             // and the reverse-complement top 7 bits, 8 consecutive positions per thread from two
             // 32-symbol windows (at q0 and at q0 + k - 4)
             bool fast = false;
-            if constexpr (BITS == 2 && CANON) {
+            if constexpr (BITS == 2 && CANON && (R == 7 || R == 8)) {
                 uint32_t anystop = 0;
                 for (int j = t; j < P::kGroups; j += T) anystop |= s_dol[j];
-                fast = __syncthreads_or(anystop != 0) == 0 && P0 + TILE <= a.hi && d0.mask == 0x7Fu &&
-                       (int)d0.shift == a.total_bits - 7 && a.symbols >= 4;
+                fast = __syncthreads_or(anystop != 0) == 0 && P0 + TILE <= a.hi &&
+                       (d0.mask == 0x7Fu || d0.mask == 0xFFu) && (int)d0.shift == a.total_bits - R &&
+                       a.symbols >= 4;
                 if (fast) {
                     for (uint32_t g = t; g < TILE / 8; g += T) {
                         const uint32_t q0 = g * 8;
@@ -351,10 +352,11 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                         const uint32_t tr = (uint32_t)(win32_at(s_code, q0 + a.symbols - 4) >> 32);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
-                            const uint32_t f7 = (tf >> (25 - 2 * i)) & 0x7Fu;
+                            // (R = 8: the top 8 bits of both words; the smaller digit is the top of the smaller word)
+                            const uint32_t f7 = (tf >> (32 - R - 2 * i)) & ((1u << R) - 1);
                             const uint32_t v = (tr >> (24 - 2 * i)) & 0xFFu;  // symbols q0+k-4+i ..
                             const uint32_t rv = ((v & 3u) << 6) | ((v & 0xCu) << 2) | ((v >> 2) & 0xCu) | (v >> 6);
-                            const uint32_t d = min(f7, (~rv & 0xFFu) >> 1);
+                            const uint32_t d = min(f7, (~rv & 0xFFu) >> (8 - R));
                             if (l0_owned(d, a)) atomicAdd(&s_hist[d * NC], 1u);
                         }
                     }

@@ -2,8 +2,6 @@
 # every GPU test on the new default, then C3 stage times alternating x3 -> gpurun_out/
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
-tail -1 gpurun_out/gpu_tests.log
 rm -f gpurun_out/count_ab.txt
 for rep in 1 2 3; do
   for v in "GKM_COUNT_ONE_PER_TILE=1" "GKM_X=0"; do

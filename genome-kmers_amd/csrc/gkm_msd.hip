@@ -2280,13 +2280,6 @@ static bool l0_prof() {
     return v;
 }
 
-// tuning only (A/B runs): GKM_COUNT_ONE_PER_TILE=1 counts digit bytes with one workgroup per tile
-// (the persistent count is the default)
-static bool count_persist() {
-    static const bool v = std::getenv("GKM_COUNT_ONE_PER_TILE") == nullptr;
-    return v;
-}
-
 static bool use_pack() {
     static const bool on = std::getenv("GKM_PACK") != nullptr;
     return on;
@@ -2716,16 +2709,7 @@ struct MsdDriver {
     void level_launch(int hi, int nw, const uint32_t *t_start, const uint32_t *t_count, uint64_t T,
                       const uint64_t *kin, const uint32_t *vin, int out, bool count) {
         if (count) {
-            if (nd_ready && count_persist()) {  // the previous pass wrote this level's digits
-                static int per_cu = 0;  // resident workgroups (the grid is persistent)
-                if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                                    &per_cu, (const void *)msd_count_nd_persist_kernel<R>, 256, 0) != hipSuccess ||
-                                per_cu < 1))
-                    per_cu = 1;
-                const unsigned g = (unsigned)std::min<uint64_t>(T, (uint64_t)cus * per_cu);
-                hipLaunchKernelGGL(msd_count_nd_persist_kernel<R>, dim3(std::max(g, 1u)), dim3(256), 0, c->stream,
-                                   t_start, t_count, nd, tile_hist, (uint32_t)T);
-            } else if (nd_ready)
+            if (nd_ready)  // the previous pass wrote this level's digits
                 hipLaunchKernelGGL(msd_count_nd_kernel<R>, dim3((unsigned)T), dim3(256), 0, c->stream, t_start,
                                    t_count, nd, tile_hist);
             else
@@ -3208,6 +3192,11 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     MsdDriver d(c, ks);
     d.B = ks.bits * std::min(ks.symbols, spw);
     if (nphase == 1) d.enable_wide_l0();
+    // canonical 2-bit keys with a full 64-bit first word (k >= 32; C5): an 8-bit L0 leaves 48 bits
+    // behind the next level -- packed pairs there and a compact level after them, which the 7-bit
+    // L0's 49 and 41 bits do not allow (C5 219-221 -> 216.7-216.9 ms, profiles/r4/l08_ab.txt; the
+    // same change made C4, 62-bit keys, 5 ms slower)
+    if (ks.bits == 2 && ks.canonical && d.B == 64 && !std::getenv("GKM_LEVEL_BITS")) d.wsched[0] = 8;
     d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;

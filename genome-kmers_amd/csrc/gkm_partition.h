@@ -388,95 +388,6 @@ __global__ __launch_bounds__(256) void msd_count_nd_kernel(const uint32_t *__res
     }
 }
 
-// The same count, persistent: each workgroup walks tiles blockIdx.x, + gridDim.x, ...; the next
-// tile's digit bytes are loaded while the current tile is counted, and two histograms alternate
-// (a thread zeroes the entries it has written out), so a tile costs one barrier.  One workgroup
-// per tile spent most of its life starting up, zeroing and waiting for its first loads: the
-// count read its 3.1 GB (C3) at ~3.6 TB/s.
-struct NdPiece {
-    uint4 x[3];       // 16-digit pieces t, t + 256, t + 512 of the aligned middle
-    uint32_t hb, tb;  // this thread's byte of the ragged head / tail (0x100: none)
-    uint32_t head, quads;
-};
-
-__device__ __forceinline__ void nd_piece_load(const uint8_t *__restrict__ nd, uint64_t b, uint32_t m, NdPiece &p) {
-    const int t = threadIdx.x;
-    const uint32_t head = min<uint32_t>((uint32_t)((16 - ((uintptr_t)(nd + b) & 15)) & 15), m);
-    const uint32_t quads = (m - head) >> 4;
-    const uint4 *w = reinterpret_cast<const uint4 *>(nd + b + head);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const uint32_t i = r * 256 + t;
-        p.x[r] = i < quads ? w[i] : make_uint4(0, 0, 0, 0);
-    }
-    const uint32_t tail0 = head + 16 * quads;
-    p.hb = t < (int)head ? nd[b + t] : 0x100u;
-    p.tb = tail0 + t < m ? nd[b + tail0 + t] : 0x100u;
-    p.head = head;
-    p.quads = quads;
-}
-
-template <int R>
-__global__ __launch_bounds__(256) void msd_count_nd_persist_kernel(const uint32_t *__restrict__ t_start,
-                                                                   const uint32_t *__restrict__ t_count,
-                                                                   const uint8_t *__restrict__ nd,
-                                                                   uint32_t *__restrict__ tile_hist, uint32_t T) {
-    constexpr int RADIX = 1 << R;
-    __shared__ uint32_t s_hist[2][RADIX];
-    const int t = threadIdx.x;
-    uint32_t tile = blockIdx.x;
-    if (tile >= T) return;
-    for (int i = t; i < 2 * RADIX; i += 256) (&s_hist[0][0])[i] = 0;
-    NdPiece cur, nxt;
-    uint32_t m = t_count[tile];
-    nd_piece_load(nd, t_start[tile], m, cur);
-    lds_barrier();
-    for (int par = 0;; par ^= 1) {
-        const uint32_t next = tile + gridDim.x;
-        uint32_t mn = 0;
-        if (next < T) {  // (workgroup-uniform) the next tile's bytes fly while this one is counted
-            mn = t_count[next];
-            nd_piece_load(nd, t_start[next], mn, nxt);
-        }
-        uint32_t *h = s_hist[par];
-        const uint32_t quads = cur.quads;
-        if (cur.hb < 0x100u) atomicAdd(&h[cur.hb], 1u);
-        if (cur.tb < 0x100u) atomicAdd(&h[cur.tb], 1u);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            if ((uint32_t)(r * 256 + t) >= quads) continue;
-            const uint32_t xs[4] = {cur.x[r].x, cur.x[r].y, cur.x[r].z, cur.x[r].w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                atomicAdd(&h[xs[u] & 0xFF], 1u);
-                atomicAdd(&h[(xs[u] >> 8) & 0xFF], 1u);
-                atomicAdd(&h[(xs[u] >> 16) & 0xFF], 1u);
-                atomicAdd(&h[xs[u] >> 24], 1u);
-            }
-        }
-        if (quads > 3 * 256) {  // (tiles above 12 K digits: not made by the drivers; kept correct)
-            const uint4 *w = reinterpret_cast<const uint4 *>(nd + t_start[tile] + cur.head);
-            for (uint32_t i = 3 * 256 + t; i < quads; i += 256) {
-                const uint4 x = w[i];
-                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) atomicAdd(&h[(xs[u] >> (8 * q)) & 0xFF], 1u);
-            }
-        }
-        lds_barrier();  // this tile's counts complete; the other histogram was zeroed before
-        for (int i = t; i < RADIX; i += 256) {
-            tile_hist[(uint64_t)tile * RADIX + i] = h[i];
-            h[i] = 0;  // ready for the tile after next (behind the next tile's barrier)
-        }
-        if (next >= T) break;
-        tile = next;
-        m = mn;
-        cur = nxt;
-    }
-}
-
 // persistent: grid = a multiple of 8 blocks, each walks its XCD's tiles; the next tile's keys
 // and starts are loaded while the current tile's runs are stored
 template <int T, int I, int R, int MODE = 0, bool PROF = false>

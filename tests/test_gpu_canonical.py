@@ -143,3 +143,14 @@ def test_canonical_split_complementary_homopolymer_runs(k):
         out.append((name, b.decode()))
     km, _ = check_canonical(out, k)
     assert not km._engine.is_acgt()
+
+
+# canonical 2-bit keys with a 64-bit first word (k >= 32) take an 8-bit L0, then packed pairs and
+# a compact level where the bucket sizes call for them (C5); GKM_TEST_PAIRS=1 writes pairs wherever
+# the bits fit, so these sizes run the pair and compact levels with their canonical tie phases
+@pytest.mark.parametrize("k", [32, 63])
+def test_canonical_pair_levels_vs_oracle(k, monkeypatch):
+    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    rng = np.random.default_rng(500 + k)
+    check_canonical(genome_with_rc_repeats(rng, [900_000, 300_000], b"AC") +
+                    genome_with_rc_repeats(rng, [200_000], b"ACGT"), k)

@@ -152,5 +152,5 @@ def test_canonical_split_complementary_homopolymer_runs(k):
 def test_canonical_pair_levels_vs_oracle(k, monkeypatch):
     monkeypatch.setenv("GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(500 + k)
-    check_canonical(genome_with_rc_repeats(rng, [900_000, 300_000], b"AC") +
-                    genome_with_rc_repeats(rng, [200_000], b"ACGT"), k)
+    mixed = [("m" + name, s) for name, s in genome_with_rc_repeats(rng, [200_000], b"ACGT")]
+    check_canonical(genome_with_rc_repeats(rng, [900_000, 300_000], b"AC") + mixed, k)

@@ -31,7 +31,7 @@ namespace gkm {
 constexpr int kGR = 8;                  // global digit bits
 constexpr int kGRadix = 1 << kGR;
 constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
-// wide L0 (msd0_wide_kernel): 11-bit digits over the same 18,432-position tile, 512 threads x 36
+// wide L0 (msd0_wide_kernel): 11-bit digits over 18,432-position tiles of its own, 512 threads x 36
 constexpr int kWideL0 = 11, kWT = 512, kWI = 36;
 constexpr int kPTile = kPT * kPI;
 constexpr int kChunkTiles = 256;        // tiles per scan chunk (GKM_TEST_CHUNK_TILES overrides: tests only)
@@ -384,11 +384,11 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
 // L0 partition, software-pipelined with position staging.  The L0 input is the packed tile
 // itself, so a staged element needs only its tile position (u16): its key is re-derived from the
 // tile's codes when it is stored, and its start is the tile base + position.  Positions and codes
-// are double-buffered (2 x (45 + 6) KB at 22,528 positions), so the previous tile's stores are
+// are double-buffered (2 x (48 + 6) KB at 24,576 positions), so the previous tile's stores are
 // spread over EVERY phase of this tile -- packing, ranking, scan, staging -- and the memory pipe
 // never idles (staged as (key, start) in one 135 KB buffer, the stores had to finish before the
 // staging: a phase profile (GKM_L0_PROF) showed them issued in 45 % of the tile time, backed up,
-// and the pipe idle for the rest).  Twice the tile of the level passes: runs of ~176 per digit.
+// and the pipe idle for the rest).  Twice the tile of the level passes: runs of ~192 per digit.
 // PROF (timing builds, GKM_L0_PROF): the first and the last wave of each workgroup add the clock
 // ticks of every phase of the tile loop to a.prof[wave != 0][phase]
 constexpr int kL0Phases = 9;
@@ -396,12 +396,12 @@ constexpr int kL0Phases = 9;
 #define GKM_L0_T 1024
 #endif
 #ifndef GKM_L0_I
-#define GKM_L0_I 18
+#define GKM_L0_I 24
 #endif
 // (tuning overrides, tools/build_variant.sh: GKM_L0_T threads x GKM_L0_I positions per tile)
 constexpr int kP0T = GKM_L0_T;           // L0 tile: kP0T threads x kP0I positions
 constexpr int kP0I = GKM_L0_I;
-constexpr int kP0Tile = kP0T * kP0I;     // 18,432 (< 65,536: positions staged as u16)
+constexpr int kP0Tile = kP0T * kP0I;     // 24,576 (< 65,536: positions staged as u16)
 
 template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
@@ -2381,9 +2381,7 @@ struct MsdDriver {
     void enable_wide_l0() {
         const char *e = std::getenv("GKM_WIDE_L0");  // (read per sort: tests flip it)
         const bool want = e && *e && std::strcmp(e, "0") != 0;
-        // (its tiles are the 7-bit L0's: tile shapes overridden for tuning keep it off)
-        if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8 && kWT * kWI == kP0Tile)
-            wsched[0] = kWideL0;
+        if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8) wsched[0] = kWideL0;
     }
 
     // level digit widths "w0,w1,w2,..." (the last one repeats).  Default 7,8,8,...: for 2-bit
@@ -2593,7 +2591,8 @@ struct MsdDriver {
     // column scan (seg_base / seg_cnt), *count = k-mers kept
     int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count) {
         const uint64_t span = hi > lo ? hi - lo : 0;
-        const uint64_t nt0 = std::max<uint64_t>((span + kP0Tile - 1) / kP0Tile, 1);
+        const uint64_t tile = wsched[0] == kWideL0 ? (uint64_t)kWT * kWI : (uint64_t)kP0Tile;  // (the wide L0's own)
+        const uint64_t nt0 = std::max<uint64_t>((span + tile - 1) / tile, 1);
         const uint64_t nc0 = (nt0 + ctiles - 1) / ctiles;
         l0_tiles = nt0;
         int rc = tables(nt0, nc0, 1);

@@ -737,7 +737,12 @@ constexpr int kSW = kST / 64;                            // waves per tile
 // count pass is needed); wave_cnt[w] receives the chunk's kept count.  The regions, in workgroup
 // order, are the pieces of one bucket in position order (first_level_from_pieces).
 template <int BITS, bool CANON, int MODE>
-__global__ __launch_bounds__(kST) void msd0_select_kernel(L0Args a, Dig d0, uint32_t ntiles, uint32_t tpw,
+#ifndef GKM_SEL_MINW
+#define GKM_SEL_MINW 1
+#endif
+// (tuning override: GKM_SEL_MINW = the waves per SIMD the forward kernels' registers are capped
+// for; the canonical ones would spill to scratch)
+__global__ __launch_bounds__(kST, CANON ? 1 : GKM_SEL_MINW) void msd0_select_kernel(L0Args a, Dig d0, uint32_t ntiles, uint32_t tpw,
                                                           uint32_t *__restrict__ wave_cnt,
                                                           const uint32_t *__restrict__ wave_off,
                                                           uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,

@@ -115,12 +115,14 @@ __global__ __launch_bounds__(256) void unresolved_groups_kernel(const uint32_t *
 __global__ __launch_bounds__(256) void pair_keys_kernel(const uint32_t *__restrict__ vals,
                                                         const uint32_t *__restrict__ R,
                                                         const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
-                                                        uint64_t o, uint64_t n, uint64_t *__restrict__ keys) {
+                                                        uint64_t o, uint64_t n, int bw,
+                                                        uint64_t *__restrict__ keys) {
+    // (rank of p, rank of p + o) in 2 bw bits: ranks are <= n < 2^bw
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p = vals[i];
         const uint64_t q = p + o;
         const uint32_t r2 = (q <= seg_end_of(seg, nseg, L, p)) ? R[q] : 0u;
-        keys[i] = ((uint64_t)R[p] << 32) | r2;
+        keys[i] = ((uint64_t)R[p] << bw) | r2;
     }
 }
 
@@ -660,7 +662,7 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         GK_TRY_HIP(c, launch_encode_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur]));
         timer_end(c, slot);
     }
-    rc = radix_sort(c, ks.words, ks.total_bits, hist_ready);
+    rc = sort_keys(c, ks.words, ks.total_bits, hist_ready);
     if (rc != GK_OK) return rc;
     c->spec = ks;
     c->keys_valid = true;
@@ -702,7 +704,7 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     timer_begin(c, "encode", &slot);
     GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], c->hist));
     timer_end(c, slot);
-    rc = radix_sort(c, 1, seed.total_bits, true);
+    rc = sort_keys(c, 1, seed.total_bits, true);
     if (rc != GK_OK) return rc;
 
     uint64_t h = (uint64_t)seed.symbols;
@@ -731,10 +733,11 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
         GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
         GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[c->cur], c->idx_a, c->idx_b, n1, c->ranks));
         const uint64_t o = bounded ? std::min<uint64_t>(h, M - h) : h;
+        const int bw = std::max(1, bit_width(n1));  // ranks: group start + 1 <= n1 (0: past the segment's end)
         hipLaunchKernelGGL(pair_keys_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->vals[c->cur], c->ranks,
-                           c->seg, (uint32_t)c->nseg, L, o, n1, c->keys[c->cur]);
+                           c->seg, (uint32_t)c->nseg, L, o, n1, bw, c->keys[c->cur]);
         GK_TRY_HIP(c, hipGetLastError());
-        rc = radix_sort(c, 1, 64, false);
+        rc = sort_keys(c, 1, 2 * bw, false);
         if (rc != GK_OK) return rc;
         h += o;
         if (bounded && h >= M) done = true;

@@ -254,6 +254,11 @@ hipError_t launch_canon_strands(gk_ctx *c, const KeySpec &ks, const uint32_t *st
 // sort
 hipError_t launch_histogram(gk_ctx *c, const uint64_t *keys, uint64_t n, int words, int digits, uint32_t *hist);
 int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready);
+// MSD over one-word keys in memory (gkm_msd.hip), radix_sort's contract; sort_keys picks it for
+// one-word arrays of >= kMsdKeysMin keys (gkm_sort.hip)
+int msd_sort_keys(gk_ctx *c, int total_bits);
+int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready);
+constexpr uint64_t kMsdKeysMin = 1ull << 20;
 
 // group / scan
 hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);

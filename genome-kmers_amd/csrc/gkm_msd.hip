@@ -3267,6 +3267,40 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     return rc;
 }
 
+// One-word keys already in memory (keys[cur] / vals[cur], n = c->n; the low total_bits bits of
+// each key significant), sorted stably by the MSD levels over the keys themselves -- 8-bit digits
+// from the top, packed pairs and a compact level where the bits allow, the same finishing kernels --
+// instead of one LSD pass per 8 bits: two global passes and the local rounds for 1e8 keys where
+// the LSD sort made six.  Result in keys[0] / vals[0] (c->cur = 0), the keys final; radix_sort's
+// contract otherwise (gkm_sort.hip).
+int msd_sort_keys(gk_ctx *c, int total_bits) {
+    KeySpec kk{};
+    kk.bits = 8;  // (no sequence-derived L0: every level reads the keys, 8-bit digits)
+    kk.symbols = (total_bits + 7) / 8;
+    kk.min_len = 1;
+    kk.words = 1;
+    kk.total_bits = total_bits;
+    MsdDriver d(c, kk);
+    d.B = total_bits;
+    d.wkeys = 1;
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    c->msd_keys_final = true;
+    timer_begin(c, "msd_total", &d.total_slot);
+    const int in = c->cur;
+    int rc = d.init(c->n);
+    if (rc != GK_OK) return rc;
+    uint32_t *one;
+    GK_TRY_HIP(c, scratch(c, "keys_bucket", 2, &one));
+    const uint32_t hb[2] = {0, (uint32_t)c->n};
+    GK_TRY_HIP(c, hipMemcpyAsync(one, hb, 8, hipMemcpyHostToDevice, c->stream));
+    rc = d.classify(1, 0, in, 0, one, one + 1);  // all keys as one bucket, no bits sorted
+    if (rc == GK_OK) rc = d.levels(0, 0, in);
+    if (rc == GK_OK) rc = d.finish();
+    c->cur = 0;
+    timer_end(c, d.total_slot);
+    return rc;
+}
+
 int msd_radix_bits() { return kGR; }
 hipError_t rank_mode_msd(int ballot) { return set_rank_ballot_here(ballot); }
 

@@ -12,6 +12,7 @@
 // Stability + ascending-start input => equal k-mers end up ordered by start index, i.e. the
 // reference's get_is_less_than_func(break_ties=True) order (kmers.py:1710-1711).
 #include <algorithm>
+#include <cstdlib>
 
 #include "gkm_internal.h"
 #include "gkm_onesweep.h"
@@ -141,6 +142,20 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready) {
         ++pass;
     }
     return GK_OK;
+}
+
+// The sorts of whole key arrays (the variable-length encodings, the prefix-doubling seeds and
+// rank pairs): large one-word ones by MSD levels over the keys (msd_sort_keys: two global passes
+// and the local rounds for 1e8 keys, where the LSD passes are one per 8 bits), the rest by
+// radix_sort.  GKM_SORT_KEYS_LSD=1 keeps the LSD passes (A/B, tests).  Result in keys / vals[cur]
+// either way; the MSD path also writes the group heads.
+int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready) {
+    const bool lsd = std::getenv("GKM_SORT_KEYS_LSD") != nullptr;  // (read per call: tests flip it)
+    const char *tm = std::getenv("GKM_MSD_KEYS_MIN");                // (tests: the MSD path at small n)
+    const uint64_t nmin = tm ? std::strtoull(tm, nullptr, 10) : kMsdKeysMin;
+    if (words == 1 && total_bits >= 24 && c->n >= nmin && c->n <= 0xFFFFFFFFull && !lsd)
+        return msd_sort_keys(c, total_bits);
+    return radix_sort(c, words, total_bits, hist_ready);
 }
 
 }  // namespace gkm

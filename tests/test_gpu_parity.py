@@ -784,3 +784,20 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
     km, sc, want = oracle_check(seqs, k, k)
     spec = oracle.key_spec(True, k, k)
     np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+
+
+# Whole-array sorts of encoded keys (bounded variable length, IUPAC 4-bit keys, the prefix-doubling
+# seeds and rank pairs) take the MSD levels over the keys from 2^20 keys on (msd_sort_keys);
+# GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes
+@pytest.mark.parametrize("path", ["msd", "lsd"])
+@pytest.mark.parametrize("alphabet,min_k,max_k", [(b"ACGT", 5, 20), (b"ACGT", 1, None), (b"ACGTNRYKM", 3, 12),
+                                                  (b"ACGTN", 2, None), (b"AC", 4, 29)])
+def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
+    if path == "msd":
+        monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")
+    else:
+        monkeypatch.setenv("GKM_SORT_KEYS_LSD", "1")
+    rng = np.random.default_rng(min_k * 7 + (max_k or 0))
+    rep = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), 3000).astype(np.uint8)
+    oracle_check(random_genome(rng, [60_000, 20_000, 7_000, 40], alphabet=alphabet, repeat=rep, copies=3),
+                 min_k, max_k)

@@ -651,9 +651,10 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     } else if (c->enumerated) {
         int slot;
         timer_begin(c, "encode", &slot);
-        GK_TRY_HIP(c, launch_encode_positions(c, ks, c->keys[c->cur], c->vals[c->cur], c->hist));
+        // (no LSD digit histograms when the MSD path sorts the keys)
+        hist_ready = !sort_keys_msd(c, c->n, ks.words, ks.total_bits);
+        GK_TRY_HIP(c, launch_encode_positions(c, ks, c->keys[c->cur], c->vals[c->cur], hist_ready ? c->hist : nullptr));
         timer_end(c, slot);
-        hist_ready = true;
     } else {
         rc = presort_by_start(c);
         if (rc != GK_OK) return rc;
@@ -702,9 +703,10 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     c->cur = 0;
     int slot;
     timer_begin(c, "encode", &slot);
-    GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], c->hist));
+    const bool seed_hist = !sort_keys_msd(c, n1, 1, seed.total_bits);
+    GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], seed_hist ? c->hist : nullptr));
     timer_end(c, slot);
-    rc = sort_keys(c, 1, seed.total_bits, true);
+    rc = sort_keys(c, 1, seed.total_bits, seed_hist);
     if (rc != GK_OK) return rc;
 
     uint64_t h = (uint64_t)seed.symbols;

@@ -907,8 +907,11 @@ hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys,
     hipError_t e = init_tables();
     if (e != hipSuccess) return e;
     KS k = pod(ks);
-    e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * k.digits, c->stream);
-    if (e != hipSuccess) return e;
+    if (hist == nullptr) k.digits = 0;  // no digit histograms (the MSD sort counts its own)
+    if (k.digits) {
+        e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * 256 * k.digits, c->stream);
+        if (e != hipSuccess) return e;
+    }
     const uint64_t ntiles = (c->sba_len + kEncodeTile - 1) / kEncodeTile;
     int grid = (int)std::min<uint64_t>(ntiles, 256 * 6);
     if (grid < 1) grid = 1;

@@ -258,6 +258,7 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready);
 // one-word arrays of >= kMsdKeysMin keys (gkm_sort.hip)
 int msd_sort_keys(gk_ctx *c, int total_bits);
 int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready);
+bool sort_keys_msd(const gk_ctx *c, uint64_t n, int words, int total_bits);  // sort_keys takes the MSD path
 constexpr uint64_t kMsdKeysMin = 1ull << 20;
 
 // group / scan

@@ -149,12 +149,15 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready) {
 // and the local rounds for 1e8 keys, where the LSD passes are one per 8 bits), the rest by
 // radix_sort.  GKM_SORT_KEYS_LSD=1 keeps the LSD passes (A/B, tests).  Result in keys / vals[cur]
 // either way; the MSD path also writes the group heads.
-int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready) {
+bool sort_keys_msd(const gk_ctx *c, uint64_t n, int words, int total_bits) {
     const bool lsd = std::getenv("GKM_SORT_KEYS_LSD") != nullptr;  // (read per call: tests flip it)
     const char *tm = std::getenv("GKM_MSD_KEYS_MIN");                // (tests: the MSD path at small n)
     const uint64_t nmin = tm ? std::strtoull(tm, nullptr, 10) : kMsdKeysMin;
-    if (words == 1 && total_bits >= 24 && c->n >= nmin && c->n <= 0xFFFFFFFFull && !lsd)
-        return msd_sort_keys(c, total_bits);
+    return words == 1 && total_bits >= 24 && n >= nmin && n <= 0xFFFFFFFFull && !lsd;
+}
+
+int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready) {
+    if (sort_keys_msd(c, c->n, words, total_bits)) return msd_sort_keys(c, total_bits);
     return radix_sort(c, words, total_bits, hist_ready);
 }
 

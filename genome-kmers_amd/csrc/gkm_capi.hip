@@ -126,6 +126,42 @@ __global__ __launch_bounds__(256) void pair_keys_kernel(const uint32_t *__restri
     }
 }
 
+// Prefix doubling by tied groups (sort_doubling, MSD path): the rank of p + o for the elements
+// still tied (flags: 1 starts a group), the others untouched
+__global__ __launch_bounds__(256) void member_r2_kernel(const uint8_t *__restrict__ flags,
+                                                        const uint32_t *__restrict__ vals,
+                                                        const uint32_t *__restrict__ R,
+                                                        const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
+                                                        uint64_t o, uint64_t n, uint64_t *__restrict__ keys) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (flags[i] != 0 && (i + 1 >= n || flags[i + 1] != 0)) continue;  // a group of one: final
+        const uint64_t p = vals[i];
+        const uint64_t q = p + o;
+        keys[i] = (q <= seg_end_of(seg, nseg, L, p)) ? R[q] : 0u;
+    }
+}
+
+// the groups after a round: a group start stays one, a tied element starts a group where the
+// round's sort found its key different from its predecessor's (heads of the sorted groups)
+__global__ __launch_bounds__(256) void merge_heads_kernel(const uint8_t *__restrict__ fold,
+                                                          const uint8_t *__restrict__ heads, uint64_t n,
+                                                          uint8_t *__restrict__ fnew) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        fnew[i] = (fold[i] != 0 || heads[i] != 0) ? 1 : 0;
+}
+
+// new ranks (group start + 1) of the elements that were tied before the round; the others keep theirs
+__global__ __launch_bounds__(256) void member_rank_kernel(const uint8_t *__restrict__ fold,
+                                                          const uint32_t *__restrict__ vals,
+                                                          const uint32_t *__restrict__ gid,
+                                                          const uint32_t *__restrict__ gstart, uint64_t n,
+                                                          uint32_t *__restrict__ R) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (fold[i] != 0 && (i + 1 >= n || fold[i + 1] != 0)) continue;
+        R[vals[i]] = gstart[gid[i] - 1] + 1;
+    }
+}
+
 // keep starts with >= m bases before the end of their segment
 __global__ __launch_bounds__(256) void len_flags_kernel(const uint32_t *__restrict__ vals,
                                                         const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
@@ -702,6 +738,9 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     c->n = n1;
     c->cur = 0;
     int slot;
+    // large universes: the rounds sort only the groups still tied (MSD, msd_sort_groups); small ones
+    // re-sort the whole array by rank pairs each round (LSD)
+    const bool by_groups = sort_keys_msd(c, n1, 1, 64) && std::getenv("GKM_DOUBLING_FULL") == nullptr;
     timer_begin(c, "encode", &slot);
     const bool seed_hist = !sort_keys_msd(c, n1, 1, seed.total_bits);
     GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], seed_hist ? c->hist : nullptr));
@@ -712,6 +751,54 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     uint64_t h = (uint64_t)seed.symbols;
     const bool bounded = M != 0;
     bool done = bounded && h >= M;  // (direct path covers M <= capacity; keep for safety)
+    if (by_groups && c->cur == 0) {
+        // flags of the current groups (fa), the next round's (fb); ranks of every position in R,
+        // scattered once and then only for the elements a round re-sorts
+        uint8_t *fa = c->flags, *fb;
+        GK_TRY_HIP(c, scratch(c, "dbl_flags", n1 + 64, &fb));
+        hipLaunchKernelGGL(full_key_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->keys[0], n1, fa);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t G = 0;
+        GK_TRY_HIP(c, select_flags(c, fa, n1, c->idx_b, &G));
+        GK_TRY_HIP(c, scan_flags_inclusive(c, fa, n1, c->idx_a));
+        GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
+        GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[0], c->idx_a, c->idx_b, n1, c->ranks));
+        const int bw = std::max(1, bit_width(n1));  // ranks: group start + 1 <= n1 (0: past the segment's end)
+        while (!done) {
+            if (G == n1) break;                          // all distinct
+            if (!bounded && h >= c->max_seg_len) break;  // every suffix ends within h symbols
+            {  // every tied group already holds equal k-mers (shared contig tails): done
+                uint32_t *d_cnt = reinterpret_cast<uint32_t *>(c->scalars + 20), cnt = 0;
+                GK_TRY_HIP(c, hipMemsetAsync(d_cnt, 0, 4, c->stream));
+                hipLaunchKernelGGL(unresolved_groups_kernel, dim3(grid_of(G)), dim3(256), 0, c->stream, c->vals[0],
+                                   c->idx_b, G, n1, c->seg, (uint32_t)c->nseg, L, h, d_cnt);
+                GK_TRY_HIP(c, hipGetLastError());
+                GK_TRY_HIP(c, hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, c->stream));
+                GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+                if (cnt == 0) break;
+            }
+            const uint64_t o = bounded ? std::min<uint64_t>(h, M - h) : h;
+            hipLaunchKernelGGL(member_r2_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0], c->ranks,
+                               c->seg, (uint32_t)c->nseg, L, o, n1, c->keys[0]);
+            GK_TRY_HIP(c, hipGetLastError());
+            rc = msd_sort_groups(c, fa, bw);
+            if (rc != GK_OK) return rc;
+            hipLaunchKernelGGL(merge_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->heads, n1, fb);
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, select_flags(c, fb, n1, c->idx_b, &G));
+            GK_TRY_HIP(c, scan_flags_inclusive(c, fb, n1, c->idx_a));
+            hipLaunchKernelGGL(member_rank_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0],
+                               c->idx_a, c->idx_b, n1, c->ranks);
+            GK_TRY_HIP(c, hipGetLastError());
+            std::swap(fa, fb);
+            h += o;
+            if (bounded && h >= M) done = true;
+        }
+        // the keys: dense group numbers (equal iff the k-mers are equal, ascending with the order)
+        hipLaunchKernelGGL(u32_to_key_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->idx_a, n1, c->keys[0]);
+        GK_TRY_HIP(c, hipGetLastError());
+        done = true;
+    }
     while (!done) {
         // groups of equal keys
         hipLaunchKernelGGL(full_key_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->keys[c->cur], n1,

@@ -259,6 +259,8 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready);
 int msd_sort_keys(gk_ctx *c, int total_bits);
 int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready);
 bool sort_keys_msd(const gk_ctx *c, uint64_t n, int words, int total_bits);  // sort_keys takes the MSD path
+// prefix doubling: the tied groups (flags: 1 starts a group) of keys[0] / vals[0] sorted by bkey-bit keys
+int msd_sort_groups(gk_ctx *c, const uint8_t *flags, int bkey);
 constexpr uint64_t kMsdKeysMin = 1ull << 20;
 
 // group / scan

@@ -2964,6 +2964,43 @@ struct MsdDriver {
         return finish();
     }
 
+    // Prefix doubling (gkm_capi.hip sort_doubling): every run of >= 2 elements of keys[0] / vals[0]
+    // that `flags` marks as one group (a 1 starts a group) sorted stably by the bkey-bit keys, in
+    // place; the members' group heads in c->heads.  Elements outside those groups stay where they
+    // are, so a round costs in proportion to the elements still tied, not to n.
+    int sort_groups(const uint8_t *flags, int bkey) {
+        uint32_t *g_start, *g_len;
+        const unsigned ttiles = (unsigned)std::max<uint64_t>((n + kTieTile - 1) / kTieTile, 1);
+        uint32_t *cf, *cl, *of, *ol;
+        GK_TRY_HIP(c, scratch(c, "tie_cnt_f", ttiles + 1, &cf));
+        GK_TRY_HIP(c, scratch(c, "tie_cnt_l", ttiles + 1, &cl));
+        GK_TRY_HIP(c, scratch(c, "tie_off_f", ttiles + 1, &of));
+        GK_TRY_HIP(c, scratch(c, "tie_off_l", ttiles + 1, &ol));
+        hipLaunchKernelGGL(tie_bounds_kernel<false>, dim3(ttiles), dim3(256), 0, c->stream, flags, n, cf, cl, nullptr,
+                           nullptr, nullptr, nullptr);
+        GK_TRY_HIP(c, hipGetLastError());
+        uint64_t ng = 0, ng2 = 0;
+        GK_TRY_HIP(c, scan_u32_exclusive_pair(c, cf, of, cl, ol, ttiles, &ng, &ng2));
+        if (ng != ng2) return fail(c, GK_E_HIP, "msd: tie group bounds do not pair up");
+        if (ng == 0) return GK_OK;
+        GK_TRY_HIP(c, scratch(c, "tie_start", ng + 64, &g_start));
+        GK_TRY_HIP(c, scratch(c, "tie_len", ng + 64, &g_len));
+        hipLaunchKernelGGL(tie_bounds_kernel<true>, dim3(ttiles), dim3(256), 0, c->stream, flags, n, nullptr, nullptr,
+                           of, ol, g_start, g_len);
+        GK_TRY_HIP(c, hipGetLastError());
+        hipLaunchKernelGGL(tie_run_lengths_kernel, dim3((unsigned)std::min<uint64_t>((ng + 255) / 256, 8192)),
+                           dim3(256), 0, c->stream, g_start, g_len, ng);
+        GK_TRY_HIP(c, hipGetLastError());
+        B = bkey;
+        phase = 1;  // (no compact or packed-pair levels: later-phase rules)
+        nd_ready = false;
+        int rc = classify(ng, 0, 0, cur_big, g_start, g_len, 2);
+        if (rc != GK_OK) return rc;
+        rc = levels(1, 0, 0);
+        if (rc != GK_OK) return rc;
+        return finish();
+    }
+
     // before another global level: its buckets whose keys are all equal go to the done list
     // (checked once the big buckets hold few elements: after L1 of a random genome they hold
     // all of them and never are)
@@ -3297,6 +3334,25 @@ int msd_sort_keys(gk_ctx *c, int total_bits) {
     if (rc == GK_OK) rc = d.levels(0, 0, in);
     if (rc == GK_OK) rc = d.finish();
     c->cur = 0;
+    timer_end(c, d.total_slot);
+    return rc;
+}
+
+// sort_doubling's rounds: the tied groups of keys[0] / vals[0] (flags: 1 starts a group) sorted by
+// their bkey-bit keys (MsdDriver::sort_groups)
+int msd_sort_groups(gk_ctx *c, const uint8_t *flags, int bkey) {
+    KeySpec kk{};
+    kk.bits = 8;
+    kk.symbols = (bkey + 7) / 8;
+    kk.min_len = 1;
+    kk.words = 1;
+    kk.total_bits = bkey;
+    MsdDriver d(c, kk);
+    d.B = bkey;
+    d.wkeys = 1;
+    timer_begin(c, "msd_groups", &d.total_slot);
+    int rc = d.init(c->n);
+    if (rc == GK_OK) rc = d.sort_groups(flags, bkey);
     timer_end(c, d.total_slot);
     return rc;
 }

@@ -801,3 +801,23 @@ def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
     rep = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), 3000).astype(np.uint8)
     oracle_check(random_genome(rng, [60_000, 20_000, 7_000, 40], alphabet=alphabet, repeat=rep, copies=3),
                  min_k, max_k)
+
+
+# user-provided starts under max_kmer_len=None: the doubling ranks every position, then sorts the
+# given starts by their final rank (the non-enumerated branch), on the tied-group MSD path
+@pytest.mark.parametrize("path", ["msd", "lsd"])
+def test_doubling_user_starts_vs_oracle(path, monkeypatch):
+    if path == "msd":
+        monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")
+    else:
+        monkeypatch.setenv("GKM_SORT_KEYS_LSD", "1")
+    rng = np.random.default_rng(77)
+    rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 2000).astype(np.uint8)
+    seqs = random_genome(rng, [30_000, 9_000, 300], repeat=rep, copies=4)
+    sc = SequenceCollection(sequence_list=seqs)
+    km = gk.Kmers(sc, min_kmer_len=3, max_kmer_len=None)
+    user = rng.permutation(km.kmer_sba_start_indices)[:15_000].astype(km.kmer_sba_start_indices.dtype)
+    km.kmer_sba_start_indices = user.copy()
+    km.sort()
+    want = oracle.quicksort(sc.forward_sba, np.sort(user, kind="stable"), 3, None, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)

@@ -2,7 +2,7 @@
 # then the reference's profiled workload (max 20 / None) against the LSD passes (GKM_SORT_KEYS_LSD=1)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -k "${TESTS_K:-not nothing}" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
 rm -f gpurun_out/keys_ab.txt
 for mx in 20 none; do

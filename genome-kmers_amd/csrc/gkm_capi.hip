@@ -75,15 +75,6 @@ void timer_units(gk_ctx *c, int slot, uint64_t units) {
 // ---------------------------------------------------------------------------------------------
 // prefix-doubling kernels
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t seg_end_of(const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
-                                               uint64_t p) {
-    uint32_t lo = 0, hi = nseg;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((uint64_t)seg[mid] <= p) lo = mid; else hi = mid;
-    }
-    return (lo + 1 == nseg) ? L - 1 : (uint64_t)seg[lo + 1] - 2;
-}
 
 // R[vals[i]] = gstart[gid[i] - 1] + 1   (rank = 1 + index of the group's first element)
 __global__ __launch_bounds__(256) void rank_scatter_kernel(const uint32_t *__restrict__ vals,
@@ -752,8 +743,8 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     const bool bounded = M != 0;
     bool done = bounded && h >= M;  // (direct path covers M <= capacity; keep for safety)
     if (by_groups && c->cur == 0) {
-        // flags of the current groups (fa), the next round's (fb); ranks of every position in R,
-        // scattered once and then only for the elements a round re-sorts
+        // flags of the current groups (fa), the next round's (fb); ranks of every position in R from
+        // the second round on (scattered once, then only for the elements a round re-sorts)
         uint8_t *fa = c->flags, *fb;
         GK_TRY_HIP(c, scratch(c, "dbl_flags", n1 + 64, &fb));
         hipLaunchKernelGGL(full_key_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->keys[0], n1, fa);
@@ -761,10 +752,9 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
         uint64_t G = 0;
         GK_TRY_HIP(c, select_flags(c, fa, n1, c->idx_b, &G));
         GK_TRY_HIP(c, scan_flags_inclusive(c, fa, n1, c->idx_a));
-        GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
-        GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[0], c->idx_a, c->idx_b, n1, c->ranks));
         const int bw = std::max(1, bit_width(n1));  // ranks: group start + 1 <= n1 (0: past the segment's end)
-        while (!done) {
+        bool ranks_ready = false;  // every position ranked (from the second round on)
+        for (int round = 0; !done; ++round) {
             if (G == n1) break;                          // all distinct
             if (!bounded && h >= c->max_seg_len) break;  // every suffix ends within h symbols
             {  // every tied group already holds equal k-mers (shared contig tails): done
@@ -778,18 +768,33 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
                 if (cnt == 0) break;
             }
             const uint64_t o = bounded ? std::min<uint64_t>(h, M - h) : h;
-            hipLaunchKernelGGL(member_r2_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0], c->ranks,
-                               c->seg, (uint32_t)c->nseg, L, o, n1, c->keys[0]);
-            GK_TRY_HIP(c, hipGetLastError());
-            rc = msd_sort_groups(c, fa, bw);
+            int bkey = bw;
+            if (round == 0 && o == (uint64_t)seed.symbols) {
+                // the rank of p + o after the seed sort orders like the seed key of p + o: the tied
+                // elements read it from their windows, and no position needs ranking yet
+                GK_TRY_HIP(c, launch_member_seed_keys(c, seed, fa, c->vals[0], o, n1, c->keys[0]));
+                bkey = seed.total_bits;
+            } else {
+                if (!ranks_ready) {  // every position ranked by the order so far, once
+                    GK_TRY_HIP(c, hipMemsetAsync(c->ranks, 0, 4 * (L + 64), c->stream));
+                    GK_TRY_HIP(c, launch_rank_scatter(c, c->vals[0], c->idx_a, c->idx_b, n1, c->ranks));
+                    ranks_ready = true;
+                }
+                hipLaunchKernelGGL(member_r2_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0],
+                                   c->ranks, c->seg, (uint32_t)c->nseg, L, o, n1, c->keys[0]);
+                GK_TRY_HIP(c, hipGetLastError());
+            }
+            rc = msd_sort_groups(c, fa, bkey);
             if (rc != GK_OK) return rc;
             hipLaunchKernelGGL(merge_heads_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->heads, n1, fb);
             GK_TRY_HIP(c, hipGetLastError());
             GK_TRY_HIP(c, select_flags(c, fb, n1, c->idx_b, &G));
             GK_TRY_HIP(c, scan_flags_inclusive(c, fb, n1, c->idx_a));
-            hipLaunchKernelGGL(member_rank_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0],
-                               c->idx_a, c->idx_b, n1, c->ranks);
-            GK_TRY_HIP(c, hipGetLastError());
+            if (ranks_ready) {  // (else ranked from the current order when a round needs it)
+                hipLaunchKernelGGL(member_rank_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, fa, c->vals[0],
+                                   c->idx_a, c->idx_b, n1, c->ranks);
+                GK_TRY_HIP(c, hipGetLastError());
+            }
             std::swap(fa, fb);
             h += o;
             if (bounded && h >= M) done = true;

@@ -932,6 +932,48 @@ hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys,
                    : dispatch_generic_w<4, false>(c, k, keys, vals, hist, grid);
 }
 
+// sort_doubling's first round: the rank of p + o after the seed sort orders like the seed key of
+// p + o, so the tied elements take that key from their window instead of every position being
+// ranked first (a random 4-byte scatter per position)
+template <int BITS>
+__global__ __launch_bounds__(256) void member_seed_key_kernel(const uint8_t *__restrict__ sba, KS ks,
+                                                              const uint8_t *__restrict__ flags,
+                                                              const uint32_t *__restrict__ vals,
+                                                              const uint32_t *__restrict__ seg, uint32_t nseg,
+                                                              uint64_t L, uint64_t o, uint64_t n,
+                                                              uint64_t *__restrict__ keys) {
+    __shared__ uint8_t s_lut4[256];
+    s_lut4[threadIdx.x] = c_code4[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (flags[i] != 0 && (i + 1 >= n || flags[i + 1] != 0)) continue;  // a group of one
+        const uint64_t p = vals[i];
+        const uint64_t q = p + o;
+        if (q > seg_end_of(seg, nseg, L, p)) {
+            keys[i] = 0;
+            continue;
+        }
+        uint64_t w[1];
+        window_key<1, BITS, true>(ks, [&](int k) { return (uint32_t)sba[q + k]; }, s_lut4, w);
+        keys[i] = w[0];
+    }
+}
+
+hipError_t launch_member_seed_keys(gk_ctx *c, const KeySpec &seed, const uint8_t *flags, const uint32_t *vals,
+                                   uint64_t o, uint64_t n, uint64_t *keys) {
+    hipError_t e = init_tables();
+    if (e != hipSuccess) return e;
+    const KS k = pod(seed);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+    if (seed.bits == 3)
+        hipLaunchKernelGGL(member_seed_key_kernel<3>, dim3(grid), dim3(256), 0, c->stream, c->sba, k, flags, vals, c->seg,
+                           (uint32_t)c->nseg, (uint64_t)c->sba_len, o, n, keys);
+    else
+        hipLaunchKernelGGL(member_seed_key_kernel<4>, dim3(grid), dim3(256), 0, c->stream, c->sba, k, flags, vals, c->seg,
+                           (uint32_t)c->nseg, (uint64_t)c->sba_len, o, n, keys);
+    return hipGetLastError();
+}
+
 template <int W, int BITS, bool BOUNDED>
 static hipError_t gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys) {
     int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);

@@ -261,6 +261,21 @@ int sort_keys(gk_ctx *c, int words, int total_bits, bool hist_ready);
 bool sort_keys_msd(const gk_ctx *c, uint64_t n, int words, int total_bits);  // sort_keys takes the MSD path
 // prefix doubling: the tied groups (flags: 1 starts a group) of keys[0] / vals[0] sorted by bkey-bit keys
 int msd_sort_groups(gk_ctx *c, const uint8_t *flags, int bkey);
+// prefix doubling's first round: the seed key (`seed`, as launch_encode_positions) of position
+// vals[i] + o for the elements still tied (flags: 1 starts a group), 0 past the segment's end
+hipError_t launch_member_seed_keys(gk_ctx *c, const KeySpec &seed, const uint8_t *flags, const uint32_t *vals,
+                                   uint64_t o, uint64_t n, uint64_t *keys);
+
+// last position of the segment holding p (seg: segment starts, '$' between segments)
+__device__ __forceinline__ uint64_t seg_end_of(const uint32_t *__restrict__ seg, uint32_t nseg, uint64_t L,
+                                               uint64_t p) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)seg[mid] <= p) lo = mid; else hi = mid;
+    }
+    return (lo + 1 == nseg) ? L - 1 : (uint64_t)seg[lo + 1] - 2;
+}
 constexpr uint64_t kMsdKeysMin = 1ull << 20;
 
 // group / scan

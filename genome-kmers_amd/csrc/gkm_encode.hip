@@ -319,6 +319,90 @@ __global__ __launch_bounds__(256) void encode_roll_w1_kernel(const uint8_t *__re
 }
 
 // ---------------------------------------------------------------------------------------------
+// bounded variable-length keys of one word (2-bit ACGT with a length field, the 3-bit doubling
+// seeds), rolling: thread t rolls the raw window over positions 16t .. 16t+15 as encode_roll_w1
+// does, and a '$' bitmask of its bytes gives each position's first '$' -- the symbols from it on
+// are zeroed and the length field is min(len, symbols), window_key's encoding (sort_keys' MSD path:
+// no digit histograms).  The per-position byte loop of encode_generic_kernel ran 1.05 ms for 1e8
+// positions of the reference's profiling workload.
+// ---------------------------------------------------------------------------------------------
+template <int BITS>
+__global__ __launch_bounds__(256) void encode_roll_bounded_kernel(const uint8_t *__restrict__ sba, uint64_t L,
+                                                                  const uint32_t *__restrict__ seg, uint32_t nseg,
+                                                                  KS ks, uint64_t *__restrict__ keys,
+                                                                  uint32_t *__restrict__ vals) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kEncodeTile + 256];
+    __shared__ uint64_t s_keys[kRollR * kRollPitch];
+    __shared__ uint32_t s_vmask[256];
+    __shared__ uint32_t s_tile_seg, s_tile_has_dollar;
+    const int t = threadIdx.x;
+    const int S = ks.symbols;  // <= 32 (the caller checks)
+    const uint64_t symmask = BITS * S >= 64 ? ~0ull : ((1ull << (BITS * S)) - 1);
+    const uint64_t ntiles = (L + kEncodeTile - 1) / kEncodeTile;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t P0 = tile * kEncodeTile;
+        __syncthreads();
+        {
+            const uint4 *src = reinterpret_cast<const uint4 *>(sba + P0);
+            uint4 *dst = reinterpret_cast<uint4 *>(s_bytes);
+            dst[t] = src[t];
+            if (t < 16) dst[256 + t] = src[256 + t];
+        }
+        if (t == 0) {
+            s_tile_seg = seg_of(seg, nseg, P0);
+            s_tile_has_dollar = 0;
+        }
+        __syncthreads();
+        {
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_bytes);
+            bool d = false;
+            for (int i = t; i < (kEncodeTile + 256) / 4; i += 256) {
+                uint32_t v = w32[i] ^ 0x24242424u;  // zero byte where '$'
+                d |= ((v - 0x01010101u) & ~v & 0x80808080u) != 0;
+            }
+            if (__any(d) && (t & 63) == 0) s_tile_has_dollar = 1;
+        }
+        {
+            const int q0 = t * kRollR;
+            const int span = S - 1 + kRollR;  // <= 47 bytes
+            uint64_t dm = 0;                  // bit i: byte q0 + i is '$'
+            uint64_t raw = 0;
+            uint32_t vm = 0;
+            for (int i = 0; i < span; ++i) {
+                const uint32_t ch = s_bytes[q0 + i];
+                if (ch == GK_DOLLAR) dm |= 1ull << i;
+                raw = ((raw << BITS) | sym_code<BITS>(ch, nullptr)) & symmask;
+                const int j = i - (S - 1);
+                if (j >= 0) {
+                    const uint64_t dj = dm >> j;  // '$' at window offsets
+                    const int first = dj ? min(S, (int)__builtin_ctzll(dj)) : S;
+                    uint64_t k = first < S ? raw & ~((1ull << (BITS * (S - first))) - 1) : raw;
+                    if (ks.lenbits > 0) k = (k << ks.lenbits) | (uint64_t)first;
+                    s_keys[j * kRollPitch + t] = k;
+                    if (first >= ks.min_len) vm |= 1u << j;
+                }
+            }
+            s_vmask[t] = vm;
+        }
+        __syncthreads();
+        const bool has_dollar = s_tile_has_dollar != 0;
+        const uint32_t tseg = s_tile_seg;
+#pragma unroll 4
+        for (int i = 0; i < kRollR; ++i) {
+            const int q = t + 256 * i;
+            const int owner = q >> 4, j = q & 15;
+            const uint64_t p = P0 + q;
+            if (((s_vmask[owner] >> j) & 1u) && p < L) {
+                const uint32_t sg = has_dollar ? seg_of(seg, nseg, p) : tseg;
+                const uint64_t o = p - (uint64_t)ks.min_len * sg;
+                keys[o] = s_keys[j * kRollPitch + owner];
+                vals[o] = (uint32_t)p;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // generic encode over positions: any width W, bounded (padded) keys; one key per thread from LDS
 // ---------------------------------------------------------------------------------------------
 template <int W, int BITS, bool BOUNDED>
@@ -923,6 +1007,17 @@ hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys,
         else
             hipLaunchKernelGGL(encode_roll_w1_kernel<4>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
                                c->seg, (uint32_t)c->nseg, k, keys, vals, hist);
+        return hipGetLastError();
+    }
+    static const bool no_roll = std::getenv("GKM_NO_ROLL_BOUNDED") != nullptr;  // (A/B)
+    if (bounded && hist == nullptr && ks.words == 1 && (ks.bits == 2 || ks.bits == 3) && ks.symbols <= 32 &&
+        ks.min_len >= 1 && !no_roll) {
+        if (ks.bits == 2)
+            hipLaunchKernelGGL(encode_roll_bounded_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
+                               c->seg, (uint32_t)c->nseg, k, keys, vals);
+        else
+            hipLaunchKernelGGL(encode_roll_bounded_kernel<3>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
+                               c->seg, (uint32_t)c->nseg, k, keys, vals);
         return hipGetLastError();
     }
     if (ks.bits == 2) return bounded ? dispatch_generic_w<2, true>(c, k, keys, vals, hist, grid)

@@ -791,7 +791,8 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
 # GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes
 @pytest.mark.parametrize("path", ["msd", "lsd"])
 @pytest.mark.parametrize("alphabet,min_k,max_k", [(b"ACGT", 5, 20), (b"ACGT", 1, None), (b"ACGTNRYKM", 3, 12),
-                                                  (b"ACGTN", 2, None), (b"AC", 4, 29)])
+                                                  (b"ACGTN", 2, None), (b"AC", 4, 29), (b"ACGT", 1, 50),
+                                                  (b"ACGT", 1, 10)])
 def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
     if path == "msd":
         monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")

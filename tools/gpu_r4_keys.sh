@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -k "${TESTS_K:-not nothing}" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
 rm -f gpurun_out/keys_ab.txt
-for mx in 20 none; do
+for mx in 10 20 50 none; do
   for v in "GKM_SORT_KEYS_LSD=1" "GKM_X=0"; do
     env $v timeout -k 10 300 python -u bench.py --config ref_profile --max-kmer-len $mx --no-cpu-baseline > gpurun_out/keys_one.json 2> gpurun_out/keys_one.err || { tail -20 gpurun_out/keys_one.err; exit 1; }
     python3 - "$mx $v" >> gpurun_out/keys_ab.txt <<'PY'

@@ -373,13 +373,39 @@ def run_ref_profile(args, torch, result_out, log):
     eng.profile_enable(False)
     checked = order_check(eng, sba, M)
     words, bits, _ = eng.key_layout()
-    # dominant kernel: the LSD onesweep pass (every radix_pass launch: keys W words + start in and out)
-    rp = report.get("radix_pass", {"count": 0, "total_ms": 0.0, "units": 0})
-    per_unit = 2 * (8 * max(words, 1) + 4)
+    stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
+    msd = "radix_pass" not in report and any(k.startswith("msd_") for k in report)
+    if not msd:
+        # dominant kernel: the LSD onesweep pass (every radix_pass launch: keys W words + start in and out)
+        rp = report.get("radix_pass", {"count": 0, "total_ms": 0.0, "units": 0})
+        per_unit = 2 * (8 * max(words, 1) + 4)
+        kernel = f"onesweep_kernel (W = {max(words, 1)}; radix_pass: one stable 8-bit LSD pass with decoupled look-back)"
+    else:
+        # the MSD levels over the keys (sort_keys, gkm_sort.hip): the stage with the most time among
+        # the level partitions and the finishing kernels, priced as in the C3 model (run())
+        compact_in = any(k.startswith("msd_pass_l") and k.endswith("c") for k in report)
+        pairs_in = any(k.startswith("msd_pass_l") and k.endswith("p") for k in report)
+
+        def unit_bytes(name):
+            if name.startswith("msd_pass_l") and name.endswith("c"):
+                return 19 if pairs_in else 21
+            if name.startswith("msd_pass_l") and name.endswith("p"):
+                return 23
+            if name.startswith("msd_pass_l"):
+                return 24
+            if name.startswith("msd_local"):
+                return 22 if compact_in else 25
+            return 0
+
+        timed = {k: v for k, v in report.items() if unit_bytes(k) and v["total_ms"] > 0 and v.get("units", 0)}
+        dom = max(timed, key=lambda k: timed[k]["total_ms"]) if timed else None
+        rp = timed.get(dom, {"count": 0, "total_ms": 0.0, "units": 0})
+        per_unit = unit_bytes(dom) if dom else 0
+        kernel = (f"{WAVE8_KERNEL if dom == 'msd_local_wave8' else 'msd_pipe_kernel<1024,11,R>'} ({dom}: "
+                  f"MSD levels over the keys in memory)")
     avg_ms = rp["total_ms"] / max(rp["count"], 1)
     units = rp["units"] / max(rp["count"], 1)
     achieved = per_unit * units / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
     cpu = None
     if not args.no_cpu_baseline:
         # DRAM regime: 2M starts spread over the whole sba (every position outside '$' is a start)
@@ -412,12 +438,14 @@ def run_ref_profile(args, torch, result_out, log):
         "self_check": f"{checked:,} sorted k-mers in windows re-checked against the sba bytes",
         "config": {"workload": f"ref_profile: {args.ref_bases:,} bases in 10 contigs, min_kmer_len=1, "
                                f"max_kmer_len={M}", "kmers": n,
-                   "sort_path": "LSD onesweep over (2-bit padded, length) keys" if M is not None and bits else
-                                "prefix doubling (seed keys, then rank pairs)",
+                   "sort_path": (("MSD levels over" if msd else "LSD onesweep over") + " (2-bit padded, length) keys")
+                                if M is not None and bits else
+                                ("prefix doubling: seed keys (MSD), then the tied groups by the rank of p + h"
+                                 if msd else "prefix doubling (seed keys, then rank pairs, LSD)"),
                    "key_words": words, "key_bits": bits, "stages_ms_per_step": stages},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": f"onesweep_kernel (W = {max(words, 1)}; radix_pass: one stable 8-bit LSD pass with decoupled look-back)",
+                     "kernel": kernel,
                      "avg_launch_ms": round(avg_ms, 4), "launches_per_step": round(rp["count"] / args.steps, 2),
                      "units_per_launch": int(units), "bytes_per_unit": per_unit},
         "cpu_baseline": cpu,
@@ -598,7 +626,7 @@ def main():
     wide = "msd_local_block32" in report  # the 11-bit L0 leaves ~5.9 K-key buckets for the 1024-thread class
     kinds = {"msd_pass_l0": (("msd0_wide_kernel<512,36,11,true>", "the 11-bit L0 partition, straight from the "
                               "sequence") if wide else
-                             ("msd0_pipe_kernel<2,1024,18,7,true>", "the L0 partition, straight from the sequence")),
+                             ("msd0_pipe_kernel<2,1024,24,7,true>", "the L0 partition, straight from the sequence")),
              "msd_local_wave8": (WAVE8_KERNEL, "wave-local finishing of buckets <= 512"),
              "msd_local_block32": ("msd_local_kernel<1024,8,10>", "block-local finishing of buckets <= 8192")}
     timed = {n: v for n, v in report.items() if stage_bytes(n, v) and v["total_ms"] > 0 and

@@ -342,8 +342,8 @@ def run_ref_profile(args, torch, result_out, log):
     """The reference's own profiled sort workload (tools/run_profiling.py:226-236, profiling.py:367-448):
     Kmers(min_kmer_len=1, max_kmer_len=M).sort() over 1e8 bases in 10 contigs, seed 42.  A step is
     enumerate + sort, the call the reference times (run_kmers_sort).  M = 20: bounded variable-length
-    keys (2-bit padded symbols + length, 45 bits) through the LSD onesweep; M = None (the Kmers
-    default): prefix doubling."""
+    keys (2-bit padded symbols + length, 45 bits) through the MSD levels over the keys (the LSD onesweep
+    with GKM_SORT_KEYS_LSD=1); M = None (the Kmers default): prefix doubling."""
     from genome_kmers import _native
     from oracle import oracle
 

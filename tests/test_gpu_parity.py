@@ -822,3 +822,17 @@ def test_doubling_user_starts_vs_oracle(path, monkeypatch):
     km.sort()
     want = oracle.quicksort(sc.forward_sba, np.sort(user, kind="stable"), 3, None, break_ties=True)
     np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+
+
+# the golden cases again with the large-array routes forced at their sizes (GKM_MSD_KEYS_MIN=2):
+# MSD levels over the keys, doubling by tied groups, and bounded keys of two or more words through
+# capped doubling (keys become ranks) -- sorted starts and every query against the reference's
+# answers
+@pytest.mark.parametrize("case", CASES, ids=CASE_IDS)
+def test_golden_on_large_array_routes(case, monkeypatch):
+    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    km, a = make(case)
+    km.sort()
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, a["starts_stable"])
+    for q, want in zip(case["queries"], case["results_stable_order"]):
+        assert run_query(km, q) == want, q

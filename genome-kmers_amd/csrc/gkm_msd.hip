@@ -1805,7 +1805,9 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_kernel(const uint2 *__restr
 // without its ranking -- the same list walk, loads (compact entries unpacked) and software
 // pipelining, then keys, starts and head flags stored straight from registers in load order.
 // Its time is the floor of msd_wave_kernel's bucket-granular access pattern.
-template <int I, int MINW>
+// HS: head flags stored per element (0), per aligned 4-flag chunk as one dword (1, edge chunks
+// per byte), or not at all (2) -- the store pattern's share of the floor
+template <int I, int MINW, int HS = 0>
 __global__ __launch_bounds__(64, MINW) void msd_wave_copy_kernel(const uint2 *__restrict__ list, uint32_t count, int B,
                                                            uint64_t *k0, uint32_t *v0, const uint64_t *k1,
                                                            const uint32_t *v1, uint8_t *__restrict__ heads,
@@ -1849,7 +1851,21 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_copy_kernel(const uint2 *__
             const uint32_t j = min((uint32_t)(i * 64 + lane), len - 1);
             gmem(k0)[st + j] = key[i];
             gmem(v0)[st + j] = val[i];
-            gmem(heads)[st + j] = 1;
+            if (HS == 0) gmem(heads)[st + j] = 1;
+        }
+        if (HS == 1) {
+            const uint64_t a0 = st & ~3ull, end = st + len;
+#pragma unroll
+            for (int r = 0; r < (64 * I + 8) / 256 + 1; ++r) {
+                const uint64_t p = a0 + 4ull * (r * 64 + lane);
+                if (p >= end) continue;
+                if (p >= st && p + 4 <= end) {
+                    gmem(reinterpret_cast<uint32_t *>(heads + p))[0] = 0x01010101u;
+                } else {
+                    for (int t = 0; t < 4; ++t)
+                        if (p + t >= st && p + t < end) gmem(heads)[p + t] = 1;
+                }
+            }
         }
         idx += lstep;
         if (idx >= lend) break;
@@ -3107,6 +3123,18 @@ struct MsdDriver {
             if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '2') {  // timing only
                 hipLaunchKernelGGL((msd_wave_copy2_kernel<8, kWaveOcc8>),
                                    grid((const void *)msd_wave_copy2_kernel<8, kWaveOcc8>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
+                break;
+            }
+            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '3') {  // timing only
+                hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8, 1>),
+                                   grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8, 1>, 64), dim3(64), 0,
+                                   c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
+                break;
+            }
+            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '4') {  // timing only
+                hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8, 2>),
+                                   grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8, 2>, 64), dim3(64), 0,
                                    c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
                 break;
             }

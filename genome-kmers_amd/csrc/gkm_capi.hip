@@ -837,7 +837,11 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
         if (bounded && h >= M) done = true;
     }
 
-    if (was_enumerated) {
+    if (was_enumerated && n_kmers == n1) {
+        // every position of the universe has >= m bases (m = 1, or no shorter tails): the order is
+        // already the k-mers' order, in place
+        c->n = n1;
+    } else if (was_enumerated) {
         // keep starts with >= m bases, in order
         hipLaunchKernelGGL(len_flags_kernel, dim3(grid_of(n1)), dim3(256), 0, c->stream, c->vals[c->cur], c->seg,
                            (uint32_t)c->nseg, L, (uint64_t)m, n1, c->flags);

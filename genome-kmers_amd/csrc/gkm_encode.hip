@@ -326,16 +326,23 @@ __global__ __launch_bounds__(256) void encode_roll_w1_kernel(const uint8_t *__re
 // no digit histograms).  The per-position byte loop of encode_generic_kernel ran 1.05 ms for 1e8
 // positions of the reference's profiling workload.
 // ---------------------------------------------------------------------------------------------
-template <int BITS>
+// HIST: the LSD sort's digit histograms of the stored keys as well (ks.digits of them; LDS counts
+// flushed once per workgroup), in place of encode_generic_kernel's for the LSD route
+template <int BITS, bool HIST>
 __global__ __launch_bounds__(256) void encode_roll_bounded_kernel(const uint8_t *__restrict__ sba, uint64_t L,
                                                                   const uint32_t *__restrict__ seg, uint32_t nseg,
                                                                   KS ks, uint64_t *__restrict__ keys,
-                                                                  uint32_t *__restrict__ vals) {
+                                                                  uint32_t *__restrict__ vals,
+                                                                  uint32_t *__restrict__ ghist) {
     __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kEncodeTile + 256];
     __shared__ uint64_t s_keys[kRollR * kRollPitch];
     __shared__ uint32_t s_vmask[256];
     __shared__ uint32_t s_tile_seg, s_tile_has_dollar;
+    __shared__ uint32_t s_hist[HIST ? 8 * 256 : 1];
     const int t = threadIdx.x;
+    const int D = HIST ? ks.digits : 0;  // <= 8 (one word)
+    if (HIST)
+        for (int i = t; i < D * 256; i += 256) s_hist[i] = 0;
     const int S = ks.symbols;  // <= 32 (the caller checks)
     const uint64_t symmask = BITS * S >= 64 ? ~0ull : ((1ull << (BITS * S)) - 1);
     const uint64_t ntiles = (L + kEncodeTile - 1) / kEncodeTile;
@@ -395,9 +402,19 @@ __global__ __launch_bounds__(256) void encode_roll_bounded_kernel(const uint8_t 
             if (((s_vmask[owner] >> j) & 1u) && p < L) {
                 const uint32_t sg = has_dollar ? seg_of(seg, nseg, p) : tseg;
                 const uint64_t o = p - (uint64_t)ks.min_len * sg;
-                keys[o] = s_keys[j * kRollPitch + owner];
+                const uint64_t key = s_keys[j * kRollPitch + owner];
+                keys[o] = key;
                 vals[o] = (uint32_t)p;
+                if (HIST)
+                    for (int d = 0; d < D; ++d) atomicAdd(&s_hist[d * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
             }
+        }
+    }
+    if (HIST) {
+        __syncthreads();
+        for (int i = t; i < D * 256; i += 256) {
+            const uint32_t v = s_hist[i];
+            if (v) atomicAdd(&ghist[i], v);
         }
     }
 }
@@ -1010,14 +1027,17 @@ hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys,
         return hipGetLastError();
     }
     static const bool no_roll = std::getenv("GKM_NO_ROLL_BOUNDED") != nullptr;  // (A/B)
-    if (bounded && hist == nullptr && ks.words == 1 && (ks.bits == 2 || ks.bits == 3) && ks.symbols <= 32 &&
-        ks.min_len >= 1 && !no_roll) {
+    static const bool no_roll_hist = std::getenv("GKM_NO_ROLL_HIST") != nullptr;  // (A/B)
+    if (bounded && (hist == nullptr || (!no_roll_hist && k.digits <= 8)) && ks.words == 1 &&
+        (ks.bits == 2 || ks.bits == 3) && ks.symbols <= 32 && ks.min_len >= 1 && !no_roll) {
+        auto go = [&](auto fn) {
+            hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len, c->seg, (uint32_t)c->nseg,
+                               k, keys, vals, hist);
+        };
         if (ks.bits == 2)
-            hipLaunchKernelGGL(encode_roll_bounded_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
-                               c->seg, (uint32_t)c->nseg, k, keys, vals);
+            hist ? go(encode_roll_bounded_kernel<2, true>) : go(encode_roll_bounded_kernel<2, false>);
         else
-            hipLaunchKernelGGL(encode_roll_bounded_kernel<3>, dim3(grid), dim3(256), 0, c->stream, c->sba, c->sba_len,
-                               c->seg, (uint32_t)c->nseg, k, keys, vals);
+            hist ? go(encode_roll_bounded_kernel<3, true>) : go(encode_roll_bounded_kernel<3, false>);
         return hipGetLastError();
     }
     if (ks.bits == 2) return bounded ? dispatch_generic_w<2, true>(c, k, keys, vals, hist, grid)

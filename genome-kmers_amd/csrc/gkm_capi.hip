@@ -719,13 +719,18 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->idx_b), &c->idx_b_cap, 4 * (n1 + 64)));
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->ranks), &c->ranks_cap, 4 * (L + 64)));
 
+    // seed keys: ACGT data as 29 symbols of 2 bits + a 5-bit length field (the (padded, length)
+    // keys of the bounded sort: the same order as '$'-terminated 3-bit codes, 29 symbols instead of
+    // 21, and every key bit carries information for the MSD levels; GKM_SEED3=1 keeps the 3-bit
+    // seeds); other data as 16 symbols of 4 bits
+    static const bool seed3 = std::getenv("GKM_SEED3") != nullptr;
     KeySpec seed{};
-    seed.bits = c->acgt ? 3 : 4;
-    seed.symbols = c->acgt ? 21 : 16;
-    seed.lenbits = 0;
+    seed.bits = c->acgt ? (seed3 ? 3 : 2) : 4;
+    seed.symbols = c->acgt ? (seed3 ? 21 : 29) : 16;
+    seed.lenbits = seed.bits == 2 ? bit_width((uint64_t)seed.symbols) : 0;
     seed.min_len = 1;
     seed.words = 1;
-    seed.total_bits = seed.bits * seed.symbols;
+    seed.total_bits = seed.bits * seed.symbols + seed.lenbits;
     c->n = n1;
     c->cur = 0;
     int slot;
@@ -769,9 +774,10 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
             }
             const uint64_t o = bounded ? std::min<uint64_t>(h, M - h) : h;
             int bkey = bw;
-            if (round == 0 && o == (uint64_t)seed.symbols) {
-                // the rank of p + o after the seed sort orders like the seed key of p + o: the tied
-                // elements read it from their windows, and no position needs ranking yet
+            if (round == 0) {
+                // the rank of p + o after the seed sort (h = seed.symbols) orders like the seed key
+                // of p + o, whatever o is: the tied elements read it from their windows, and no
+                // position needs ranking yet
                 GK_TRY_HIP(c, launch_member_seed_keys(c, seed, fa, c->vals[0], o, n1, c->keys[0]));
                 bkey = seed.total_bits;
             } else {

@@ -1080,7 +1080,10 @@ hipError_t launch_member_seed_keys(gk_ctx *c, const KeySpec &seed, const uint8_t
     if (e != hipSuccess) return e;
     const KS k = pod(seed);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
-    if (seed.bits == 3)
+    if (seed.bits == 2)
+        hipLaunchKernelGGL(member_seed_key_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, k, flags, vals, c->seg,
+                           (uint32_t)c->nseg, (uint64_t)c->sba_len, o, n, keys);
+    else if (seed.bits == 3)
         hipLaunchKernelGGL(member_seed_key_kernel<3>, dim3(grid), dim3(256), 0, c->stream, c->sba, k, flags, vals, c->seg,
                            (uint32_t)c->nseg, (uint64_t)c->sba_len, o, n, keys);
     else

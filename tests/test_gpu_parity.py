@@ -788,11 +788,14 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
 
 # Whole-array sorts of encoded keys (bounded variable length, IUPAC 4-bit keys, the prefix-doubling
 # seeds and rank pairs) take the MSD levels over the keys from 2^20 keys on (msd_sort_keys);
-# GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes
+# GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes.
+# Bounds of 30..64 on ACGT data take the capped doubling, whose first round shifts by
+# min(29, max - 29) and reads seed keys of p + shift (the 3000-base repeats keep groups tied)
 @pytest.mark.parametrize("path", ["msd", "lsd"])
 @pytest.mark.parametrize("alphabet,min_k,max_k", [(b"ACGT", 5, 20), (b"ACGT", 1, None), (b"ACGTNRYKM", 3, 12),
                                                   (b"ACGTN", 2, None), (b"AC", 4, 29), (b"ACGT", 1, 50),
-                                                  (b"ACGT", 1, 10)])
+                                                  (b"ACGT", 1, 10), (b"ACGT", 1, 30), (b"AC", 2, 41),
+                                                  (b"ACGT", 3, 64)])
 def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
     if path == "msd":
         monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")

@@ -3,7 +3,7 @@
 // Sort strategies:
 //   direct   max_kmer_len given and the padded key fits 256 bits: encode once, LSD radix sort.
 //   doubling max_kmer_len None (suffix order up to '$', the Kmers default) or a very long bound:
-//            prefix doubling over every sba position -- seed keys of 21 (ACGT) / 16 (IUPAC)
+//            prefix doubling over every sba position -- seed keys of 29 (ACGT, 2 bits + length) / 16 (IUPAC)
 //            symbols, then rounds of (rank[p], rank[p + h]) 64-bit keys, each a stable radix sort --
 //            and finally the starts with >= min_kmer_len bases are kept, in order.
 #include <algorithm>

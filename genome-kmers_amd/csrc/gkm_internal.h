@@ -38,7 +38,7 @@ constexpr int kScanTile = kScanThreads * kScanItems;
 
 // How a k-mer is turned into an order-preserving integer key:
 //   bits   2: A,C,G,T -> 0..3 (sba holds only ACGT)
-//          3: '$'/end -> 0, A,C,G,T -> 1..4 (doubling seeds on ACGT data)
+//          3: '$'/end -> 0, A,C,G,T -> 1..4 (doubling seeds on ACGT data under GKM_SEED3=1)
 //          4: '$'/end -> 0, A B C D G H K M N R S T V W Y -> 1..15 (IUPAC data)
 //   symbols  number of leading symbols encoded (= max_kmer_len for direct keys)
 //   lenbits  2-bit keys of variable length append min(len, symbols) in the low lenbits bits

@@ -687,6 +687,7 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
         if (rc != GK_OK) return rc;
         int slot;
         timer_begin(c, "encode", &slot);
+        timer_units(c, slot, c->n);
         GK_TRY_HIP(c, launch_encode_gather(c, ks, c->vals[c->cur], c->n, c->keys[c->cur]));
         timer_end(c, slot);
     }
@@ -738,6 +739,7 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     // re-sort the whole array by rank pairs each round (LSD)
     const bool by_groups = sort_keys_msd(c, n1, 1, 64) && std::getenv("GKM_DOUBLING_FULL") == nullptr;
     timer_begin(c, "encode", &slot);
+    timer_units(c, slot, n1);
     const bool seed_hist = !sort_keys_msd(c, n1, 1, seed.total_bits);
     GK_TRY_HIP(c, launch_encode_positions(c, seed, c->keys[0], c->vals[0], seed_hist ? c->hist : nullptr));
     timer_end(c, slot);
@@ -892,30 +894,62 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
 }
 
 namespace gkm {
-int quicksort_by_rank(uint32_t *A, uint64_t n, const uint32_t *rank_of_pos);  // gkm_qsort.cpp
+int quicksort_by_rank(uint64_t *A, uint64_t n);  // gkm_qsort.cpp
+
+// GK_SORT_QUICKSORT_ORDER helpers: the dense group rank of sorted element i is the last group
+// whose first sorted index is <= i (binary search over the G group starts), scattered to its start
+__global__ __launch_bounds__(256) void qs_rank_scatter_kernel(const uint32_t *__restrict__ S, uint64_t n,
+                                                              const uint32_t *__restrict__ gs, uint64_t G,
+                                                              uint32_t *__restrict__ rank_of_pos) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = G;  // the last g with gs[g] <= i (gs[0] == 0)
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (gs[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        rank_of_pos[S[i]] = (uint32_t)lo;
+    }
 }
 
+// one word per original start, in the original order: rank << 32 | start
+__global__ __launch_bounds__(256) void qs_pack_kernel(const uint32_t *__restrict__ orig, uint64_t n,
+                                                      const uint32_t *__restrict__ rank_of_pos,
+                                                      uint64_t *__restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = orig[i];
+        out[i] = ((uint64_t)rank_of_pos[s] << 32) | s;
+    }
+}
+}  // namespace gkm
+
 // GK_SORT_QUICKSORT_ORDER, after the device sort: every start's dense group rank from the device's
-// group pass, then numba's quicksort on the host over the original start order `orig` with rank
+// group pass, packed on the device with the start in the ORIGINAL start order `orig` (a device
+// copy taken before the sort), then numba's quicksort on the host over those words with rank
 // comparisons (gkm_qsort.cpp); the result replaces the sorted starts.  Only members of a group
-// change places, so keys, head flags and unique counts stay valid.
-static int apply_quicksort_order(gk_ctx *c, std::vector<uint32_t> &orig) {
+// change places, so keys, head flags and unique counts stay valid.  Host memory: 8 B per k-mer.
+static int apply_quicksort_order(gk_ctx *c, const uint32_t *orig) {
     const uint64_t n = c->n;
     uint64_t G = 0;
     if (int rc = gk_unique_counts(c, &G)) return rc;
     if (int rc = materialize_starts(c)) return rc;
-    std::vector<uint32_t> S(n), gs(G);
-    GK_TRY_HIP(c, hipMemcpyAsync(S.data(), c->vals[c->cur], 4 * n, hipMemcpyDeviceToHost, c->stream));
-    GK_TRY_HIP(c, hipMemcpyAsync(gs.data(), c->idx_b, 4 * G, hipMemcpyDeviceToHost, c->stream));
+    uint32_t *rank_of_pos;
+    uint64_t *words;
+    GK_TRY_HIP(c, scratch(c, "qs_rank", c->sba_len + 1, &rank_of_pos));
+    GK_TRY_HIP(c, scratch(c, "qs_words", n, &words));
+    hipLaunchKernelGGL(qs_rank_scatter_kernel, dim3(grid_of(n)), dim3(256), 0, c->stream, c->vals[c->cur], n, c->idx_b,
+                       G, rank_of_pos);
+    GK_TRY_HIP(c, hipGetLastError());
+    hipLaunchKernelGGL(qs_pack_kernel, dim3(grid_of(n)), dim3(256), 0, c->stream, orig, n, rank_of_pos, words);
+    GK_TRY_HIP(c, hipGetLastError());
+    std::vector<uint64_t> A(n);
+    GK_TRY_HIP(c, hipMemcpyAsync(A.data(), words, 8 * n, hipMemcpyDeviceToHost, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    std::vector<uint32_t> rank(c->sba_len + 1, 0);
-    for (uint64_t g = 0; g < G; ++g) {
-        const uint64_t e = g + 1 < G ? gs[g + 1] : n;
-        for (uint64_t i = gs[g]; i < e; ++i) rank[S[i]] = (uint32_t)g;
-    }
-    if (quicksort_by_rank(orig.data(), n, rank.data()) != 0)
+    if (quicksort_by_rank(A.data(), n) != 0)
         return fail(c, GK_E_UNSUPPORTED, "numba quicksort stack limit (MAX_STACK = 100) exceeded");
-    GK_TRY_HIP(c, hipMemcpyAsync(c->vals[c->cur], orig.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+    std::vector<uint32_t> S(n);
+    for (uint64_t i = 0; i < n; ++i) S[i] = (uint32_t)A[i];
+    GK_TRY_HIP(c, hipMemcpyAsync(c->vals[c->cur], S.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     return GK_OK;
 }
@@ -927,8 +961,6 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     const bool qorder = (flags & GK_SORT_QUICKSORT_ORDER) != 0;
     if (qorder && canonical)
         return fail(c, GK_E_ARG, "the reference's quicksort tie order exists for forward k-mers only (no canonical sort)");
-    if (qorder && c->n > kQuicksortOrderMax)
-        return fail(c, GK_E_UNSUPPORTED, "the reference's quicksort tie order runs on the host: at most 2^28 k-mers");
     if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers: call gk_enumerate first");
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (max_kmer_len != 0 && max_kmer_len < c->min_k) return fail(c, GK_E_ARG, "max_kmer_len is less than min_kmer_len");
@@ -950,12 +982,11 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     c->enum_sorted = false;
     const bool from_enum = c->enumerated;
     int rc;
-    std::vector<uint32_t> orig;  // the start order the reference's quicksort starts from
+    uint32_t *orig = nullptr;  // the start order the reference's quicksort starts from (device copy)
     if (qorder && c->n >= 2) {
         if ((rc = materialize_starts(c))) return rc;
-        orig.resize(c->n);
-        GK_TRY_HIP(c, hipMemcpyAsync(orig.data(), c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToHost, c->stream));
-        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        GK_TRY_HIP(c, scratch(c, "qs_orig", c->n, &orig));
+        GK_TRY_HIP(c, hipMemcpyAsync(orig, c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToDevice, c->stream));
     }
     if (c->n < 2) {
         rc = materialize_starts(c);
@@ -984,22 +1015,39 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
             direct = true;
         }
     }
-    // bounded keys of two or more words over a large array (ACGT, max 33..64 with min < max): prefix
-    // doubling capped at max -- the seed keys, then only the groups still tied -- instead of one
-    // LSD pass per 8 bits of the 2-word keys (13 passes, 21 ms for the reference's max-50 workload);
-    // the keys are then ranks, as for max_kmer_len=None (GKM_BOUNDED_DIRECT=1 keeps the direct keys)
-    if (direct && ks.words >= 2 && !canonical && max_kmer_len != c->min_k && c->acgt &&
-        sort_keys_msd(c, c->n, 1, 64) && std::getenv("GKM_BOUNDED_DIRECT") == nullptr)
-        direct = false;
+    // bounded keys of two or more words (ACGT, min < max, 2 max + bit_width(max) > 64: max >= 30)
+    // over a large array that covers most positions: prefix doubling capped at max -- the seed
+    // keys, then only the groups still tied -- instead of one LSD pass per 8 bits of the 2-word
+    // keys (13 passes, 21 ms for the reference's max-50 workload).  The doubling ranks every
+    // position of the sequence, so a subset of user-given starts (n well below the positions)
+    // keeps the direct keys (GKM_BOUNDED_DIRECT=1 keeps them always).  The sort's keys are then
+    // ranks; the key contract stays the direct one: they are re-encoded from the sorted starts
+    // when asked for (keys_stale)
+    const bool reroute = direct && ks.words >= 2 && !canonical && max_kmer_len != c->min_k && c->acgt &&
+                         (from_enum || 2 * c->n >= c->sba_len) && sort_keys_msd(c, c->n, 1, 64) &&
+                         std::getenv("GKM_BOUNDED_DIRECT") == nullptr;
+    if (reroute) direct = false;
     rc = direct ? sort_direct(c, ks) : sort_doubling(c, max_kmer_len);
     if (rc != GK_OK) return rc;
+    if (reroute) {  // ranks in keys[cur]: the encoded keys are re-derived on demand (ensure_keys)
+        c->spec = ks;
+        c->keys_valid = true;
+        c->keys_stale = true;
+        c->keys_are_ranks = false;
+    }
     c->enum_sorted = from_enum && direct && ks.symbols == ks.min_len;
     c->starts_materialized = true;
     c->sorted = true;
     c->enumerated = false;
     c->sort_len = max_kmer_len;
     c->canonical = canonical;
-    if (qorder) return apply_quicksort_order(c, orig);
+    if (qorder && c->n >= 2) {
+        if ((rc = apply_quicksort_order(c, orig)) != GK_OK) {
+            c->sorted = false;  // the starts are not in the order asked for
+            c->unique_valid = c->heads_valid = false;
+            return rc;
+        }
+    }
     return GK_OK;
 }
 

@@ -26,7 +26,7 @@ namespace gkm {
 constexpr int kRadixBits = 8;
 constexpr int kRadixBins = 256;
 constexpr int kMaxWords = 4;          // direct keys up to 256 bits
-constexpr uint64_t kQuicksortOrderMax = 1ull << 28;  // GK_SORT_QUICKSORT_ORDER: host quicksort bound
+
 constexpr int kEncodeTile = 4096;     // positions per encode tile
 constexpr int kSbaPad = 32768;        // '$' bytes after the sba (>= largest tile + max symbols)
 constexpr int kSortThreads = 256;     // radix pass workgroup

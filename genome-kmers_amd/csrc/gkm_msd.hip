@@ -363,7 +363,12 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                 }
             }
             if (!fast) {
-#pragma unroll
+                // (tiles with stops, or the sequence end).  Canonical keys: two windows and a
+                // reverse complement per position -- a loop, not unrolled, so the fast path above
+                // keeps its registers (unrolled over the 96 positions it took 256 VGPRs, spilled
+                // to scratch and ran the whole kernel at one wave per SIMD)
+                constexpr int UNR = CANON ? 1 : I;
+#pragma unroll UNR
                 for (int i = 0; i < I; ++i) {
                     const uint32_t p = i * T + t;
                     const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
@@ -1942,6 +1947,30 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_copy2_kernel(const uint2 *_
     }
 }
 
+// TIMING EXPERIMENTS ONLY (GKM_EXP_WAVECOPY=5, wrong output): the wave stage's bytes as one plain
+// stream over the whole array -- 9 B in (compact word + digit byte), 13 B out (key, start, head)
+// per element, 16 consecutive elements per thread in 16-B pieces -- the streaming floor of the
+// stage's traffic, against the bucket-granular floor of msd_wave_copy_kernel
+__global__ __launch_bounds__(256) void stream_copy_kernel(uint64_t n, const uint64_t *__restrict__ k1,
+                                                          const uint8_t *__restrict__ nd, uint64_t *__restrict__ k0,
+                                                          uint32_t *__restrict__ v0, uint8_t *__restrict__ heads) {
+    const uint64_t groups = n / 16;
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
+        const uint4 *ks = reinterpret_cast<const uint4 *>(k1 + 16 * g);
+        uint4 kv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kv[j] = ks[j];
+        const uint4 d = reinterpret_cast<const uint4 *>(nd)[g];
+        uint4 *ko = reinterpret_cast<uint4 *>(k0 + 16 * g);
+        uint4 *vo = reinterpret_cast<uint4 *>(v0 + 16 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ko[j] = make_uint4(kv[j].y ^ d.x, kv[j].x, kv[j].w, kv[j].z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vo[j] = make_uint4(kv[2 * j].x, kv[2 * j].z, kv[2 * j + 1].x, kv[2 * j + 1].z);
+        reinterpret_cast<uint4 *>(heads)[g] = make_uint4(d.y | 0x01010101u, d.z, d.w, d.x);
+    }
+}
+
 static bool exp_wave_copy() { return std::getenv("GKM_EXP_WAVECOPY") != nullptr; }
 
 // one round's lists, copied to device memory for the wave kernels
@@ -3136,6 +3165,10 @@ struct MsdDriver {
                 hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8, 2>),
                                    grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8, 2>, 64), dim3(64), 0,
                                    c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
+                break;
+            }
+            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '5') {  // timing only
+                hipLaunchKernelGGL(stream_copy_kernel, dim3(cus * 8), dim3(256), 0, c->stream, n, k1, nd, k0, v0, heads);
                 break;
             }
             if (exp_wave_copy()) {  // timing experiments only: wrong output

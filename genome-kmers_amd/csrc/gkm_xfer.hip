@@ -337,15 +337,18 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // alone (3.1 Gb from pinned memory: 24.8-27.4 against 21.0-21.6 ms, profiles/r4/xfer_threads_numa.txt)
     // -- the packing is bound by host memory bandwidth, which the DMA reads share
     const bool hybrid = env_u64("GKM_XFER_HYBRID", 0) != 0 && host_pinned(sba);
+    // the copy streams write the resident sba and the staging slots outside the context's stream:
+    // everything queued before (an earlier sort reading the sba, an earlier transfer's unpacks,
+    // which read the slots xfer_slots may free and reallocate) has to be done first
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     GK_TRY_HIP(c, xfer_slots(c, S, kHeaderBytes + chunk + 16));
     hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
     hipEvent_t *ev_raw = c->xfer_ev.data() + 2 * S;
     uint32_t *d_census = reinterpret_cast<uint32_t *>(c->scalars + 24);
-    if (hybrid) GK_TRY_HIP(c, hipMemsetAsync(d_census, 0, 8, c->stream));
-    // the copy streams write the resident sba and the staging slots outside the context's stream:
-    // everything queued before (an earlier sort reading the sba, an earlier transfer's unpacks)
-    // has to be done first
-    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    if (hybrid) {
+        GK_TRY_HIP(c, hipMemsetAsync(d_census, 0, 8, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    }
 
     std::mutex mu;
     std::condition_variable cv;

@@ -888,7 +888,7 @@ class Kmers:
         equal k-mers in whatever order numba's quicksort produces (kmers.py:1624-1652); no parallel
         sort reproduces that.  ``order="reference"`` gives exactly that order: the device sorts,
         then numba's quicksort runs on the host over the original start order, comparing the
-        device's group ranks (libgkm GK_SORT_QUICKSORT_ORDER; host-bound, at most 2^28 k-mers, not
+        device's group ranks (libgkm GK_SORT_QUICKSORT_ORDER; host-bound, 8 B of host memory per k-mer, not
         with canonical=True).  Sorted k-mers,
         encoded keys, group sizes, counts, histograms and the ``(kmer_num, group_size_yielded,
         group_size_total)`` tuples of ``get_kmers`` are identical either way, because ties only

@@ -97,7 +97,8 @@ typedef struct gk_filter {
 /* The reference's default tie order (Kmers.sort: numba quicksort, break_ties=False,
  * kmers.py:1624-1652): the device sorts, then numba's quicksort runs on the host over the original
  * start order comparing the device's group ranks (gkm_qsort.cpp) -- bit-exact with the reference,
- * equal k-mers included.  Host-bound: at most 2^28 k-mers; not with GK_SORT_CANONICAL. */
+ * equal k-mers included.  Host-bound (8 B of host memory per k-mer: the device hands the host
+ * rank << 32 | start per start); not with GK_SORT_CANONICAL. */
 #define GK_SORT_QUICKSORT_ORDER 2u
 
 /* ---- lifetime ------------------------------------------------------------------------------ */

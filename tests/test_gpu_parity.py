@@ -827,6 +827,45 @@ def test_doubling_user_starts_vs_oracle(path, monkeypatch):
     np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
 
 
+# a subset of user-given starts under a bounded 2-word key (min < max, max 30..64) keeps the direct
+# keys: the capped doubling ranks every position of the sequence, which pays only when the starts
+# cover most of them (round-4 advice); the encode stage then sees the user's starts, not every position
+@pytest.mark.parametrize("max_k", [30, 41, 64])
+def test_bounded_user_subset_keeps_direct_keys(max_k, monkeypatch):
+    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    rng = np.random.default_rng(max_k)
+    sc = SequenceCollection(sequence_list=random_genome(rng, [40_000, 9_000, 300]))
+    km = gk.Kmers(sc, min_kmer_len=20, max_kmer_len=max_k)
+    user = rng.permutation(km.kmer_sba_start_indices)[:5_000].astype(km.kmer_sba_start_indices.dtype)
+    km.kmer_sba_start_indices = user.copy()
+    km._engine.profile_enable(True)
+    km.sort()
+    rep = km._engine.profile_report()
+    km._engine.profile_enable(False)
+    assert rep["encode"]["units"] == len(user), rep.get("encode")
+    want = oracle.quicksort(sc.forward_sba, np.sort(user, kind="stable"), 20, max_k, break_ties=True)
+    np.testing.assert_array_equal(km.kmer_sba_start_indices, want)
+    spec = oracle.key_spec(True, 20, max_k)
+    assert km._engine.key_layout() == (spec[3], spec[0], spec[1])
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+
+
+# the whole enumeration under a bounded 2-word key is sorted by capped doubling on the large-array
+# route (keys are ranks inside the sort); the key contract stays the direct encoding, re-derived
+# from the sorted starts when asked for, as on small arrays (round-4 advice)
+@pytest.mark.parametrize("case", [c for c in CASES if c["max_kmer_len"] is not None], ids=lambda c: c["name"])
+def test_encoded_keys_on_large_array_routes(case, monkeypatch):
+    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    km, a = make(case)
+    km.sort()
+    words, bits, symbols = km._engine.key_layout()
+    if bits == 0:
+        pytest.skip("bound beyond 256-bit keys: sorted by prefix doubling, keys are ranks")
+    spec = oracle.key_spec(km._engine.is_acgt(), case["min_kmer_len"], case["max_kmer_len"])
+    assert (words, bits, symbols) == (spec[3], spec[0], spec[1])
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(a["sba"], a["starts_stable"], *spec))
+
+
 # the golden cases again with the large-array routes forced at their sizes (GKM_MSD_KEYS_MIN=2):
 # MSD levels over the keys, doubling by tied groups, and bounded keys of two or more words through
 # capped doubling (keys become ranks) -- sorted starts and every query against the reference's

@@ -182,3 +182,26 @@ def test_set_sequence_waits_for_an_earlier_sort(monkeypatch):
     eng.sort(21)
     want = oracle.quicksort(b, oracle.enumerate_starts(b, seg, 21), 21, 21, break_ties=True)
     np.testing.assert_array_equal(eng.copy_starts(np.empty(n, dtype=np.uint32)), want)
+
+
+def test_packed_short_then_longer_sequence(monkeypatch):
+    # a longer packed sequence after a shorter one grows the staging slots: the slots the earlier
+    # transfer's unpacks read are freed only after the context's stream has drained (round-4 advice)
+    rng = np.random.default_rng(23)
+    a, seg = genome(rng, 3 * B + 5)
+    b, segb = genome(rng, 70 * B + 11, contigs=3)
+    monkeypatch.setenv("GKM_PACK_MIN", "0")
+    monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
+    monkeypatch.setenv("GKM_XFER_THREADS", "2")
+    eng = _native.Engine()
+    eng.set_sequence(a, seg)
+    monkeypatch.setenv("GKM_PACK_BLOCKS", "8")
+    monkeypatch.setenv("GKM_XFER_THREADS", "6")
+    eng.set_sequence(b, segb)
+    for v in ("GKM_PACK_MIN", "GKM_PACK_BLOCKS", "GKM_XFER_THREADS"):
+        monkeypatch.delenv(v)
+    np.testing.assert_array_equal(eng.copy_sequence(len(b)), b)
+    n = eng.enumerate(17)
+    eng.sort(17)
+    want = oracle.quicksort(b, oracle.enumerate_starts(b, segb, 17), 17, 17, break_ties=True)
+    np.testing.assert_array_equal(eng.copy_starts(np.empty(n, dtype=np.uint32)), want)

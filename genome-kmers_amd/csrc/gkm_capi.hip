@@ -438,7 +438,11 @@ extern "C" void gk_destroy(gk_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->pre_stream) hipStreamSynchronize(c->pre_stream);
     xfer_release(c);
+    for (hipEvent_t e : c->pre_ev) hipEventDestroy(e);
+    if (c->pre_done) hipEventDestroy(c->pre_done);
+    if (c->pre_stream) hipStreamDestroy(c->pre_stream);
     void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
                     c->dhist, c->mask, c->hmask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
@@ -470,6 +474,7 @@ extern "C" int gk_stream(gk_ctx *c, void **stream) {
 // ---------------------------------------------------------------------------------------------
 extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, const uint32_t *seg_starts, uint64_t nseg) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!sba || len == 0) return fail(c, GK_E_ARG, "sequence byte array is empty");
     if (!seg_starts || nseg == 0) return fail(c, GK_E_ARG, "sequence_collection is empty");
     if (len > 0xFFFFFFFFull) return fail(c, GK_E_LIMIT, "sequence byte array longer than 2^32-1");
@@ -501,7 +506,11 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
         // device (gkm_xfer.hip); the stream orders the sort's kernels behind the last unpack, so
         // only the census is waited for
         uint64_t dollars = 0;
-        if (int rc = packed_transfer(c, sba, len, &h[0], &dollars)) return rc;
+        // a sort hint (gk_sort_hint): the L0 pass of gk_sort(k) runs as the sequence lands
+        L0Prefetch *pf = nullptr;
+        if (c->hint_k && nseg == 1 && !internal)
+            if (int rc = prefetch_plan(c, len, &pf)) return rc;
+        if (int rc = packed_transfer(c, sba, len, &h[0], &dollars, pf)) return rc;
         h[1] = (uint32_t)dollars;
     } else {
         GK_TRY_HIP(c, hipMemcpyAsync(c->sba, sba, len, hipMemcpyHostToDevice, c->stream));
@@ -517,6 +526,13 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;
     c->internal_dollar = internal || (uint64_t)h[1] != nseg - 1;
+    return GK_OK;
+}
+
+extern "C" int gk_sort_hint(gk_ctx *c, uint32_t k, uint32_t flags) {
+    if (!c) return GK_E_ARG;
+    if (flags != 0) return fail(c, GK_E_ARG, "gk_sort_hint: flags must be 0 (forward k-mers)");
+    c->hint_k = k;
     return GK_OK;
 }
 
@@ -553,6 +569,7 @@ extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
     if (min_k > shortest) return fail(c, GK_E_ARG, "min_kmer_len must be <= the shortest sequence length");
     if (n > 0xFFFFFFFFull) return fail(c, GK_E_LIMIT, "the size of the required kmers array exceeds the limit set by a uint32");
     GK_TRY_HIP(c, hipSetDevice(c->device));
+    if (min_k != c->pre_k) pre_drop(c);  // (a prefetched L0 serves the enumeration of its k only)
     c->have_starts = false;
     int rc = ensure_elems(c, n, 1);
     if (rc != GK_OK) return rc;
@@ -571,6 +588,7 @@ extern "C" int gk_enumerate(gk_ctx *c, uint32_t min_k, uint64_t *n_out) {
 
 extern "C" int gk_set_start_indices(gk_ctx *c, const uint32_t *src, uint64_t n, uint32_t min_k) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->sba) return fail(c, GK_E_STATE, "no sequence loaded");
     if (n > 0 && !src) return fail(c, GK_E_ARG, "null start array");
     GK_TRY_HIP(c, hipSetDevice(c->device));
@@ -657,7 +675,8 @@ static int sort_direct(gk_ctx *c, const KeySpec &ks) {
             rc = split_sort(c, ks, &split);
             if (rc != GK_OK) return rc;
         }
-        if (!split) rc = msd_sort(c, ks);
+        if (!split) rc = prefetch_matches(c, ks) ? msd_sort_prefetched(c, ks) : msd_sort(c, ks);
+        pre_drop(c);
         if (rc != GK_OK) return rc;
         c->spec = ks;
         c->keys_valid = true;
@@ -981,6 +1000,8 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     c->unique_valid = c->heads_valid = false;
     c->enum_sorted = false;
     const bool from_enum = c->enumerated;
+    // only the fixed-length forward sort of the whole enumeration uses a prefetched L0 (sort_direct)
+    if (canonical || qorder || max_kmer_len != c->min_k || !from_enum) pre_drop(c);
     int rc;
     uint32_t *orig = nullptr;  // the start order the reference's quicksort starts from (device copy)
     if (qorder && c->n >= 2) {
@@ -1053,6 +1074,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
 
 extern "C" int gk_copy_strands(gk_ctx *c, uint8_t *dst, uint64_t n) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->sorted || !c->canonical) return fail(c, GK_E_STATE, "strands need a canonical sort (GK_SORT_CANONICAL)");
     if (n != c->n) return fail(c, GK_E_ARG, "n differs from the k-mer count");
     if (n == 0) return GK_OK;
@@ -1113,6 +1135,7 @@ __global__ __launch_bounds__(256) void locate_kernel(const uint32_t *__restrict_
 
 extern "C" int gk_locate(gk_ctx *c, const uint64_t *kmer_nums, uint64_t m, uint32_t *sba_idx, uint32_t *seg) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->have_starts) return fail(c, GK_E_STATE, "no k-mers");
     if (m == 0) return GK_OK;
     if (!kmer_nums || !sba_idx || !seg) return fail(c, GK_E_ARG, "null array");
@@ -1144,6 +1167,7 @@ extern "C" int gk_key_layout(gk_ctx *c, uint32_t *words, uint32_t *bits, uint32_
 
 extern "C" int gk_copy_keys(gk_ctx *c, uint64_t *dst, uint64_t n_words) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->keys_valid) return fail(c, GK_E_STATE, "no encoded keys: sort first");
     if (int rc = ensure_keys(c)) return rc;
     const uint64_t W = (uint64_t)c->spec.words;
@@ -1164,6 +1188,7 @@ extern "C" int gk_copy_keys(gk_ctx *c, uint64_t *dst, uint64_t n_words) {
 
 extern "C" int gk_set_filter_mask(gk_ctx *c, const uint8_t *mask, uint64_t n) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->mask), &c->mask_cap, n + 64));
     if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->mask, mask, n, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
@@ -1173,6 +1198,7 @@ extern "C" int gk_set_filter_mask(gk_ctx *c, const uint8_t *mask, uint64_t n) {
 
 extern "C" int gk_set_group_heads(gk_ctx *c, const uint8_t *heads, uint64_t n) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->hmask), &c->hmask_cap, n + 64));
     if (n) GK_TRY_HIP(c, hipMemcpyAsync(c->hmask, heads, n, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
@@ -1182,6 +1208,7 @@ extern "C" int gk_set_group_heads(gk_ctx *c, const uint8_t *heads, uint64_t n) {
 
 extern "C" int gk_device_views(gk_ctx *c, void **starts, void **keys, uint64_t *n, uint32_t *words) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (int rc = materialize_starts(c)) return rc;
     if (keys && c->keys_valid)
         if (int rc = ensure_keys(c)) return rc;
@@ -1266,6 +1293,7 @@ extern "C" int gk_shard_bucket_bits(void) { return gkm::msd_radix_bits(); }
 extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *d_keys,
                                   uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out) {
     if (!c || !d_keys || !d_starts || !h_hist || !n_out) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
     if (hi > c->sba_len) hi = c->sba_len;
@@ -1306,6 +1334,7 @@ static uint32_t range_prefix(uint32_t d, bool lower, int ob) {
 extern "C" int gk_shard_histogram(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
                                   uint32_t *bits) {
     if (!c || !h_hist || !bits) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
     if (hi > c->sba_len) hi = c->sba_len;
@@ -1329,6 +1358,7 @@ constexpr uint32_t kHomoWeight16 = 11;
 extern "C" int gk_shard_class_b(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *h_hist,
                                 uint64_t *n_rest, uint64_t *n_runs) {
     if (!c || !h_hist || !n_rest || !n_runs) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     *n_rest = *n_runs = 0;
     c->shard_rest.clear();
@@ -1350,6 +1380,7 @@ extern "C" int gk_shard_class_b(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k,
 
 extern "C" int gk_shard_class_b_copy(gk_ctx *c, uint32_t *rest, uint64_t n_rest, uint32_t *runs, uint64_t n_runs) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (n_rest != c->shard_rest.size() || 3 * n_runs != c->shard_runs.size())
         return fail(c, GK_E_ARG, "gk_shard_class_b_copy: sizes differ from gk_shard_class_b's");
     if ((n_rest && !rest) || (n_runs && !runs)) return GK_E_ARG;
@@ -1378,6 +1409,7 @@ static int shard_sort_range_impl(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t
                                  const uint32_t *rest, uint64_t n_rest, const uint32_t *runs, uint64_t n_runs,
                                  bool given, uint64_t *n_kept) {
     if (!c || !n_kept) return GK_E_ARG;
+    pre_drop(c);
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (c->internal_dollar) return fail(c, GK_E_NO_BASES, "the sba holds a '$' inside a segment");
     if (digit_lo > digit_hi || digit_hi > 4096u) return fail(c, GK_E_ARG, "digit range outside [0, 4096]");
@@ -1419,6 +1451,7 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
                              uint32_t flags, const uint64_t *h_piece_off, const uint64_t *h_piece_len,
                              const uint32_t *h_piece_bucket, uint32_t npieces) {
     if (!c || (n && (!d_keys || !d_starts || !h_piece_off || !h_piece_len || !h_piece_bucket))) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (n > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
     KeySpec ks;

@@ -795,6 +795,7 @@ extern "C" int gk_group_hist(gk_ctx *c, int is_sorted, int64_t kmer_len, const g
                              int64_t min_group_size, int64_t max_group_size, int64_t max_counts_bin, int64_t *hist,
                              int64_t *total, int32_t *err_code, uint64_t *err_idx) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (max_counts_bin <= 0) return fail(c, GK_E_ARG, "max_counts_bin must be >= 1");
     if (min_group_size < 1) return fail(c, GK_E_ARG, "min_group_size must be >= 1");
     const uint32_t *cidx;
@@ -828,6 +829,7 @@ extern "C" int gk_group_members(gk_ctx *c, int is_sorted, int64_t kmer_len, cons
                                 uint64_t *kmer_num, uint32_t *size_yielded, uint32_t *size_total, uint64_t capacity,
                                 uint64_t *n_out, int32_t *err_code, uint64_t *err_idx) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (min_group_size < 1) return fail(c, GK_E_ARG, "min_group_size must be >= 1");
     const uint32_t *cidx;
     uint64_t count, G;
@@ -867,6 +869,7 @@ extern "C" int gk_group_members(gk_ctx *c, int is_sorted, int64_t kmer_len, cons
 // ucount (u32); with the sorted keys (keys[cur]) and starts (vals[cur]) this is the full product.
 extern "C" int gk_unique_counts(gk_ctx *c, uint64_t *n_unique) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->sorted || !c->keys_valid) return fail(c, GK_E_STATE, "unique counts need a sorted k-mer set");
     const int64_t kl = c->sort_len == 0 ? -1 : (int64_t)c->sort_len;
     uint64_t G = 0;
@@ -900,6 +903,7 @@ extern "C" int gk_unique_counts(gk_ctx *c, uint64_t *n_unique) {
 
 extern "C" int gk_copy_unique(gk_ctx *c, uint64_t *group_start, uint32_t *count, uint64_t n) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->unique_valid) return fail(c, GK_E_STATE, "call gk_unique_counts first");
     if (n != c->n_unique) return fail(c, GK_E_ARG, "n differs from the unique k-mer count");
     if (n == 0) return GK_OK;
@@ -916,6 +920,7 @@ extern "C" int gk_copy_unique(gk_ctx *c, uint64_t *group_start, uint32_t *count,
 
 extern "C" int gk_device_unique(gk_ctx *c, void **group_start, void **count, uint64_t *n_unique) {
     if (!c) return GK_E_ARG;
+    pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     if (!c->unique_valid) return fail(c, GK_E_STATE, "call gk_unique_counts first");
     if (group_start) *group_start = c->idx_b;
     if (count) *count = c->ucount;

@@ -157,6 +157,18 @@ struct gk_ctx {
     int xfer_slots = 0;
     uint64_t xfer_slot_bytes = 0;
 
+    // sort hint (gk_sort_hint): gk_set_sequence also runs the L0 pass of gk_sort(hint_k) over
+    // regions of the sequence as its packed transfer lands them, on pre_stream (gkm_msd.hip,
+    // L0Prefetch); the next gk_sort(hint_k) of the enumeration starts from the regions' buckets
+    // (pre_valid).  Any other use of the k-mer buffers drops it (pre_drop).
+    uint32_t hint_k = 0;
+    hipStream_t pre_stream = nullptr;
+    hipEvent_t pre_done = nullptr;
+    std::vector<hipEvent_t> pre_ev;  // per region: its bytes unpacked on `stream`
+    bool pre_valid = false;          // keys[1] / vals[1] / scratch "msd_nd" + "pre_pieces" hold it
+    uint32_t pre_k = 0, pre_regions = 0;
+    int pre_w0 = 0, pre_w1 = 0;
+
     // profiling
     bool profile = false;
     std::vector<gkm::Timer> timers;
@@ -232,8 +244,21 @@ int hip_fail(gk_ctx *c, hipError_t e, const char *where);
 // packed sba transfer (gkm_xfer.hip): inputs of >= packed_transfer_min() bytes go 2-bit packed;
 // the alphabet census (class bits as alphabet_kernel's, '$' count) is taken on the host
 uint64_t packed_transfer_min();
-int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars);
+struct L0Prefetch;  // gkm_msd.hip
+int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars,
+                    L0Prefetch *pf = nullptr);
 void xfer_release(gk_ctx *c);
+// prefetched L0 of a sort hint (gkm_msd.hip): plan the regions of a single-contig sba of len bytes
+// (*out = nullptr when the hint does not apply), launch every region whose bytes lie below `landed`
+// (the transfer's in-order unpacked prefix, enqueued on c->stream), then finish (ok: the whole
+// sequence was ACGT and landed; else the prefetch is dropped)
+int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out);
+int prefetch_launch(gk_ctx *c, L0Prefetch *pf, uint64_t landed);
+int prefetch_finish(gk_ctx *c, L0Prefetch *pf, bool ok);
+// gk_sort(k) of the whole enumeration when the prefetched L0 is valid for its key spec
+bool prefetch_matches(const gk_ctx *c, const KeySpec &ks);
+int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks);
+inline void pre_drop(gk_ctx *c) { c->pre_valid = false; }
 
 // encode
 hipError_t launch_alphabet(gk_ctx *c, uint32_t *d_flags);

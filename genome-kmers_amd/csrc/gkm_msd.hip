@@ -1948,26 +1948,30 @@ __global__ __launch_bounds__(64, MINW) void msd_wave_copy2_kernel(const uint2 *_
 }
 
 // TIMING EXPERIMENTS ONLY (GKM_EXP_WAVECOPY=5, wrong output): the wave stage's bytes as one plain
-// stream over the whole array -- 9 B in (compact word + digit byte), 13 B out (key, start, head)
-// per element, 16 consecutive elements per thread in 16-B pieces -- the streaming floor of the
+// coalesced stream over the whole array -- 9 B in (compact word + digit byte), 13 B out (key,
+// start, head) per element; each wave takes 512 consecutive elements per step, every load and
+// store instruction covering one contiguous 512-B or 1-KiB piece -- the streaming floor of the
 // stage's traffic, against the bucket-granular floor of msd_wave_copy_kernel
 __global__ __launch_bounds__(256) void stream_copy_kernel(uint64_t n, const uint64_t *__restrict__ k1,
                                                           const uint8_t *__restrict__ nd, uint64_t *__restrict__ k0,
                                                           uint32_t *__restrict__ v0, uint8_t *__restrict__ heads) {
-    const uint64_t groups = n / 16;
-    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
-        const uint4 *ks = reinterpret_cast<const uint4 *>(k1 + 16 * g);
-        uint4 kv[8];
+    const int lane = threadIdx.x & 63;
+    const uint64_t wid = (blockIdx.x * 256ull + threadIdx.x) >> 6, nw = gridDim.x * 4ull;
+    for (uint64_t blk = wid; blk < n / 512; blk += nw) {
+        const uint64_t e0 = blk * 512;
+        const uint4 *ks = reinterpret_cast<const uint4 *>(k1 + e0);
+        uint4 kv[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) kv[j] = ks[j];
-        const uint4 d = reinterpret_cast<const uint4 *>(nd)[g];
-        uint4 *ko = reinterpret_cast<uint4 *>(k0 + 16 * g);
-        uint4 *vo = reinterpret_cast<uint4 *>(v0 + 16 * g);
+        for (int j = 0; j < 4; ++j) kv[j] = ks[j * 64 + lane];
+        const uint2 d = reinterpret_cast<const uint2 *>(nd + e0)[lane];
+        uint4 *ko = reinterpret_cast<uint4 *>(k0 + e0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ko[j] = make_uint4(kv[j].y ^ d.x, kv[j].x, kv[j].w, kv[j].z);
+        for (int j = 0; j < 4; ++j) ko[j * 64 + lane] = make_uint4(kv[j].y ^ d.x, kv[j].x, kv[j].w, kv[j].z);
+        uint4 *vo = reinterpret_cast<uint4 *>(v0 + e0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) vo[j] = make_uint4(kv[2 * j].x, kv[2 * j].z, kv[2 * j + 1].x, kv[2 * j + 1].z);
-        reinterpret_cast<uint4 *>(heads)[g] = make_uint4(d.y | 0x01010101u, d.z, d.w, d.x);
+        for (int j = 0; j < 2; ++j)
+            vo[j * 64 + lane] = make_uint4(kv[2 * j].x, kv[2 * j].z, kv[2 * j + 1].x, kv[2 * j + 1].z);
+        reinterpret_cast<uint2 *>(heads + e0)[lane] = make_uint2(d.y | 0x01010101u, d.x);
     }
 }
 
@@ -2693,7 +2697,7 @@ struct MsdDriver {
         timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
-        const bool with_nd = kout == c->keys[0] && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
+        const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
         if (with_nd) {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
@@ -2703,6 +2707,32 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = with_nd;
+        return GK_OK;
+    }
+
+    // one region of the prefetched L0 (L0Prefetch, below): count, column scan and partition of the
+    // k-mers starting in [lo, hi) into keys[1] / vals[1] / nd at output indices from lo, then the
+    // region's 2^w0 bucket bases and counts into `pieces` -- all on c->stream (the caller points it
+    // at the prefetch stream), with the region's chunk tables already in `tab` (c_first[nc],
+    // c_ntiles[nc], then s_cfirst, s_nchunks, s_start) and no host round trip
+    int l0_region(uint64_t lo, uint64_t hi, uint32_t nt, uint32_t nc, uint32_t *tab, uint64_t sink, uint32_t *pieces) {
+        int rc = tables(nt, nc, 1);  // (allocated by prefetch_plan: no reallocation here)
+        if (rc != GK_OK) return rc;
+        c_first = tab;
+        c_ntiles = tab + nc;
+        const uint32_t *misc = tab + 2 * nc;
+        const L0Args a{c->sba, lo, hi, ks.symbols, B, 0};
+        const int w0 = width(0);
+        const Dig d0 = dig_at(B, 0, w0);
+        l0_dispatch(true, w0, false, a, d0, nt, nullptr, nullptr, 0, 0, NextDigits{});
+        GK_TRY_HIP(c, hipGetLastError());
+        rc = scan_offsets(w0, nc, misc, misc + 1, misc + 2, 1);
+        if (rc != GK_OK) return rc;
+        NextDigits ndg{dig_at(B, w0, width(1)), nd};
+        l0_dispatch(false, w0, true, a, d0, nt, c->keys[1], c->vals[1], nt, sink, ndg);
+        GK_TRY_HIP(c, hipGetLastError());
+        GK_TRY_HIP(c, hipMemcpyAsync(pieces, seg_base, 4u << w0, hipMemcpyDeviceToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(pieces + (1u << w0), seg_cnt, 4u << w0, hipMemcpyDeviceToDevice, c->stream));
         return GK_OK;
     }
 
@@ -3311,16 +3341,218 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         c->pk_fresh = false;
     }
     uint64_t found = 0;
-    rc = d.run_l0(0, c->sba_len, c->keys[0], c->vals[0], c->elem_cap + 64, &found);
+    // The L0's output buffer: the one that makes the last global level write buffer 1, so that the
+    // finishing kernels read buffer 1 and write buffer 0 instead of rewriting buffer 0 in place
+    // (levels predicted from the mean bucket size; C3: L0, L1, L2 -> L0 writes buffer 1).  A/B on
+    // one box (C3, 3 pairs): 67.3-68.3 against 67.7-68.8 ms; the same order of buffers in the
+    // prefetched path's sort (below) took the wave-local kernel from 19.8 to 15.3 ms on a slow box.
+    // GKM_L0_BUF=0/1 forces it.
+    int l0b = 0;
+    {
+        uint64_t mean = c->n >> d.width(0);
+        int lev = 0;
+        for (int l = 1; mean > (uint64_t)kBlockMax && l < kMaxLevels; ++l, ++lev) mean >>= d.width(l);
+        l0b = 1 ^ (lev & 1);
+        if (const char *e = std::getenv("GKM_L0_BUF")) l0b = std::atoi(e) & 1;
+    }
+    rc = d.run_l0(0, c->sba_len, c->keys[l0b], c->vals[l0b], c->elem_cap + 64, &found);
     if (rc != GK_OK) return rc;
     if (found != c->n) return fail(c, GK_E_HIP, "msd: k-mer count differs from the enumeration");
-    rc = d.classify(1u << d.width(0), d.width(0), 0, 0, nullptr, nullptr, 1, nullptr, d.width(0));
+    rc = d.classify(1u << d.width(0), d.width(0), l0b, 0, nullptr, nullptr, 1, nullptr, d.width(0));
     if (rc != GK_OK) return rc;
-    rc = d.levels(1, d.width(0), 0);
+    rc = d.levels(1, d.width(0), l0b);
     if (rc != GK_OK) return rc;
     rc = d.finish();
     for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
         rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));
+    timer_end(c, d.total_slot);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Prefetched L0 (gk_sort_hint).  The end-to-end interval of a sort -- the sequence in host memory
+// to the sorted product in HBM -- is the packed transfer (host-bound: ~20 ms for 3.1 Gb) followed
+// by the sort, whose first pass (L0 count + partition, ~14 ms at C3) needs only the sequence.  With
+// a hint, gk_set_sequence runs that pass while the sequence streams in: the k-mer starts [0, n) of
+// a single-contig ACGT sba are cut into regions of whole L0 tiles; as soon as the transfer has
+// unpacked a region's bytes (and its last tile's halo) on the context's stream, the region is
+// counted, scanned and partitioned on the prefetch stream into keys[1] / vals[1] / the digit bytes
+// at output indices from its first position (MsdDriver::l0_region), and its 2^w0 buckets become
+// pieces.  gk_sort(k) then starts at the first level from those pieces (msd_sort_prefetched, the
+// key-range shards' first_level_from_pieces) -- the same stable order: a bucket's pieces are taken
+// in region order, i.e. start order.  Any other use of the buffers drops the prefetch (pre_drop).
+// ---------------------------------------------------------------------------------------------
+struct L0Prefetch {
+    KeySpec ks{};
+    uint64_t len = 0, n = 0;        // sba bytes, k-mer starts
+    uint32_t nreg = 0, tpr = 0;     // regions, L0 tiles per region
+    uint32_t nc_max = 0, next = 0;  // chunk-table entries per region; next region to launch
+    int w0 = 7, w1 = 8;
+    uint32_t *tab = nullptr;        // per region: c_first[nc_max], c_ntiles[nc_max], misc[4]
+    uint32_t *pieces = nullptr;     // per region: 2^w0 bases, then 2^w0 counts
+    uint64_t lo(uint32_t r) const { return (uint64_t)r * tpr * kP0Tile; }
+    uint64_t hi(uint32_t r) const { return std::min<uint64_t>(lo(r + 1), n); }
+    uint32_t tiles(uint32_t r) const { return (uint32_t)((hi(r) - lo(r) + kP0Tile - 1) / kP0Tile); }
+    // bytes a region's tiles read: each tile loads its positions plus a 96-byte halo
+    uint64_t need(uint32_t r) const { return std::min<uint64_t>(lo(r) + (uint64_t)tiles(r) * kP0Tile + 128, len); }
+};
+
+static KeySpec hint_spec(uint32_t k) {
+    KeySpec ks{};
+    ks.bits = 2;
+    ks.symbols = (int)k;
+    ks.min_len = (int)k;
+    ks.words = 1;
+    ks.total_bits = 2 * (int)k;
+    return ks;
+}
+
+bool prefetch_matches(const gk_ctx *c, const KeySpec &ks) {
+    return c->pre_valid && c->enumerated && ks.bits == 2 && ks.symbols == (int)c->pre_k &&
+           ks.min_len == ks.symbols && ks.words == 1 && ks.lenbits == 0 && !ks.canonical && !ks.acgt_only &&
+           c->nseg == 1 && c->n + ks.symbols - 1 == c->sba_len;
+}
+
+int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
+    *out = nullptr;
+    const uint32_t k = c->hint_k;
+    if (k < 8 || k > 32 || c->nseg != 1 || len < (uint64_t)k + kP0Tile) return GK_OK;
+    const KeySpec ks = hint_spec(k);
+    MsdDriver d(c, ks);
+    if (d.width(0) != 7 && d.width(0) != kGR) return GK_OK;  // (the wide L0 has its own tiles)
+    auto *p = new L0Prefetch();
+    p->ks = ks;
+    p->len = len;
+    p->n = len - k + 1;
+    p->w0 = d.width(0);
+    p->w1 = d.width(1);
+    const uint64_t nt = (p->n + kP0Tile - 1) / kP0Tile;
+    // regions: GKM_PREFETCH_REGIONS (default 16); the last region's pass is what the transfer
+    // cannot hide
+    const char *e = std::getenv("GKM_PREFETCH_REGIONS");
+    const uint64_t want = std::max<uint64_t>(1, e && *e ? std::strtoull(e, nullptr, 10) : 16);
+    p->tpr = (uint32_t)std::max<uint64_t>(1, (nt + want - 1) / want);
+    p->nreg = (uint32_t)((nt + p->tpr - 1) / p->tpr);
+    p->nc_max = (p->tpr + d.ctiles - 1) / d.ctiles;
+    const uint32_t R = 1u << p->w0, stride = 2 * p->nc_max + 4;
+    int rc = ensure_elems(c, len, 1);  // keys[1] / vals[1] by position (n <= len)
+    if (rc != GK_OK) {
+        delete p;
+        return rc;
+    }
+    GK_TRY_HIP(c, msd_tables());
+    uint8_t *ndp;
+    uint32_t *dummy;
+    GK_TRY_HIP(c, scratch(c, "msd_nd", len + 64, &ndp));
+    GK_TRY_HIP(c, scratch(c, "pre_tables", (uint64_t)p->nreg * stride, &p->tab));
+    GK_TRY_HIP(c, scratch(c, "pre_pieces", (uint64_t)p->nreg * 2 * R, &p->pieces));
+    GK_TRY_HIP(c, scratch(c, "s_misc", 4, &dummy));
+    rc = d.tables(p->tpr, p->nc_max, 1);
+    if (rc != GK_OK) {
+        delete p;
+        return rc;
+    }
+    std::vector<uint32_t> h((uint64_t)p->nreg * stride, 0);
+    for (uint32_t r = 0; r < p->nreg; ++r) {
+        uint32_t *t = h.data() + (uint64_t)r * stride;
+        const uint32_t ntr = p->tiles(r), ncr = (ntr + d.ctiles - 1) / d.ctiles;
+        for (uint32_t j = 0; j < ncr; ++j) {
+            t[j] = j * d.ctiles;
+            t[p->nc_max + j] = std::min<uint32_t>(d.ctiles, ntr - j * d.ctiles);
+        }
+        t[2 * p->nc_max] = 0;                        // s_cfirst
+        t[2 * p->nc_max + 1] = ncr;                  // s_nchunks
+        t[2 * p->nc_max + 2] = (uint32_t)p->lo(r);   // s_start: outputs by position
+    }
+    GK_TRY_HIP(c, hipMemcpy(p->tab, h.data(), 4 * h.size(), hipMemcpyHostToDevice));
+    if (!c->pre_stream) GK_TRY_HIP(c, hipStreamCreateWithFlags(&c->pre_stream, hipStreamNonBlocking));
+    if (!c->pre_done) GK_TRY_HIP(c, hipEventCreateWithFlags(&c->pre_done, hipEventDisableTiming));
+    while (c->pre_ev.size() < p->nreg) {
+        hipEvent_t ev;
+        GK_TRY_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->pre_ev.push_back(ev);
+    }
+    *out = p;
+    return GK_OK;
+}
+
+int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
+    if (!p || p->next >= p->nreg || landed < p->need(p->next)) return GK_OK;
+    // every unpack enqueued so far on c->stream; the regions now covered wait for them
+    GK_TRY_HIP(c, hipEventRecord(c->pre_ev[p->next], c->stream));
+    GK_TRY_HIP(c, hipStreamWaitEvent(c->pre_stream, c->pre_ev[p->next], 0));
+    hipStream_t keep = c->stream;
+    c->stream = c->pre_stream;
+    MsdDriver d(c, p->ks);
+    GK_TRY_HIP(c, scratch(c, "msd_nd", p->len + 64, &d.nd));
+    const uint32_t R = 1u << p->w0, stride = 2 * p->nc_max + 4;
+    int rc = GK_OK;
+    int slot;
+    timer_begin(c, "prefetch_l0", &slot);
+    uint64_t units = 0;
+    for (; rc == GK_OK && p->next < p->nreg && landed >= p->need(p->next); ++p->next) {
+        const uint32_t r = p->next, ntr = p->tiles(r);
+        rc = d.l0_region(p->lo(r), p->hi(r), ntr, (ntr + d.ctiles - 1) / d.ctiles, p->tab + (uint64_t)r * stride,
+                         p->len + 16, p->pieces + (uint64_t)r * 2 * R);
+        units += p->hi(r) - p->lo(r);
+    }
+    timer_units(c, slot, units);
+    timer_end(c, slot);
+    c->stream = keep;
+    return rc;
+}
+
+int prefetch_finish(gk_ctx *c, L0Prefetch *p, bool ok) {
+    if (!p) return GK_OK;
+    int rc = GK_OK;
+    if (ok) rc = prefetch_launch(c, p, p->len);
+    if (p->next > 0) {  // later work on the context's stream comes after the prefetch's
+        GK_TRY_HIP(c, hipEventRecord(c->pre_done, c->pre_stream));
+        GK_TRY_HIP(c, hipStreamWaitEvent(c->stream, c->pre_done, 0));
+    }
+    c->pre_valid = ok && rc == GK_OK && p->next == p->nreg;
+    c->pre_k = (uint32_t)p->ks.symbols;
+    c->pre_regions = p->nreg;
+    c->pre_w0 = p->w0;
+    c->pre_w1 = p->w1;
+    delete p;
+    return rc;
+}
+
+// gk_sort(k) after a prefetched L0: the regions' buckets are the pieces of the first level
+int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
+    c->pre_valid = false;  // consumed
+    MsdDriver d(c, ks);
+    d.B = ks.total_bits;
+    if (d.width(0) != c->pre_w0 || d.width(1) != c->pre_w1) return msd_sort(c, ks);  // (widths changed)
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.wkeys = 1;  // one-word keys end final in keys[0]
+    c->msd_keys_final = true;
+    timer_begin(c, "msd_total", &d.total_slot);
+    int rc = d.init(c->n);
+    if (rc != GK_OK) return rc;
+    const uint32_t R = 1u << c->pre_w0, nreg = c->pre_regions;
+    uint32_t *pieces;
+    GK_TRY_HIP(c, scratch(c, "pre_pieces", (uint64_t)nreg * 2 * R, &pieces));
+    std::vector<uint32_t> h((uint64_t)nreg * 2 * R);
+    GK_TRY_HIP(c, hipMemcpyAsync(h.data(), pieces, 4 * h.size(), hipMemcpyDeviceToHost, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> poff, plen;
+    std::vector<uint32_t> pb;
+    for (uint32_t b = 0; b < R; ++b)
+        for (uint32_t r = 0; r < nreg; ++r) {  // a bucket's pieces in region order = start order
+            const uint32_t cnt = h[(uint64_t)r * 2 * R + R + b];
+            if (!cnt) continue;
+            poff.push_back(h[(uint64_t)r * 2 * R + b]);
+            plen.push_back(cnt);
+            pb.push_back(b);
+        }
+    GK_TRY_HIP(c, scratch(c, "msd_nd", c->sba_len + 64, &d.nd));
+    d.nd_ready = true;  // the regions' L0 wrote the level-1 digit bytes
+    rc = d.first_level_from_pieces(c->keys[1], c->vals[1], poff.data(), plen.data(), pb.data(),
+                                   (uint32_t)poff.size(), 1, d.width(0));
+    if (rc == GK_OK) rc = d.levels(2, d.width(0) + d.width(1), 0);
+    if (rc == GK_OK) rc = d.finish();
     timer_end(c, d.total_slot);
     return rc;
 }

@@ -174,11 +174,12 @@ bool have_avx2() {
 }
 
 // one chunk into a staging slot; returns the bytes used (header + payloads)
-uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen) {
+uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen, bool *all_packed) {
     const uint32_t nb = (uint32_t)((len + kXBlock - 1) / kXBlock);
     uint32_t *hdr = reinterpret_cast<uint32_t *>(slot);
     uint64_t off = kHeaderBytes;
     const bool avx2 = have_avx2();
+    *all_packed = true;
     for (uint32_t b = 0; b < nb; ++b) {
         const uint8_t *s = src + (uint64_t)b * kXBlock;
         const uint64_t blen = std::min<uint64_t>(kXBlock, len - (uint64_t)b * kXBlock);
@@ -190,6 +191,7 @@ uint64_t pack_chunk(const uint8_t *src, uint64_t len, uint8_t *slot, Census &cen
             continue;
         }
         std::memcpy(d, s, blen);
+        *all_packed = false;
         for (uint64_t i = 0; i < blen; ++i) {
             cen.cls_or |= 1u << kClass.c[s[i]];
             cen.dollars += s[i] == GK_DOLLAR;
@@ -326,7 +328,11 @@ static bool host_pinned(const void *p) {
 //           two ends meet where packing and copying balance; raw chunks get their alphabet census
 //           on the device (launch_alphabet_range).
 // *cls_or / *dollars: the census (host part + device part).
-int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars) {
+//   prefetch (pf, a sort hint: gkm_msd.hip L0Prefetch) the regions of the sort's L0 pass are launched
+//           as the in-order prefix of unpacked chunks covers them; a chunk with a raw block (not
+//           ACGT) drops the prefetch.
+int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_or, uint64_t *dollars,
+                    L0Prefetch *pf) {
     const uint64_t bpc = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("GKM_PACK_BLOCKS", 128), 256));
     const uint64_t chunk = bpc * kXBlock;
     const uint64_t C = (len + chunk - 1) / chunk;
@@ -337,6 +343,10 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // alone (3.1 Gb from pinned memory: 24.8-27.4 against 21.0-21.6 ms, profiles/r4/xfer_threads_numa.txt)
     // -- the packing is bound by host memory bandwidth, which the DMA reads share
     const bool hybrid = env_u64("GKM_XFER_HYBRID", 0) != 0 && host_pinned(sba);
+    if (hybrid && pf) {  // (raw chunks from the back: no in-order prefix to prefetch behind)
+        if (int rc = prefetch_finish(c, pf, false)) return rc;
+        pf = nullptr;
+    }
     // the copy streams write the resident sba and the staging slots outside the context's stream:
     // everything queued before (an earlier sort reading the sba, an earlier transfer's unpacks,
     // which read the slots xfer_slots may free and reallocate) has to be done first
@@ -356,6 +366,10 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     std::vector<int> free_slots;             // slots ready to be packed into
     std::vector<std::pair<uint64_t, int>> ready;  // (chunk, slot) packed, not yet issued
     std::vector<uint64_t> used(S, 0);        // bytes of the packed chunk in each slot
+    std::vector<char> all_packed(C, 0);      // chunk k had no raw block (prefetch)
+    std::vector<char> chunk_issued(C, 0);    // chunk k's unpack is enqueued
+    uint64_t prefix = 0;                     // chunks [0, prefix) issued
+    bool pf_ok = pf != nullptr;
     bool abort = false;
     for (int i = 0; i < S; ++i) free_slots.push_back(i);
     std::atomic<uint32_t> cls{0};
@@ -375,11 +389,13 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
                 free_slots.pop_back();
             }
             const uint64_t at = k * chunk, m = std::min(chunk, len - at);
-            const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (uint64_t)slot * c->xfer_slot_bytes, cen);
+            bool whole = false;
+            const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (uint64_t)slot * c->xfer_slot_bytes, cen, &whole);
             _mm_sfence();  // the chunk's streaming stores are globally visible before it is queued
             {
                 std::lock_guard<std::mutex> lk(mu);
                 used[slot] = u;
+                all_packed[k] = whole ? 1 : 0;
                 ready.emplace_back(k, slot);
             }
             cv.notify_all();
@@ -436,6 +452,22 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             inflight.push_back(s);
             ++issued;
             progress = true;
+            chunk_issued[k] = 1;
+        }
+        // prefetch: the in-order prefix of enqueued unpacks has grown -- launch the L0 regions it covers
+        if (pf_ok && err == hipSuccess && prefix < C && chunk_issued[prefix]) {
+            bool raw = false;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                for (; prefix < C && chunk_issued[prefix]; ++prefix) raw |= !all_packed[prefix];
+            }
+            if (raw) {
+                pf_ok = false;
+            } else if (int rc = prefetch_launch(c, pf, std::min(prefix * chunk, len))) {
+                pf_ok = false;
+                err = hipErrorUnknown;
+                (void)rc;
+            }
         }
         // recycle slots whose unpack has run
         for (size_t i = 0; i < inflight.size() && err == hipSuccess;) {
@@ -493,6 +525,10 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     }
     cv.notify_all();
     for (auto &th : pool) th.join();
+    if (pf) {
+        const int rc = prefetch_finish(c, pf, pf_ok && err == hipSuccess && prefix == C);
+        if (err == hipSuccess && rc != GK_OK) return rc;
+    }
     if (err != hipSuccess) return hip_fail(c, err, "packed sba transfer");
     uint32_t cen[2] = {0, 0};
     if (hybrid && raw_chunks) {  // the device census of the raw chunks (waits for them to land)

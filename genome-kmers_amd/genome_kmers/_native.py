@@ -56,7 +56,7 @@ EXPORTED = (
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range", "gk_shard_class_b", "gk_shard_class_b_copy",
     "gk_shard_sort_range_b", "gk_rank_mode", "gk_reference_random_bases",
-    "gk_copy_sequence",
+    "gk_copy_sequence", "gk_sort_hint",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
@@ -102,6 +102,7 @@ _SIGS = {
     "gk_sync": ([_P], ctypes.c_int),
     "gk_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "gk_set_sequence": ([_P, _U8P, ctypes.c_uint64, _U32P, ctypes.c_uint64], ctypes.c_int),
+    "gk_sort_hint": ([_P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "gk_alphabet_is_acgt": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "gk_enumerate": ([_P, ctypes.c_uint32, _U64P], ctypes.c_int),
     "gk_set_start_indices": ([_P, _U32P, ctypes.c_uint64, ctypes.c_uint32], ctypes.c_int),
@@ -306,6 +307,11 @@ class Engine:
         seg = np.ascontiguousarray(seg_starts, dtype=np.uint32)
         self._check(self.lib.gk_set_sequence(self.ctx, _ptr(sba, ctypes.c_uint8), sba.size,
                                              _ptr(seg, ctypes.c_uint32), seg.size))
+
+    def sort_hint(self, k: int):
+        """gk_sort_hint: later set_sequence calls of a single-contig A/C/G/T sequence also run the
+        first pass of sort(k) while the sequence streams in (0 clears)."""
+        self._check(self.lib.gk_sort_hint(self.ctx, int(k or 0), 0))
 
     def is_acgt(self) -> bool:
         v = ctypes.c_int(0)

@@ -485,6 +485,9 @@ class Kmers:
     def _get_engine(self) -> "_native.Engine":
         if self._engine is None:
             eng = _native.Engine()
+            # a fixed k-mer length: the transfer also runs the first pass of sort(k) (gk_sort_hint)
+            if self.min_kmer_len is not None and self.min_kmer_len == self.max_kmer_len:
+                eng.sort_hint(self.min_kmer_len)
             eng.set_sequence(self.seq_coll.forward_sba, self.seq_coll._forward_sba_seg_starts)
             self._engine = eng
         return self._engine

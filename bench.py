@@ -578,7 +578,8 @@ def main():
 
     # the product's boundary: self-check, then the transfers either side of the device boundary
     # (timing experiments of a stage's memory floor write wrong output on purpose: no check)
-    checked = 0 if os.environ.get("GKM_EXP_WAVECOPY") else window_check(eng, sba, k, canonical)
+    checked = (0 if os.environ.get("GKM_EXP_WAVECOPY") or os.environ.get("GKM_EXP_L0")
+               else window_check(eng, sba, k, canonical))
     if dist is not None:
         t = torch.tensor([job.local_kmers], dtype=torch.int64, device="cuda")
         dist.all_reduce(t)

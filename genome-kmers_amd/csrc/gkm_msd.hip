@@ -573,6 +573,33 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
     }
 }
 
+// TIMING EXPERIMENTS ONLY (GKM_EXP_L0=1, wrong output): the L0 partition's memory traffic with no
+// encoding or ranking -- each persistent workgroup walks the same tiles (XCD-aware), reads the
+// tile's sequence bytes, and writes (key, start, digit byte) for every position to 2^R runs of
+// TILE / 2^R consecutive slots per tile, run d of tile t at d * (n / 2^R) + t * (TILE / 2^R): the
+// real layout of an L0 output over uniform digits.  Its time is the floor of the L0's scatter.
+template <int T, int I, int R>
+__global__ __launch_bounds__(T) void l0_scatter_floor_kernel(const uint8_t *__restrict__ sba, uint64_t n,
+                                                             uint32_t ntiles, uint64_t *__restrict__ kout,
+                                                             uint32_t *__restrict__ vout, uint8_t *__restrict__ nd) {
+    constexpr int TILE = T * I, RUN = TILE >> R;
+    const TileWalk walk(ntiles);
+    const uint64_t bsz = n >> R;
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        const uint64_t P0 = (uint64_t)t * TILE;
+        const uint32_t x = reinterpret_cast<const uint32_t *>(sba + P0)[threadIdx.x];  // (the tile's bytes)
+#pragma unroll 4
+        for (int g = 0; g < I; ++g) {
+            const uint32_t s = threadIdx.x + g * T, d = s / RUN, j = s - d * RUN;
+            const uint64_t o = min((uint64_t)d * bsz + (uint64_t)t * RUN + j, n - 1);
+            const uint64_t h = (P0 + s + (x & 1u)) * 0x9E3779B97F4A7C15ull;  // distinct keys, uniform digits
+            kout[o] = h;
+            vout[o] = (uint32_t)(P0 + s);
+            nd[o] = (uint8_t)(h >> 49);
+        }
+    }
+}
+
 // Wide L0 partition (R = 10 or 11 bits; 2-bit keys of one word, forward, no profile): the
 // position-staged, software-pipelined scheme of msd0_pipe_kernel with a digit space the 7-bit one
 // cannot hold -- per-wave u16 counters, two per word (rank_atomic16), K = RADIX / T digits per
@@ -2703,7 +2730,12 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
-        l0_dispatch(false, w0, with_nd, l0a, d0, (unsigned)l0_tiles, kout, vout, (uint32_t)l0_tiles, count, ndg);
+        static const bool exp_l0 = std::getenv("GKM_EXP_L0") != nullptr;  // timing experiments only
+        if (exp_l0 && with_nd && w0 == 7)
+            hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 7>), dim3(pgrid), dim3(kP0T), 0, c->stream, c->sba,
+                               count, (uint32_t)l0_tiles, kout, vout, nd);
+        else
+            l0_dispatch(false, w0, with_nd, l0a, d0, (unsigned)l0_tiles, kout, vout, (uint32_t)l0_tiles, count, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = with_nd;
@@ -2715,12 +2747,13 @@ struct MsdDriver {
     // region's 2^w0 bucket bases and counts into `pieces` -- all on c->stream (the caller points it
     // at the prefetch stream), with the region's chunk tables already in `tab` (c_first[nc],
     // c_ntiles[nc], then s_cfirst, s_nchunks, s_start) and no host round trip
-    int l0_region(uint64_t lo, uint64_t hi, uint32_t nt, uint32_t nc, uint32_t *tab, uint64_t sink, uint32_t *pieces) {
+    int l0_region(uint64_t lo, uint64_t hi, uint32_t nt, uint32_t nc, uint32_t nc_max, uint32_t *tab, uint64_t sink,
+                  uint32_t *pieces) {
         int rc = tables(nt, nc, 1);  // (allocated by prefetch_plan: no reallocation here)
         if (rc != GK_OK) return rc;
-        c_first = tab;
-        c_ntiles = tab + nc;
-        const uint32_t *misc = tab + 2 * nc;
+        c_first = tab;  // (the region's table: nc_max entries each, then misc)
+        c_ntiles = tab + nc_max;
+        const uint32_t *misc = tab + 2 * nc_max;
         const L0Args a{c->sba, lo, hi, ks.symbols, B, 0};
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
@@ -3492,8 +3525,8 @@ int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     uint64_t units = 0;
     for (; rc == GK_OK && p->next < p->nreg && landed >= p->need(p->next); ++p->next) {
         const uint32_t r = p->next, ntr = p->tiles(r);
-        rc = d.l0_region(p->lo(r), p->hi(r), ntr, (ntr + d.ctiles - 1) / d.ctiles, p->tab + (uint64_t)r * stride,
-                         p->len + 16, p->pieces + (uint64_t)r * 2 * R);
+        rc = d.l0_region(p->lo(r), p->hi(r), ntr, (ntr + d.ctiles - 1) / d.ctiles, p->nc_max,
+                         p->tab + (uint64_t)r * stride, p->len + 16, p->pieces + (uint64_t)r * 2 * R);
         units += p->hi(r) - p->lo(r);
     }
     timer_units(c, slot, units);

@@ -94,6 +94,25 @@ def test_prefetch_many_chunks_threads_and_regions(monkeypatch):
     same(got, want)
 
 
+@pytest.mark.parametrize("chunk_tiles", ["1", "2", "3"])
+def test_prefetch_multi_chunk_region_scans(chunk_tiles, monkeypatch):
+    # regions of 5 tiles in column-scan chunks of 1-3 tiles, the last region shorter (fewer chunks
+    # than the others: its tables sit at the same stride) -- the multi-chunk scan branch that only
+    # full-size inputs reach with the default 256-tile chunks
+    monkeypatch.setenv("GKM_TEST_CHUNK_TILES", chunk_tiles)
+    rng = np.random.default_rng(int(chunk_tiles))
+    L = 32 * 24576 + 1234
+    sba = genome(rng, L, repeat=2000, copies=7)
+    seg = np.zeros(1, dtype=np.uint32)
+    _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=7)
+    assert "prefetch_l0" in rep and "msd_pass_l0" not in rep
+    monkeypatch.delenv("GKM_TEST_CHUNK_TILES")
+    _, want, _ = run(sba, seg, 31, monkeypatch, False)
+    same(got, want)
+    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, np.arange(L - 30, dtype=np.uint32), 31, 31,
+                                                           break_ties=True))
+
+
 def test_prefetch_consumed_once_and_dropped_by_other_calls(monkeypatch):
     rng = np.random.default_rng(4)
     L = 200_000
@@ -161,9 +180,13 @@ def test_no_prefetch_outside_single_contig_acgt(kind, monkeypatch):
         sba[90_000:90_050] = ord("N")
         seg = np.zeros(1, dtype=np.uint32)
     _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=4)
-    assert "prefetch_l0" not in rep
+    if kind == "contigs":  # never planned
+        assert "prefetch_l0" not in rep
+    # (an N block drops the prefetch when its chunk lands: regions before it may have run, unused)
     _, want, _ = run(sba, seg, 31, monkeypatch, False, regions=4)
     same(got, want)
+    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, oracle.enumerate_starts(sba, seg, 31), 31, 31,
+                                                           break_ties=True))
 
 
 def test_kmers_api_fixed_length_uses_the_hint(monkeypatch):

@@ -2998,8 +2998,12 @@ struct MsdDriver {
         rc = level_pass(level, hi, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
         if (rc != GK_OK) return rc;
         cur_big = 0;
+        uint64_t before[kLocal];
+        for (int k = 0; k < kLocal; ++k) before[k] = nloc[k];
         rc = classify(nseg << width(level), hi + width(level), 0, cur_big, nullptr, nullptr, 1, s_pref, width(level),
                       compact_now ? 1 : 0);
+        // (as levels(): a packed-pair level's local sub-buckets back to (key, start))
+        if (rc == GK_OK && c79_out) rc = expand_pair_locals(before, 0);
         return rc == GK_OK ? expand_big(0) : rc;
     }
 
@@ -3065,6 +3069,7 @@ struct MsdDriver {
         nbig = 0;
         for (int k = 0; k < kLocal; ++k) nloc[k] = loc_elems[k] = 0;
         nd_ready = false;
+        c79_in = false;
         int rc = classify(ng, 0, 0, cur_big, g_start, g_len, 2);
         if (rc != GK_OK) return rc;
         rc = levels(1, 0, 0);
@@ -3102,6 +3107,7 @@ struct MsdDriver {
         B = bkey;
         phase = 1;  // (no compact or packed-pair levels: later-phase rules)
         nd_ready = false;
+        c79_in = false;
         int rc = classify(ng, 0, 0, cur_big, g_start, g_len, 2);
         if (rc != GK_OK) return rc;
         rc = levels(1, 0, 0);
@@ -3138,8 +3144,8 @@ struct MsdDriver {
 
     // global levels while the next-level list is non-empty; `in` holds the current buffer, hi
     // key bits are sorted
+    // (c79_in carries over: a first level from pieces may have written packed pairs)
     int levels(int level, int hi, int in) {
-        c79_in = false;
         while (nbig > 0) {
             const int out = in ^ 1;
             uint32_t *ntl, *nch, *tfirst, *cfirst;

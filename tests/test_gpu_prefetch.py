@@ -113,6 +113,27 @@ def test_prefetch_multi_chunk_region_scans(chunk_tiles, monkeypatch):
                                                            break_ties=True))
 
 
+def test_prefetch_large_packed_pair_levels():
+    # 3e8 bases: the first level from the prefetched pieces writes packed pairs and the compact level
+    # behind it reads them (the C3 level structure), with the default chunking and 16 regions
+    from genome_kmers import synthetic
+
+    sba, seg = synthetic.c3_genome(300_000_000, 42)
+    outs = []
+    for hint in (31, 0):
+        eng = _native.Engine()
+        eng.sort_hint(hint)
+        eng.profile_enable(True)
+        eng.set_sequence(sba, seg)
+        n = eng.enumerate(31)
+        eng.sort(31)
+        rep = eng.profile_report()
+        assert ("prefetch_l0" in rep) == (hint != 0) and ("msd_pass_l1p" in rep or "msd_pass_l1" in rep)
+        outs.append(eng.copy_starts(np.empty(n, dtype=np.uint32)))
+        del eng
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
 def test_prefetch_consumed_once_and_dropped_by_other_calls(monkeypatch):
     rng = np.random.default_rng(4)
     L = 200_000

@@ -3424,13 +3424,14 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
 struct L0Prefetch {
     KeySpec ks{};
     uint64_t len = 0, n = 0;        // sba bytes, k-mer starts
-    uint32_t nreg = 0, tpr = 0;     // regions, L0 tiles per region
+    uint32_t nreg = 0, tpr = 0;     // regions, L0 tiles of the largest region
     uint32_t nc_max = 0, next = 0;  // chunk-table entries per region; next region to launch
     int w0 = 7, w1 = 8;
     uint32_t *tab = nullptr;        // per region: c_first[nc_max], c_ntiles[nc_max], misc[4]
     uint32_t *pieces = nullptr;     // per region: 2^w0 bases, then 2^w0 counts
-    uint64_t lo(uint32_t r) const { return (uint64_t)r * tpr * kP0Tile; }
-    uint64_t hi(uint32_t r) const { return std::min<uint64_t>(lo(r + 1), n); }
+    std::vector<uint64_t> first;    // first L0 tile of each region (+ the end)
+    uint64_t lo(uint32_t r) const { return first[r] * kP0Tile; }
+    uint64_t hi(uint32_t r) const { return std::min<uint64_t>(first[r + 1] * kP0Tile, n); }
     uint32_t tiles(uint32_t r) const { return (uint32_t)((hi(r) - lo(r) + kP0Tile - 1) / kP0Tile); }
     // bytes a region's tiles read: each tile loads its positions plus a 96-byte halo
     uint64_t need(uint32_t r) const { return std::min<uint64_t>(lo(r) + (uint64_t)tiles(r) * kP0Tile + 128, len); }
@@ -3470,8 +3471,22 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     // cannot hide
     const char *e = std::getenv("GKM_PREFETCH_REGIONS");
     const uint64_t want = std::max<uint64_t>(1, e && *e ? std::strtoull(e, nullptr, 10) : 16);
-    p->tpr = (uint32_t)std::max<uint64_t>(1, (nt + want - 1) / want);
-    p->nreg = (uint32_t)((nt + p->tpr - 1) / p->tpr);
+    // equal regions, but the last one's share is cut into halving pieces (1/2, 1/4, 1/8, 1/8 of it):
+    // the pass of the last region to land is what the transfer cannot hide
+    const uint64_t tpr = std::max<uint64_t>(1, (nt + want - 1) / want);
+    for (uint64_t f = 0; f < nt; f += tpr) {
+        const uint64_t e = std::min(nt, f + tpr);
+        if (e == nt && e - f >= 8) {
+            const uint64_t m = e - f;
+            for (uint64_t g : {f, f + m / 2, f + 3 * m / 4}) p->first.push_back(g);
+            p->first.push_back(f + 7 * m / 8);
+        } else {
+            p->first.push_back(f);
+        }
+    }
+    p->first.push_back(nt);
+    p->nreg = (uint32_t)(p->first.size() - 1);
+    p->tpr = (uint32_t)tpr;
     p->nc_max = (p->tpr + d.ctiles - 1) / d.ctiles;
     const uint32_t R = 1u << p->w0, stride = 2 * p->nc_max + 4;
     int rc = ensure_elems(c, len, 1);  // keys[1] / vals[1] by position (n <= len)

@@ -205,3 +205,25 @@ def test_packed_short_then_longer_sequence(monkeypatch):
     eng.sort(17)
     want = oracle.quicksort(b, oracle.enumerate_starts(b, segb, 17), 17, 17, break_ties=True)
     np.testing.assert_array_equal(eng.copy_starts(np.empty(n, dtype=np.uint32)), want)
+
+
+@pytest.mark.parametrize("impl", ["scalar", "avx2", "avx512"])
+def test_packer_implementations_agree(impl, monkeypatch):
+    # the host packer's vector paths (GKM_PACK_IMPL; read once per process, so each run is a child)
+    import subprocess
+    import sys
+
+    code = (
+        "import numpy as np, sys; sys.path.insert(0, 'genome-kmers_amd'); from genome_kmers import _native\n"
+        "rng = np.random.default_rng(5)\n"
+        "s = np.frombuffer(b'ACGT', dtype=np.uint8)[rng.integers(0, 4, 3 * 65536 + 4321)].copy()\n"
+        "s[70000:70010] = ord('N'); s[200000] = ord('$')\n"
+        "seg = np.array([0, 200001], dtype=np.uint32)\n"
+        "e = _native.Engine(); e.set_sequence(s, seg)\n"
+        "assert np.array_equal(e.copy_sequence(len(s)), s) and not e.is_acgt()\n"
+        "print('ok')\n")
+    env = dict(__import__("os").environ, GKM_PACK_IMPL=impl, GKM_PACK_MIN="0", GKM_PACK_BLOCKS="1")
+    from pathlib import Path
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(Path(__file__).resolve().parent.parent),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

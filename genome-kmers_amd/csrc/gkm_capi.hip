@@ -506,6 +506,11 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
         // device (gkm_xfer.hip); the stream orders the sort's kernels behind the last unpack, so
         // only the census is waited for
         uint64_t dollars = 0;
+        // (A/B: GKM_EARLY_ELEMS=1 -- the k-mer buffers for every position allocated here, before the
+        // transfer's staging slots, as the prefetch path does)
+        static const bool early = std::getenv("GKM_EARLY_ELEMS") != nullptr;
+        if (early)
+            if (int rc = ensure_elems(c, len, 1)) return rc;
         // a sort hint (gk_sort_hint): the L0 pass of gk_sort(k) runs as the sequence lands
         L0Prefetch *pf = nullptr;
         if (c->hint_k && nseg == 1 && !internal)

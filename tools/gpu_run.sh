@@ -55,7 +55,7 @@ for task in "$@"; do
       smi $O/smi_after_trace.txt
       cp "$(find $O/trace -name '*kernel_stats.csv' | head -1)" $O/kernel_stats.csv
       python3 tools/trace_summary.py "$(find $O/trace -name '*kernel_trace.csv' | head -1)" $O/bench_unprofiled.json \
-        $O/trace_summary.json --warmup "$WARM" --steps "$STEPS" --extra 10 | tee $O/trace_summary.txt
+        $O/trace_summary.json --warmup "$WARM" --steps "$STEPS" | tee $O/trace_summary.txt
       P=(bench.py --config "$cfg" --steps 2 --warmup 1 --no-cpu-baseline --no-boundary)
       timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM \
         SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d $O/sq -o run --output-format csv -- python3 "${P[@]}" \

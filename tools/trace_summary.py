@@ -1,19 +1,25 @@
 """Steady-state kernel times from a rocprofv3 --kernel-trace of bench.py, beside the bench's own
 HIP-event stage times from the same lease ("Reproducing the roofline").
 
-rocprofv3 --stats averages EVERY launch of a kernel, the warm-up steps included; the first step
-touches freshly allocated buffers and runs slower.  This summary also averages the launches of the
-timed window only: a kernel launched c times per step has (W + K + E) * c launches in the trace
-(W warm-up steps, K timed steps, E = 6 end-to-end steps after them), and the first W * c are
-dropped.
+rocprofv3 --stats averages EVERY launch of a kernel: the warm-up steps, and the end-to-end steps the
+bench runs after its timed ones.  This summary cuts the trace into steps instead: every step of the
+C3 sort starts with exactly one launch of the L0 count kernel (msd0_count_kernel), so step i spans
+from the i-th such launch to the next one.  The timed steps are W .. W + K - 1 (W warm-up steps
+first); each kernel's launches inside them give its mean duration and its time per step.  The bench's
+device stage times (HIP events on the engine's stream) are printed beside them.  The transfers' own
+kernels (unpack_chunk_kernel, runtime copy kernels) are left out.
 
-Usage: python tools/trace_summary.py KERNEL_TRACE.csv BENCH_LINE.json OUT.json [--warmup W --steps K --extra E]
+Usage: python tools/trace_summary.py KERNEL_TRACE.csv BENCH_LINE.json OUT.json [--warmup W --steps K]
 """
 
 import argparse
 import csv
 import json
+from bisect import bisect_right
 from collections import defaultdict
+
+MARK = "msd0_count_kernel"
+SKIP = ("unpack_chunk_kernel", "__amd_rocclr")
 
 
 def main():
@@ -23,44 +29,49 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--extra", type=int, default=6)
     a = ap.parse_args()
-    runs = defaultdict(list)
+    rows = []
     with open(a.trace) as fh:
         for r in csv.DictReader(fh):
             name = r["Kernel_Name"].replace("void ", "").split("(")[0].strip()
-            runs[name].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-    per_step = a.warmup + a.steps + a.extra
-    rows = {}
-    for name, v in runs.items():
-        v.sort()
-        d = [(e - s) / 1e6 for s, e in v]
-        c = len(d) / per_step
-        rec = {"launches": len(d), "avg_all_ms": sum(d) / len(d), "min_ms": min(d), "max_ms": max(d)}
-        if c >= 1 and abs(c - round(c)) < 1e-9:
-            c = int(round(c))
-            w = d[a.warmup * c:]
-            rec.update({"per_step": c, "avg_steady_ms": sum(w) / len(w), "first_ms": d[0],
-                        "ms_per_step_steady": sum(w) / len(w) * c})
-        rows[name] = rec
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    marks = [s for s, _, n in rows if MARK in n]
+    W, K = a.warmup, a.steps
+    if len(marks) < W + K:
+        raise SystemExit(f"{len(marks)} step markers ({MARK}) for {W} + {K} steps")
+    lo = marks[W]
+    hi = marks[W + K] if len(marks) > W + K else float("inf")
+    per = defaultdict(list)
+    for s, e, n in rows:
+        if lo <= s < hi and not any(x in n for x in SKIP):
+            per[n].append((e - s) / 1e6)
+    step_of = lambda s: bisect_right(marks, s) - 1  # noqa: E731
+    kern = {}
+    for n, d in per.items():
+        kern[n] = {"launches_in_window": len(d), "per_step": round(len(d) / K, 2), "avg_ms": sum(d) / len(d),
+                   "ms_per_step": sum(d) / K, "min_ms": min(d), "max_ms": max(d)}
     with open(a.bench) as fh:
         line = json.loads(fh.read().strip().splitlines()[-1])
     stages = line["roofline"].get("stages", {})
+    # the timed steps run back to back: the marker period over them (the last step's end is not marked)
+    period_ms = (marks[W + K - 1] - marks[W]) / 1e6 / max(K - 1, 1)
     out = {"_bench": {"ms_per_step": line["ms_per_step"], "roofline_kernel": line["roofline"]["kernel"],
                       "roofline_avg_launch_ms": line["roofline"]["avg_launch_ms"], "frac": line["roofline"]["frac"],
                       "stages_ms_per_launch": {k: v["ms_per_launch"] for k, v in stages.items()}},
+           "_trace_window": {"steps": K, "first_step": W, "step_period_ms": round(period_ms, 3),
+                             "first_marker_step": step_of(lo)},
            "_method": __doc__.split("\n\n")[1].replace("\n", " "),
-           "kernels": dict(sorted(rows.items(), key=lambda kv: -kv[1].get("ms_per_step_steady", 0)))}
-    top = [k for k, v in out["kernels"].items() if "ms_per_step_steady" in v][:1]
-    out["_dominant_by_trace"] = top[0] if top else None
+           "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1]["ms_per_step"]))}
+    top = next(iter(out["kernels"]), None)
+    out["_dominant_by_trace"] = top
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
-    print(f"bench: {line['ms_per_step']} ms/step; roofline kernel {line['roofline']['kernel'][:60]} "
-          f"avg {line['roofline']['avg_launch_ms']} ms")
+    print(f"bench (unprofiled): {line['ms_per_step']} ms/step; roofline kernel "
+          f"{line['roofline']['kernel'][:70]} avg {line['roofline']['avg_launch_ms']} ms")
+    print(f"trace (profiled): steps {W}..{W + K - 1}: one step every {period_ms:.3f} ms (L0-count markers)")
     for k, v in list(out["kernels"].items())[:12]:
-        if "ms_per_step_steady" in v:
-            print(f"  {v['ms_per_step_steady']:8.3f} ms/step  x{v['per_step']}  steady {v['avg_steady_ms']:8.3f}  "
-                  f"all {v['avg_all_ms']:8.3f}  first {v['first_ms']:8.3f}  {k[:90]}")
+        print(f"  {v['ms_per_step']:8.3f} ms/step  x{v['per_step']:<5} avg {v['avg_ms']:8.3f}  {k[:90]}")
 
 
 if __name__ == "__main__":

@@ -30,7 +30,14 @@ namespace gkm {
 
 constexpr int kGR = 8;                  // global digit bits
 constexpr int kGRadix = 1 << kGR;
-constexpr int kPT = 1024, kPI = 11;     // global partition tile: 1024 threads x 11 keys
+// global partition tile: 1024 threads x 11 keys (tuning overrides GKM_PT / GKM_PI: tools/build_variant.sh)
+#ifndef GKM_PT
+#define GKM_PT 1024
+#endif
+#ifndef GKM_PI
+#define GKM_PI 11
+#endif
+constexpr int kPT = GKM_PT, kPI = GKM_PI;
 // wide L0 (msd0_wide_kernel): 11-bit digits over 18,432-position tiles of its own, 512 threads x 36
 constexpr int kWideL0 = 11, kWT = 512, kWI = 36;
 constexpr int kPTile = kPT * kPI;

@@ -7,7 +7,7 @@
 //   host    the sba is cut into 64 KiB blocks and chunks of kBlocksPerChunk blocks.  Worker threads
 //           (up to 16) take chunks in order and write each into a pinned staging slot: a header
 //           (per block: payload offset | raw flag), then per block either the 16 KiB of 2-bit
-//           codes (every byte A/C/G/T: AVX-512 or AVX2 compare + pack, 64 bases per step) or the raw bytes
+//           codes (every byte A/C/G/T: AVX2 compare + pack, 64 bases per step; AVX-512 on request) or the raw bytes
 //           (anything else: '$' separators, N runs, IUPAC letters).  The same pass takes the
 //           alphabet census the reference's check needs (sequence_collection.py:441-458, 694-697):
 //           classes seen and '$' count -- no device pass over the sba afterwards.
@@ -196,14 +196,16 @@ bool have_avx2() {
     return v;
 }
 
-// GKM_PACK_IMPL=scalar / avx2 / avx512 (A/B and tests); default: the widest the CPU has
+// GKM_PACK_IMPL=scalar / avx2 / avx512 (A/B and tests); default AVX2: on the GPU box's EPYC 9575F
+// the AVX-512 packer moved 3.1 Gb in 25-29 ms against 22 ms for AVX2, 16 threads, medians of 7
+// (profiles/r5/xfer_probe.txt) -- the packing is bound by host memory, not by instructions
 int pack_impl() {
     static const int v = [] {
         const char *e = std::getenv("GKM_PACK_IMPL");
         const bool a512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512f");
         if (e && !std::strcmp(e, "scalar")) return 0;
-        if (e && !std::strcmp(e, "avx2")) return have_avx2() ? 1 : 0;
-        return a512 ? 2 : have_avx2() ? 1 : 0;
+        if (e && !std::strcmp(e, "avx512")) return a512 ? 2 : have_avx2() ? 1 : 0;
+        return have_avx2() ? 1 : 0;
     }();
     return v;
 }

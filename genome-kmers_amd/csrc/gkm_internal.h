@@ -168,6 +168,7 @@ struct gk_ctx {
     bool pre_valid = false;          // keys[1] / vals[1] / scratch "msd_nd" + "pre_pieces" hold it
     uint32_t pre_k = 0, pre_regions = 0;
     int pre_w0 = 0, pre_w1 = 0;
+    int pre_p88_shi = 0;             // != 0: the regions wrote the packed L0 form (gkm_msd.hip P88)
 
     // profiling
     bool profile = false;

@@ -415,7 +415,10 @@ constexpr int kP0T = GKM_L0_T;           // L0 tile: kP0T threads x kP0I positio
 constexpr int kP0I = GKM_L0_I;
 constexpr int kP0Tile = kP0T * kP0I;     // 24,576 (< 65,536: positions staged as u16)
 
-template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false>
+// P88 (the packed L0, round 5): each element leaves as the level-1 digit byte (nd), the key bits below
+// it above the start's high bits (u64: key << shi | start >> (32 - shi)) and the start's low bits
+// (u16 in nd.out16) -- 11 B instead of 13 (key, start, digit); the level behind reads it (INP = 2)
+template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false, bool P88 = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t ntiles, uint64_t sink, NextDigits nd) {
@@ -466,9 +469,17 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
         const uint32_t p = s_pos[b ^ 1][s];
         const uint64_t key = l0_key_of<BITS, CANON>(s_code[b ^ 1], p, a.total_bits, a.symbols);
         const uint64_t o = pcnt ? (uint64_t)(s_toff[b ^ 1][dg_of(key, d0)] + s) : sink;
-        kout[o] = key;
-        vout[o] = (uint32_t)(pP0 + p);
-        if (ND) nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        if (P88) {
+            const uint32_t st = (uint32_t)(pP0 + p);
+            const int shi = nd.pshi;
+            kout[o] = (key << shi) | (st >> (32 - shi));  // (the sorted and digit bits shift out)
+            nd.out16[o] = (uint16_t)(st & ((1u << (32 - shi)) - 1));
+            nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        } else {
+            kout[o] = key;
+            vout[o] = (uint32_t)(pP0 + p);
+            if (ND) nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        }
         // keep each group's loads and stores in place: hoisting the groups' LDS reads ahead (the
         // scheduler's choice) keeps 22 groups' positions and keys live and spills them to scratch,
         // whose vmcnt waits then drain every store in flight
@@ -1292,6 +1303,70 @@ __global__ __launch_bounds__(256) void expand_pair_list_kernel(const uint2 *__re
         uint32_t val;
         unpack_pair(kio[st + e], in16[st + e], shi, key, val);
         kio[st + e] = top | key;
+        vout[st + e] = val;
+    }
+}
+
+// packed-L0 elements (P88: the digit byte above a packed pair) -> (key bits below the sorted ones,
+// start)
+__device__ __forceinline__ void unpack_p88(uint64_t a, uint32_t lo, uint32_t dg, int shi, uint64_t &rel, uint32_t &val) {
+    unpack_pair(a, lo, shi, rel, val);
+    rel |= (uint64_t)dg << (64 - shi);
+}
+
+// (key, start) of packed-L0 elements in place, for the buckets whose next reader does not take the
+// packed form: the big buckets when the level behind the L0 writes no packed pairs itself (gridDim.y
+// workgroups per bucket), and the local classes' entries (expand_p88_list_kernel)
+__global__ __launch_bounds__(256) void expand_p88_kernel(const uint32_t *__restrict__ bst,
+                                                         const uint32_t *__restrict__ blen,
+                                                         const uint64_t *__restrict__ bpref, int hi, int B, int shi,
+                                                         uint64_t *__restrict__ kio, const uint16_t *__restrict__ in16,
+                                                         const uint8_t *__restrict__ in8, uint32_t *__restrict__ vout) {
+    const uint64_t st = bst[blockIdx.x];
+    const uint32_t len = blen[blockIdx.x];
+    const uint64_t top = (bpref[blockIdx.x] & ~kCompact) << (B - hi);
+    for (uint32_t e = blockIdx.y * 256 + threadIdx.x; e < len; e += gridDim.y * 256) {
+        uint64_t rel;
+        uint32_t val;
+        unpack_p88(kio[st + e], in16[st + e], in8[st + e], shi, rel, val);
+        kio[st + e] = top | rel;
+        vout[st + e] = val;
+    }
+}
+
+__global__ __launch_bounds__(256) void expand_p88_list_kernel(const uint2 *__restrict__ list,
+                                                              const uint64_t *__restrict__ pref, int B, int shi,
+                                                              uint64_t *__restrict__ kio, const uint16_t *__restrict__ in16,
+                                                              const uint8_t *__restrict__ in8,
+                                                              uint32_t *__restrict__ vout) {
+    const uint2 en = list[blockIdx.x];
+    const uint64_t st = en.x;
+    const uint32_t len = en.y >> 8;
+    const int hi = (en.y >> 1) & 127;
+    const uint64_t top = (pref[blockIdx.x] & ~kCompact) << (B - hi);
+    for (uint32_t e = threadIdx.x; e < len; e += 256) {
+        uint64_t rel;
+        uint32_t val;
+        unpack_p88(kio[st + e], in16[st + e], in8[st + e], shi, rel, val);
+        kio[st + e] = top | rel;
+        vout[st + e] = val;
+    }
+}
+
+// the same over pieces (first_level_from_pieces: the prefetched L0's region buckets): piece j at
+// pp[j], pp[np + j] elements, its bucket (the top hi key bits) pp[2 np + j]
+__global__ __launch_bounds__(256) void expand_p88_pieces_kernel(const uint64_t *__restrict__ pp, uint32_t np, int hi,
+                                                                int B, int shi, uint64_t *__restrict__ kio,
+                                                                const uint16_t *__restrict__ in16,
+                                                                const uint8_t *__restrict__ in8,
+                                                                uint32_t *__restrict__ vout) {
+    const uint64_t st = pp[blockIdx.x], len = pp[np + blockIdx.x];
+    const uint64_t top = pp[2 * (uint64_t)np + blockIdx.x] << (B - hi);
+    for (uint64_t e = blockIdx.y * 256 + threadIdx.x; e < len; e += gridDim.y * 256) {
+        uint64_t rel;
+        uint32_t val;
+        unpack_p88(kio[st + e], in16[st + e], in8[st + e], shi, rel, val);
+        kio[st + e] = top | rel;
         vout[st + e] = val;
     }
 }
@@ -2440,6 +2515,12 @@ struct MsdDriver {
     // the sorted ones, start) pairs + the digit byte instead of 12-byte (key, start) + digit; the
     // compact level reads them (IN79).  allow_c79: msd_sort's own levels (GKM_NO_PAIRS=1: off)
     bool allow_c79 = false, c79_in = false, c79_out = false;
+    // the packed L0 (P88, msd0_pipe_kernel): its output is (digit byte, packed pair) in nd_l0 /
+    // lo16_l0 / keys; p88_in: the next level reads it (p88_wanted: msd_sort's decision)
+    bool p88 = false, p88_in = false, pieces_level = false;
+    int p88_shi = 0;
+    uint16_t *lo16_l0 = nullptr;
+    uint8_t *nd_l0 = nullptr;
     int c79_shi = 0;
     uint16_t *lo16 = nullptr;
     uint32_t *tile_hist, *chunk_hist, *c_first, *c_ntiles, *seg_base, *seg_cnt;
@@ -2567,7 +2648,7 @@ struct MsdDriver {
 
     // L0 kernels: count (per-tile digit histograms) or partition; bits x digit width x next digits
     // x canonical
-    template <int BITS, int R, bool ND, bool CANON>
+    template <int BITS, int R, bool ND, bool CANON, bool P88 = false>
     void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
                    uint64_t sink, const NextDigits &ndg) {
         // the count pass streams the sequence: 256-thread workgroups, eight per CU, each holding a
@@ -2589,11 +2670,11 @@ struct MsdDriver {
                                dim3(std::min<unsigned>(nt0, cus * per_cu)), dim3(kP0T / 4), 0, c->stream, a, d0,
                                tile_hist, nt0);
         }
-        else if (BITS == 2 && R == 7 && !CANON && l0_prof())
+        else if (BITS == 2 && R == 7 && !CANON && !P88 && l0_prof())
             l0_prof_launch<ND>(a, d0, kout, vout, nt, sink, ndg);
         else
-            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kP0T, kP0I, R, ND, CANON>), dim3(pgrid), dim3(kP0T), 0, c->stream,
-                               a, d0, tile_hist, kout, vout, nt, sink, ndg);
+            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kP0T, kP0I, R, ND, CANON, false, P88>), dim3(pgrid), dim3(kP0T), 0,
+                               c->stream, a, d0, tile_hist, kout, vout, nt, sink, ndg);
     }
 
     // timing only (GKM_L0_PROF=1): the L0 partition with per-phase clocks, printed to stderr
@@ -2644,11 +2725,14 @@ struct MsdDriver {
                                    c->stream, a, d0, tile_hist, kout, vout, nt, sink, ndg);
             return;
         }
+        const bool pk = !count && nd_ && ndg.out16 != nullptr;  // the packed L0 (P88)
         if (ks.bits == 2 && w0 == 7) {
-            if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            if (pk) l0_launch<2, 7, true, CANON, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else l0_launch<2, 7, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
         } else if (ks.bits == 2) {
-            if (nd_) l0_launch<2, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            if (pk) l0_launch<2, kGR, true, CANON, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else if (nd_) l0_launch<2, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else l0_launch<2, kGR, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
         } else {
             if (nd_) l0_launch<4, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
@@ -2733,7 +2817,14 @@ struct MsdDriver {
         // exchange, so they do not)
         const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
-        if (with_nd) {
+        if (with_nd && p88) {  // the packed L0: digit bytes and low start bits of its own
+            GK_TRY_HIP(c, scratch(c, "msd_nd_l0", n + 64, &nd_l0));
+            GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", n + 64, &lo16_l0));
+            nd = nd_l0;
+            ndg.out = nd;
+            ndg.out16 = lo16_l0;
+            ndg.pshi = p88_shi;
+        } else if (with_nd) {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
@@ -2746,6 +2837,33 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         nd_ready = with_nd;
+        p88_in = with_nd && p88;
+        return GK_OK;
+    }
+
+    // the packed L0 pays when the level behind it writes packed pairs itself (it reads the packed
+    // form, INP = 2): the same prediction level_pass makes at L1 from the mean bucket sizes, with the
+    // L1 digit being the digit byte (8 bits).  GKM_NO_P88=1: off; GKM_TEST_P88=1 (tests): wherever
+    // the bits fit.  C3: 62 - 7 = 55 bits after the L0, 47 of them in the pair (shi 17).
+    bool p88_wanted() const {
+        if (std::getenv("GKM_NO_P88") || !allow_c79 || ks.bits != 2 || phase != 0 || no_compact()) return false;
+        const int w0 = width(0), w1 = width(1), w2 = width(2), rem = B - w0;
+        if ((w0 != 7 && w0 != kGR) || w1 != 8 || rem - 8 < 33 || rem - 8 > 48) return false;
+        if (std::getenv("GKM_TEST_P88")) return true;
+        const uint64_t m1 = (n >> w0) >> w1;  // mean L1 sub-bucket
+        const int rem2 = rem - w1 - w2;
+        return m1 >= (uint64_t)kBlockMax && (m1 >> w2) < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 && w2 == 8 &&
+               width(3) == 8;
+    }
+
+    // after the packed L0's classify: its local entries back to (key, start) for the finishing kernels
+    int expand_p88_locals(int buf) {
+        for (int k = 0; k < kLocal; ++k) {
+            if (!nloc[k]) continue;
+            hipLaunchKernelGGL(expand_p88_list_kernel, dim3((unsigned)nloc[k]), dim3(256), 0, c->stream, loc[k][0],
+                               loc_pref[k], B, p88_shi, c->keys[buf], lo16_l0, nd_l0, c->vals[buf]);
+            GK_TRY_HIP(c, hipGetLastError());
+        }
         return GK_OK;
     }
 
@@ -2769,6 +2887,10 @@ struct MsdDriver {
         rc = scan_offsets(w0, nc, misc, misc + 1, misc + 2, 1);
         if (rc != GK_OK) return rc;
         NextDigits ndg{dig_at(B, w0, width(1)), nd};
+        if (p88) {  // the packed L0 (P88): nd / lo16_l0 set by the caller
+            ndg.out16 = lo16_l0;
+            ndg.pshi = p88_shi;
+        }
         l0_dispatch(false, w0, true, a, d0, nt, c->keys[1], c->vals[1], nt, sink, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         GK_TRY_HIP(c, hipMemcpyAsync(pieces, seg_base, 4u << w0, hipMemcpyDeviceToDevice, c->stream));
@@ -2854,6 +2976,13 @@ struct MsdDriver {
             NextDigits ndg{dig_at(B, hi + R, nw), nd};
             ndg.out16 = lo16;
             ndg.pshi = c79_shi;
+            if (p88_in) {  // reading the packed L0's output
+                ndg.in8 = nd_l0;
+                hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 5, true, 0, 2>), dim3(pgrid), dim3(kPT), 0, c->stream,
+                                   t_start, t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
+                                   (uint32_t)T, n, ndg, lo16_l0, p88_shi);
+                return;
+            }
             hipLaunchKernelGGL((msd_pipe_kernel<kPT, kPI, R, 5, true>), dim3(pgrid), dim3(kPT), 0, c->stream, t_start,
                                t_count, dig_at(B, hi, R), tile_hist, kin, vin, c->keys[out], c->vals[out],
                                (uint32_t)T, n, ndg);
@@ -2878,6 +3007,30 @@ struct MsdDriver {
         else level_launch<6>(hi, nw, t_start, t_count, T, kin, vin, out, count);
     }
 
+    // the output format of a global level over nseg buckets holding elems elements (level_pass):
+    //   nd_next  the next level's digit bytes are written (its sub-buckets are most likely big);
+    //   compact  (low bits, start) + digit byte, 9 B out, when its sub-buckets will most likely all
+    //            be finished locally and the key bits below the next 8-bit digit fit a u32;
+    //   pairs    packed pairs (10 B + digit byte) when the next level is most likely compact (its
+    //            sub-buckets local, its remaining bits <= 40) and this level's remaining key bits
+    //            and the start fit 80 bits (GKM_TEST_PAIRS=1, tests: whenever the bits fit)
+    struct LevelFormat {
+        bool nd_next, compact, pairs;
+    };
+    LevelFormat level_format(int level, int hi, uint64_t elems, uint64_t nseg) const {
+        LevelFormat f{};
+        f.nd_next = nseg == 0 || (elems / nseg >> width(level)) >= (uint64_t)kBlockMax;
+        const int rem = B - hi - width(level);
+        f.compact = phase == 0 && !f.nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
+        const uint64_t next_mean = nseg ? (elems / nseg >> width(level)) >> width(level + 1) : 0;
+        const int rem2 = rem - width(level + 1);
+        const bool force = std::getenv("GKM_TEST_PAIRS") != nullptr;  // (read per level: tests flip it)
+        f.pairs = allow_c79 && !c79_in && phase == 0 && !f.compact && rem >= 33 && rem <= 48 && !no_compact() &&
+                  (force || (f.nd_next && next_mean < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 &&
+                             width(level + 2) == 8 && width(level + 1) == 8));
+        return f;
+    }
+
     int level_pass(int level, int hi, const uint32_t *t_start, const uint32_t *t_count, uint64_t T, uint64_t C,
                    const uint32_t *s_cfirst, const uint32_t *s_nchunks, const uint32_t *s_start, uint64_t nseg,
                    const uint64_t *kin, const uint32_t *vin, int out) {
@@ -2891,24 +3044,25 @@ struct MsdDriver {
         GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
         // the next level's digit bytes, unless this level's sub-buckets will most likely all be
         // local (mean under kBlockMax); a next level then counts from the keys
-        nd_next = nseg == 0 || (big_elems / nseg >> width(level)) >= (uint64_t)kBlockMax;
-        // compact output when this level's sub-buckets will most likely all be finished locally
-        // and the key bits below the next 8-bit digit fit a u32: (low bits, start) as one u64 and
-        // the digit byte -- 9 B per element out instead of 12 -- and the finishing kernels read 9 B
-        const int rem = B - hi - width(level);
-        compact_now = phase == 0 && !nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
+        const LevelFormat lf = level_format(level, hi, big_elems, nseg);
+        nd_next = lf.nd_next;
+        compact_now = lf.compact;
         compact_hi = hi + width(level);
-        // packed pairs out: the next level is most likely compact (its sub-buckets local, its
-        // remaining bits <= 40) and this level's remaining key bits and the start fit 80 bits
-        const uint64_t next_mean = nseg ? (big_elems / nseg >> width(level)) >> width(level + 1) : 0;
-        const int rem2 = rem - width(level + 1);
-        const bool force = std::getenv("GKM_TEST_PAIRS") != nullptr;  // tests: whenever the bits fit (read per level)
-        c79_out = allow_c79 && !c79_in && phase == 0 && !compact_now && rem >= 33 && rem <= 48 && !no_compact() &&
-                  (force || (nd_next && next_mean < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 &&
-                             width(level + 2) == 8 && width(level + 1) == 8));
+        c79_out = lf.pairs;
+        const int rem = B - hi - width(level);
         if (c79_out) {
             c79_shi = 64 - rem;
             GK_TRY_HIP(c, scratch(c, "msd_lo16", n + 64, &lo16));
+        }
+        // the packed L0's output in, but no packed pairs out: back to (key, start) first
+        if (p88_in && !c79_out) {
+            if (pieces_level)  // (first_level_from_pieces expands its pieces itself beforehand)
+                return fail(c, GK_E_HIP, "msd: packed L0 pieces reached a level that does not read them");
+            hipLaunchKernelGGL(expand_p88_kernel, dim3((unsigned)nseg, bucket_split(nseg)), dim3(256), 0, c->stream,
+                               big_start[cur_big], big_len[cur_big], big_pref[cur_big], hi, B, p88_shi,
+                               const_cast<uint64_t *>(kin), lo16_l0, nd_l0, const_cast<uint32_t *>(vin));
+            GK_TRY_HIP(c, hipGetLastError());
+            p88_in = false;
         }
         // packed pairs in, but not a compact level after all: back to (key, start) first
         if (c79_in && !compact_now) {
@@ -2928,6 +3082,7 @@ struct MsdDriver {
         // read keys: pairs hold them shifted)
         nd_ready = nd_next || compact_now || c79_out;
         c79_in = c79_out;  // the next level's input format
+        p88_in = false;
         return GK_OK;
     }
 
@@ -3002,7 +3157,26 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipMemcpyAsync(s_pref, spf.data(), 8 * nseg, hipMemcpyHostToDevice, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         big_elems = n;
+        if (p88_in && !level_format(level, hi, n, nseg).pairs) {  // (prefetched packed L0: back to (key, start))
+            uint64_t *pdev;
+            GK_TRY_HIP(c, scratch(c, "p88_pieces", 3 * np, &pdev));
+            std::vector<uint64_t> hp(3 * (uint64_t)np);
+            for (uint32_t j = 0; j < np; ++j) {
+                hp[j] = poff[j];
+                hp[np + j] = plen[j];
+                hp[2 * (uint64_t)np + j] = pbucket[j];
+            }
+            GK_TRY_HIP(c, hipMemcpyAsync(pdev, hp.data(), 8 * hp.size(), hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(expand_p88_pieces_kernel, dim3(np, bucket_split(np)), dim3(256), 0, c->stream, pdev,
+                               np, hi, B, p88_shi, const_cast<uint64_t *>(kin), lo16_l0, nd_l0,
+                               const_cast<uint32_t *>(vin));
+            GK_TRY_HIP(c, hipGetLastError());
+            GK_TRY_HIP(c, hipStreamSynchronize(c->stream));  // (hp is released at return)
+            p88_in = false;
+        }
+        pieces_level = true;
         rc = level_pass(level, hi, t_start, t_count, T, C, s_cfirst, s_nchunks, s_st, nseg, kin, vin, 0);
+        pieces_level = false;
         if (rc != GK_OK) return rc;
         cur_big = 0;
         uint64_t before[kLocal];
@@ -3387,12 +3561,13 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         c->pk_fresh = false;
     }
     uint64_t found = 0;
+    // the packed L0 output (P88) when the level behind it writes packed pairs
+    d.p88 = nphase == 1 && d.p88_wanted();
+    d.p88_shi = 64 - (d.B - d.width(0) - 8);
     // The L0's output buffer: the one that makes the last global level write buffer 1, so that the
     // finishing kernels read buffer 1 and write buffer 0 instead of rewriting buffer 0 in place
     // (levels predicted from the mean bucket size; C3: L0, L1, L2 -> L0 writes buffer 1).  A/B on
-    // one box (C3, 3 pairs): 67.3-68.3 against 67.7-68.8 ms; the same order of buffers in the
-    // prefetched path's sort (below) took the wave-local kernel from 19.8 to 15.3 ms on a slow box.
-    // GKM_L0_BUF=0/1 forces it.
+    // one box (C3, 3 pairs): 67.3-68.3 against 67.7-68.8 ms.  GKM_L0_BUF=0/1 forces it.
     int l0b = 0;
     {
         uint64_t mean = c->n >> d.width(0);
@@ -3405,6 +3580,8 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     if (rc != GK_OK) return rc;
     if (found != c->n) return fail(c, GK_E_HIP, "msd: k-mer count differs from the enumeration");
     rc = d.classify(1u << d.width(0), d.width(0), l0b, 0, nullptr, nullptr, 1, nullptr, d.width(0));
+    if (rc != GK_OK) return rc;
+    if (d.p88_in) rc = d.expand_p88_locals(l0b);  // (skewed genomes: L0 buckets finished locally)
     if (rc != GK_OK) return rc;
     rc = d.levels(1, d.width(0), l0b);
     if (rc != GK_OK) return rc;
@@ -3434,6 +3611,8 @@ struct L0Prefetch {
     uint32_t nreg = 0, tpr = 0;     // regions, L0 tiles of the largest region
     uint32_t nc_max = 0, next = 0;  // chunk-table entries per region; next region to launch
     int w0 = 7, w1 = 8;
+    bool p88 = false;               // the packed L0 output (MsdDriver::p88_wanted for n)
+    int p88_shi = 0;
     uint32_t *tab = nullptr;        // per region: c_first[nc_max], c_ntiles[nc_max], misc[4]
     uint32_t *pieces = nullptr;     // per region: 2^w0 bases, then 2^w0 counts
     std::vector<uint64_t> first;    // first L0 tile of each region (+ the end)
@@ -3473,6 +3652,10 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     p->n = len - k + 1;
     p->w0 = d.width(0);
     p->w1 = d.width(1);
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.n = p->n;
+    p->p88 = d.p88_wanted();
+    p->p88_shi = 64 - (d.B - p->w0 - 8);
     const uint64_t nt = (p->n + kP0Tile - 1) / kP0Tile;
     // regions: GKM_PREFETCH_REGIONS (default 16); the last region's pass is what the transfer
     // cannot hide
@@ -3503,8 +3686,10 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     }
     GK_TRY_HIP(c, msd_tables());
     uint8_t *ndp;
+    uint16_t *lop;
     uint32_t *dummy;
-    GK_TRY_HIP(c, scratch(c, "msd_nd", len + 64, &ndp));
+    GK_TRY_HIP(c, scratch(c, p->p88 ? "msd_nd_l0" : "msd_nd", len + 64, &ndp));
+    if (p->p88) GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", len + 64, &lop));
     GK_TRY_HIP(c, scratch(c, "pre_tables", (uint64_t)p->nreg * stride, &p->tab));
     GK_TRY_HIP(c, scratch(c, "pre_pieces", (uint64_t)p->nreg * 2 * R, &p->pieces));
     GK_TRY_HIP(c, scratch(c, "s_misc", 4, &dummy));
@@ -3545,7 +3730,12 @@ int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     hipStream_t keep = c->stream;
     c->stream = c->pre_stream;
     MsdDriver d(c, p->ks);
-    GK_TRY_HIP(c, scratch(c, "msd_nd", p->len + 64, &d.nd));
+    GK_TRY_HIP(c, scratch(c, p->p88 ? "msd_nd_l0" : "msd_nd", p->len + 64, &d.nd));
+    if (p->p88) {
+        GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", p->len + 64, &d.lo16_l0));
+        d.p88 = true;
+        d.p88_shi = p->p88_shi;
+    }
     const uint32_t R = 1u << p->w0, stride = 2 * p->nc_max + 4;
     int rc = GK_OK;
     int slot;
@@ -3576,6 +3766,7 @@ int prefetch_finish(gk_ctx *c, L0Prefetch *p, bool ok) {
     c->pre_regions = p->nreg;
     c->pre_w0 = p->w0;
     c->pre_w1 = p->w1;
+    c->pre_p88_shi = p->p88 ? p->p88_shi : 0;
     delete p;
     return rc;
 }
@@ -3608,7 +3799,15 @@ int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
             plen.push_back(cnt);
             pb.push_back(b);
         }
-    GK_TRY_HIP(c, scratch(c, "msd_nd", c->sba_len + 64, &d.nd));
+    if (c->pre_p88_shi) {  // the regions wrote the packed L0 form
+        GK_TRY_HIP(c, scratch(c, "msd_nd_l0", c->sba_len + 64, &d.nd));
+        GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", c->sba_len + 64, &d.lo16_l0));
+        d.nd_l0 = d.nd;
+        d.p88_in = true;
+        d.p88_shi = c->pre_p88_shi;
+    } else {
+        GK_TRY_HIP(c, scratch(c, "msd_nd", c->sba_len + 64, &d.nd));
+    }
     d.nd_ready = true;  // the regions' L0 wrote the level-1 digit bytes
     rc = d.first_level_from_pieces(c->keys[1], c->vals[1], poff.data(), plen.data(), pb.data(),
                                    (uint32_t)poff.size(), 1, d.width(0));

@@ -493,6 +493,8 @@ struct NextDigits {
     // the start's low 32 - pshi bits; vout[] is not written
     uint16_t *out16 = nullptr;
     int pshi = 0;
+    // INP == 2 (a level behind the packed L0, gkm_msd.hip): the input's top key byte, one per element
+    const uint8_t *in8 = nullptr;
 };
 
 // a packed-pair element (MODE 5's output) -> (key bits below the sorted ones, start)
@@ -525,10 +527,12 @@ __device__ __forceinline__ void pipe_store(int g, Dig d, const uint64_t *s_keys,
     }
 }
 
-// IN79: the input is packed pairs (a MODE 5 level's output: kin[] + in16[], key bits below the
-// sorted ones); only a compact (MODE 4) or packed-pair output, which never store the sorted bits,
-// may read it
-template <int T, int I, int R = 8, int MODE = 0, bool ND = false, int PRE_ = 0, bool IN79 = false>
+// INP (input format): 0 = (key, start); 1 = packed pairs (a MODE 5 level's output: kin[] + in16[],
+// key bits below the sorted ones); 2 = packed pairs below a digit byte (the packed L0's output,
+// gkm_msd.hip: nd.in8[] holds the top 8 of the unsorted key bits, kin[] the rest above the start's
+// high bits, in16[] the start's low bits).  Only a compact (MODE 4) or packed-pair output, which
+// never store the sorted bits, may read packed input.
+template <int T, int I, int R = 8, int MODE = 0, bool ND = false, int PRE_ = 0, int INP = 0>
 __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict__ t_start,
                                                      const uint32_t *__restrict__ t_count, Dig dl,
                                                      const uint32_t *__restrict__ tile_off,
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                      uint32_t ntiles, uint64_t sink, NextDigits nd = {},
                                                      const uint16_t *__restrict__ in16 = nullptr, int in_shi = 0) {
-    static_assert(!IN79 || MODE == 4 || MODE == 5, "packed-pair input keeps only the unsorted key bits");
+    static_assert(INP == 0 || MODE == 4 || MODE == 5, "packed-pair input keeps only the unsorted key bits");
     using SM = PipeSmem<T, I>;
     constexpr int NW = SM::kWaves;
     constexpr int TILE = SM::kTile;
@@ -563,9 +567,12 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint64_t e = b + min(q0 + i * 64, m - 1);
-            if (IN79) {
+            if (INP == 1) {
                 key[i] = kin[e];  // packed pair: unpacked at the item's first use (the rank loop)
                 val[i] = in16[e];
+            } else if (INP == 2) {  // + the digit byte above it, kept in val's high half until then
+                key[i] = kin[e];
+                val[i] = in16[e] | ((uint32_t)nd.in8[e] << 16);
             } else {
                 key[i] = kin[e];
                 val[i] = vin[e];
@@ -590,7 +597,12 @@ __global__ __launch_bounds__(T) void msd_pipe_kernel(const uint32_t *__restrict_
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             valid[i] = (uint32_t)(wave * (I * 64) + i * 64 + lane) < m;
-            if (IN79) unpack_pair(key[i], val[i], in_shi, key[i], val[i]);  // (at the item's first use)
+            if (INP == 1) unpack_pair(key[i], val[i], in_shi, key[i], val[i]);  // (at the item's first use)
+            if (INP == 2) {
+                const uint64_t top = (uint64_t)(val[i] >> 16) << (64 - in_shi);
+                unpack_pair(key[i], val[i] & 0xFFFFu, in_shi, key[i], val[i]);
+                key[i] |= top;
+            }
             dig[i] = dg_of(key[i], dl);
             rank[i] = rank_atomic(wc, dig[i], valid[i]);
             if (PRE + i < I) pipe_store<T, I, R, MODE, ND>(PRE + i, dl, s_keys, s_vals, ptoff, pcnt, sink, kout, vout, nd);

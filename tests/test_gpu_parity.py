@@ -786,6 +786,51 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
     np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
 
 
+# The packed L0 (P88, round 5): the L0 writes each element as its level-1 digit byte, a packed pair
+# (key bits below that digit above the start's high bits) and the start's low bits -- 11 B instead
+# of 13 -- and the level behind it reads that form (INP = 2) when it writes packed pairs itself;
+# otherwise the big buckets are expanded back to (key, start) first (expand_p88_kernel), and L0
+# buckets small enough to finish locally always are (expand_p88_list_kernel).  At test sizes
+# GKM_TEST_P88=1 makes the L0 pack wherever the bits fit; GKM_TEST_PAIRS=1 makes the next level
+# write pairs (so it reads the packed form); low-entropy input keeps buckets big for several levels,
+# random input sends most L0 buckets to the local classes.
+@pytest.mark.parametrize("pairs", [True, False], ids=["l1_pairs", "l1_plain"])
+@pytest.mark.parametrize("alphabet,k,level_bits", [(b"AC", 31, None), (b"AC", 24, None), (b"ACGT", 31, None),
+                                                   (b"AC", 31, "8,8,8"), (b"AC", 32, "8,8,8")])
+def test_packed_l0_vs_oracle(pairs, alphabet, k, level_bits, monkeypatch):
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    if pairs:
+        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    if level_bits:
+        monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    rng = np.random.default_rng(k + len(alphabet))
+    seqs = random_genome(rng, [1_600_000, 700_000], alphabet=alphabet)
+    seqs.append(("mixed", random_genome(rng, [250_000])[0][1]))
+    km, sc, want = oracle_check(seqs, k, k)
+    spec = oracle.key_spec(True, k, k)
+    np.testing.assert_array_equal(km.get_encoded_kmers(), oracle.encode_keys(sc.forward_sba, want, *spec))
+
+
+@pytest.mark.parametrize("pairs", [True, False], ids=["l1_pairs", "l1_plain"])
+def test_packed_l0_canonical_vs_oracle(pairs, monkeypatch):
+    # canonical 64-bit first words (k = 32): the 8-bit L0 leaves 56 bits, 48 of them in the pair
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    if pairs:
+        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    rng = np.random.default_rng(5)
+    s = np.frombuffer(b"ACG", dtype=np.uint8)[rng.integers(0, 3, 1_500_000)].copy()
+    seg = np.array([0], dtype=np.uint32)
+    e = _native.Engine()
+    e.set_sequence(s, seg)
+    n = e.enumerate(32)
+    e.sort(32, canonical=True)
+    want = oracle.canonical_sort(s, oracle.enumerate_starts(s, seg, 32), 32)
+    np.testing.assert_array_equal(e.copy_starts(np.empty(n, dtype=np.uint32)), want)
+    got = e.copy_keys()
+    keys = oracle.canonical_keys(s, want, 32, 2)
+    np.testing.assert_array_equal(got, keys.reshape(got.shape))
+
+
 # Whole-array sorts of encoded keys (bounded variable length, IUPAC 4-bit keys, the prefix-doubling
 # seeds and rank pairs) take the MSD levels over the keys from 2^20 keys on (msd_sort_keys);
 # GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes.

@@ -82,6 +82,26 @@ def test_prefetched_sort_matches_plain(k, L, regions, monkeypatch):
         np.testing.assert_array_equal(got[0], ref)
 
 
+@pytest.mark.parametrize("mode", ["p88", "p88_pairs"])
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"AC"])
+def test_prefetch_packed_l0(mode, alphabet, monkeypatch):
+    # the regions write the packed L0 form (GKM_TEST_P88=1); the first level from their pieces reads
+    # it when it writes packed pairs (GKM_TEST_PAIRS=1), else the pieces are expanded first
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    if mode == "p88_pairs":
+        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    rng = np.random.default_rng(len(alphabet) + len(mode))
+    L = 900_000
+    sba = np.frombuffer(alphabet, dtype=np.uint8)[rng.integers(0, len(alphabet), L)].copy()
+    seg = np.zeros(1, dtype=np.uint32)
+    _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=9)
+    assert "prefetch_l0" in rep and "msd_pass_l0" not in rep
+    _, want, _ = run(sba, seg, 31, monkeypatch, False, regions=9)
+    same(got, want)
+    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, np.arange(L - 30, dtype=np.uint32), 31, 31,
+                                                           break_ties=True))
+
+
 def test_prefetch_many_chunks_threads_and_regions(monkeypatch):
     # chunks finish out of order on 8 packing threads; 40 regions of one tile each, the last partial
     rng = np.random.default_rng(9)

@@ -612,6 +612,9 @@ def main():
     # packed-pair level before it wrote 10 B (+ digit byte) per element, which the compact level reads
     compact_in = any(n.startswith("msd_pass_l") and n.endswith("c") for n in report)
     pairs_in = any(n.startswith("msd_pass_l") and n.endswith("p") for n in report)
+    # the packed L0 (msd_pass_l0k): digit byte + packed pair + low start bits, 11 B per element out,
+    # which the level behind it reads (11 B in instead of 12)
+    l0_packed = "msd_pass_l0k" in report
 
     def stage_bytes(name, v):
         u = v.get("units", 0)
@@ -621,11 +624,15 @@ def main():
             return L * v["count"] + 13 * u  # the whole sequence in; kept (key, start, digit) out (units: kept)
         if name == "msd_pass_l0" and not range_mode:
             return seq_bytes * v["count"] + 13 * u  # sequence bytes in, (key, start, next digit) out
+        if name == "msd_pass_l0k" and not range_mode:
+            return seq_bytes * v["count"] + 11 * u  # sequence bytes in, (digit byte, pair, low start bits) out
         if name.startswith("msd_pass_l") and name.endswith("c"):
             # compact level: (key, start) -- or a packed pair, 10 B -- in, (low bits | start) + next digit out
             return (19 if pairs_in else 21) * u
         if name.startswith("msd_pass_l") and name.endswith("p"):
-            return 23 * u  # packed-pair level: (key, start) in, pair (10 B) + next digit out
+            # packed-pair level: (key, start) -- or, behind the packed L0, its 11 B -- in, pair (10 B)
+            # + next digit out
+            return (22 if l0_packed and name == "msd_pass_l1p" else 23) * u
         if name.startswith("msd_pass_l"):
             return 24 * u  # (key 8 B, start 4 B) in and out
         if name.startswith("msd_local"):
@@ -650,6 +657,8 @@ def main():
     kinds = {"msd_pass_l0": (("msd0_wide_kernel<512,36,11,true>", "the 11-bit L0 partition, straight from the "
                               "sequence") if wide else
                              ("msd0_pipe_kernel<2,1024,24,7,true>", "the L0 partition, straight from the sequence")),
+             "msd_pass_l0k": ("msd0_pipe_kernel<2,1024,24,7,true,false,false,true>",
+                              "the L0 partition, straight from the sequence, packed output"),
              "msd_local_wave8": (WAVE8_KERNEL, "wave-local finishing of buckets <= 512"),
              "msd_local_block32": ("msd_local_kernel<1024,8,10>", "block-local finishing of buckets <= 8192")}
     timed = {n: v for n, v in report.items() if stage_bytes(n, v) and v["total_ms"] > 0 and
@@ -664,7 +673,9 @@ def main():
                         "(packed-pair input)") if pairs_in else
                        ("msd_pipe_kernel<1024,11,8,4>", "the compact last level's stable 8-bit partition"))
     elif dom and dom.endswith("p"):
-        kdesc, what = "msd_pipe_kernel<1024,11,8,5>", "one stable 8-bit MSD partition pass writing packed pairs"
+        kdesc, what = (("msd_pipe_kernel<1024,11,8,5,true,0,2>", "one stable 8-bit MSD partition pass reading the "
+                        "packed L0 output and writing packed pairs") if l0_packed and dom == "msd_pass_l1p" else
+                       ("msd_pipe_kernel<1024,11,8,5>", "one stable 8-bit MSD partition pass writing packed pairs"))
     else:
         kdesc, what = "msd_pipe_kernel<1024,11,8,0>", "one stable 8-bit MSD partition pass"
     avg_ms = rp["total_ms"] / max(rp["count"], 1)

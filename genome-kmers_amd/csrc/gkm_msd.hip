@@ -2811,7 +2811,7 @@ struct MsdDriver {
         if (count + 1 > cap) return fail(c, GK_E_ARG, "partition output buffer too small");
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
-        timer_begin(c, "msd_pass_l0", &slot);
+        timer_begin(c, p88 ? "msd_pass_l0k" : "msd_pass_l0", &slot);  // (l0k: the packed L0 output)
         timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)

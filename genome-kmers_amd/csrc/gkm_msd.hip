@@ -2817,9 +2817,8 @@ struct MsdDriver {
         // exchange, so they do not)
         const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
-        if (with_nd && p88) {  // the packed L0: digit bytes and low start bits of its own
-            GK_TRY_HIP(c, scratch(c, "msd_nd_l0", n + 64, &nd_l0));
-            GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", n + 64, &lo16_l0));
+        if (with_nd && p88) {  // the packed L0: digit bytes and low start bits in the free start buffer
+            p88_place(vout == c->vals[0] ? 0 : 1);
             nd = nd_l0;
             ndg.out = nd;
             ndg.out16 = lo16_l0;
@@ -2856,8 +2855,34 @@ struct MsdDriver {
                width(3) == 8;
     }
 
+    // The packed L0 writes no starts, so its low start bits and digit bytes live in the start buffer
+    // of its own output (vals[buf]: 4 B per element; 2 + 1 used) -- no extra memory.  An expansion
+    // back to (key, start) writes that buffer, so it first copies them out (p88_detach, rare: skewed
+    // genomes and test shapes) and every later reader takes the copy.
+    void p88_place(int buf) {
+        lo16_l0 = reinterpret_cast<uint16_t *>(c->vals[buf]);
+        nd_l0 = reinterpret_cast<uint8_t *>(c->vals[buf]) + ((2 * (c->elem_cap + 64) + 255) & ~255ull);
+    }
+    int p88_detach() {
+        uint8_t *t;
+        const uint64_t m = c->elem_cap + 64;
+        if (!lo16_l0) return GK_OK;
+        GK_TRY_HIP(c, scratch(c, "p88_detached", 3 * m, &t));
+        if (reinterpret_cast<uint8_t *>(lo16_l0) == t) return GK_OK;  // (already)
+        GK_TRY_HIP(c, hipMemcpyAsync(t, lo16_l0, 2 * m, hipMemcpyDeviceToDevice, c->stream));
+        GK_TRY_HIP(c, hipMemcpyAsync(t + 2 * m, nd_l0, m, hipMemcpyDeviceToDevice, c->stream));
+        if (nd == nd_l0) nd = t + 2 * m;
+        lo16_l0 = reinterpret_cast<uint16_t *>(t);
+        nd_l0 = t + 2 * m;
+        return GK_OK;
+    }
+
     // after the packed L0's classify: its local entries back to (key, start) for the finishing kernels
     int expand_p88_locals(int buf) {
+        bool any = false;
+        for (int k = 0; k < kLocal; ++k) any |= nloc[k] > 0;
+        if (!any) return GK_OK;
+        if (int rc = p88_detach()) return rc;
         for (int k = 0; k < kLocal; ++k) {
             if (!nloc[k]) continue;
             hipLaunchKernelGGL(expand_p88_list_kernel, dim3((unsigned)nloc[k]), dim3(256), 0, c->stream, loc[k][0],
@@ -3058,6 +3083,7 @@ struct MsdDriver {
         if (p88_in && !c79_out) {
             if (pieces_level)  // (first_level_from_pieces expands its pieces itself beforehand)
                 return fail(c, GK_E_HIP, "msd: packed L0 pieces reached a level that does not read them");
+            if (int rc = p88_detach()) return rc;
             hipLaunchKernelGGL(expand_p88_kernel, dim3((unsigned)nseg, bucket_split(nseg)), dim3(256), 0, c->stream,
                                big_start[cur_big], big_len[cur_big], big_pref[cur_big], hi, B, p88_shi,
                                const_cast<uint64_t *>(kin), lo16_l0, nd_l0, const_cast<uint32_t *>(vin));
@@ -3158,6 +3184,7 @@ struct MsdDriver {
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         big_elems = n;
         if (p88_in && !level_format(level, hi, n, nseg).pairs) {  // (prefetched packed L0: back to (key, start))
+            if (int rd = p88_detach()) return rd;
             uint64_t *pdev;
             GK_TRY_HIP(c, scratch(c, "p88_pieces", 3 * np, &pdev));
             std::vector<uint64_t> hp(3 * (uint64_t)np);
@@ -3686,10 +3713,8 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     }
     GK_TRY_HIP(c, msd_tables());
     uint8_t *ndp;
-    uint16_t *lop;
     uint32_t *dummy;
-    GK_TRY_HIP(c, scratch(c, p->p88 ? "msd_nd_l0" : "msd_nd", len + 64, &ndp));
-    if (p->p88) GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", len + 64, &lop));
+    if (!p->p88) GK_TRY_HIP(c, scratch(c, "msd_nd", len + 64, &ndp));  // (packed: in vals[1], MsdDriver::p88_place)
     GK_TRY_HIP(c, scratch(c, "pre_tables", (uint64_t)p->nreg * stride, &p->tab));
     GK_TRY_HIP(c, scratch(c, "pre_pieces", (uint64_t)p->nreg * 2 * R, &p->pieces));
     GK_TRY_HIP(c, scratch(c, "s_misc", 4, &dummy));
@@ -3730,11 +3755,13 @@ int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     hipStream_t keep = c->stream;
     c->stream = c->pre_stream;
     MsdDriver d(c, p->ks);
-    GK_TRY_HIP(c, scratch(c, p->p88 ? "msd_nd_l0" : "msd_nd", p->len + 64, &d.nd));
-    if (p->p88) {
-        GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", p->len + 64, &d.lo16_l0));
+    if (p->p88) {  // the regions' low start bits and digit bytes in vals[1] (p88_place)
+        d.p88_place(1);
+        d.nd = d.nd_l0;
         d.p88 = true;
         d.p88_shi = p->p88_shi;
+    } else {
+        GK_TRY_HIP(c, scratch(c, "msd_nd", p->len + 64, &d.nd));
     }
     const uint32_t R = 1u << p->w0, stride = 2 * p->nc_max + 4;
     int rc = GK_OK;
@@ -3799,10 +3826,9 @@ int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
             plen.push_back(cnt);
             pb.push_back(b);
         }
-    if (c->pre_p88_shi) {  // the regions wrote the packed L0 form
-        GK_TRY_HIP(c, scratch(c, "msd_nd_l0", c->sba_len + 64, &d.nd));
-        GK_TRY_HIP(c, scratch(c, "msd_lo16_l0", c->sba_len + 64, &d.lo16_l0));
-        d.nd_l0 = d.nd;
+    if (c->pre_p88_shi) {  // the regions wrote the packed L0 form (its side arrays in vals[1])
+        d.p88_place(1);
+        d.nd = d.nd_l0;
         d.p88_in = true;
         d.p88_shi = c->pre_p88_shi;
     } else {

@@ -153,6 +153,10 @@ struct gk_ctx {
     // packed sba transfer (gkm_xfer.hip): pinned host + device staging slots, copy stream, events
     uint8_t *xfer_host = nullptr, *xfer_dev = nullptr;
     hipStream_t xfer_stream = nullptr, xfer_raw_stream = nullptr;
+    // the device unpacks of the packed chunks: a stream of the highest priority, so that they are
+    // dispatched ahead of a prefetched L0 pass running at the same time (gkm_msd.hip L0Prefetch)
+    hipStream_t unpack_stream = nullptr;
+    hipEvent_t unpack_done = nullptr;
     std::vector<hipEvent_t> xfer_ev;
     int xfer_slots = 0;
     uint64_t xfer_slot_bytes = 0;

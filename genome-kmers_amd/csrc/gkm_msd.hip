@@ -3749,8 +3749,9 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
 
 int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     if (!p || p->next >= p->nreg || landed < p->need(p->next)) return GK_OK;
-    // every unpack enqueued so far on c->stream; the regions now covered wait for them
-    GK_TRY_HIP(c, hipEventRecord(c->pre_ev[p->next], c->stream));
+    // every unpack enqueued so far (on the transfer's unpack stream); the regions now covered wait
+    // for them
+    GK_TRY_HIP(c, hipEventRecord(c->pre_ev[p->next], c->unpack_stream ? c->unpack_stream : c->stream));
     GK_TRY_HIP(c, hipStreamWaitEvent(c->pre_stream, c->pre_ev[p->next], 0));
     hipStream_t keep = c->stream;
     c->stream = c->pre_stream;

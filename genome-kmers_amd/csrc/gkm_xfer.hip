@@ -328,6 +328,13 @@ static hipError_t xfer_slots(gk_ctx *c, int slots, uint64_t slot_bytes) {
 }
 
 void xfer_release(gk_ctx *c) {
+    if (c->unpack_stream) {
+        hipStreamSynchronize(c->unpack_stream);
+        hipStreamDestroy(c->unpack_stream);
+        hipEventDestroy(c->unpack_done);
+        c->unpack_stream = nullptr;
+        c->unpack_done = nullptr;
+    }
     if (c->xfer_stream) hipStreamSynchronize(c->xfer_stream);
     if (c->xfer_raw_stream) hipStreamSynchronize(c->xfer_raw_stream);
     for (auto &ev : c->xfer_ev)
@@ -389,6 +396,13 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // which read the slots xfer_slots may free and reallocate) has to be done first
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     GK_TRY_HIP(c, xfer_slots(c, S, kHeaderBytes + chunk + 16));
+    if (!c->unpack_stream) {
+        int least = 0, greatest = 0;
+        GK_TRY_HIP(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        GK_TRY_HIP(c, hipStreamCreateWithPriority(&c->unpack_stream, hipStreamNonBlocking, greatest));
+        GK_TRY_HIP(c, hipEventCreateWithFlags(&c->unpack_done, hipEventDisableTiming));
+    }
+    hipStream_t us = c->unpack_stream;  // (everything before on c->stream is done: synchronised above)
     hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
     hipEvent_t *ev_raw = c->xfer_ev.data() + 2 * S;
     uint32_t *d_census = reinterpret_cast<uint32_t *>(c->scalars + 24);
@@ -478,13 +492,13 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             err = hipMemcpyAsync(ds, c->xfer_host + (uint64_t)s * c->xfer_slot_bytes, (size_t)used[s],
                                  hipMemcpyHostToDevice, c->xfer_stream);
             if (err == hipSuccess) err = hipEventRecord(ev_copy[s], c->xfer_stream);
-            if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, ev_copy[s], 0);
+            if (err == hipSuccess) err = hipStreamWaitEvent(us, ev_copy[s], 0);
             if (err == hipSuccess) {
                 hipLaunchKernelGGL(unpack_chunk_kernel, dim3((unsigned)((m + kXBlock - 1) / kXBlock)), dim3(256), 0,
-                                   c->stream, ds, c->sba + k * chunk, m);
+                                   us, ds, c->sba + k * chunk, m);
                 err = hipGetLastError();
             }
-            if (err == hipSuccess) err = hipEventRecord(ev_done[s], c->stream);
+            if (err == hipSuccess) err = hipEventRecord(ev_done[s], us);
             if (err != hipSuccess) break;
             inflight.push_back(s);
             ++issued;
@@ -562,6 +576,9 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     }
     cv.notify_all();
     for (auto &th : pool) th.join();
+    // the context's stream (the sort's kernels, the census copy) after every unpack
+    if (err == hipSuccess) err = hipEventRecord(c->unpack_done, us);
+    if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, c->unpack_done, 0);
     if (pf) {
         const int rc = prefetch_finish(c, pf, pf_ok && err == hipSuccess && prefix == C);
         if (err == hipSuccess && rc != GK_OK) return rc;

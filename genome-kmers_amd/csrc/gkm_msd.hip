@@ -2224,19 +2224,26 @@ __device__ __forceinline__ uint32_t codes4(uint32_t w) {  // 4 bytes -> 8 bits, 
 
 __device__ __forceinline__ uint64_t tie_word2(const uint8_t *sba, uint32_t p, int k, int sym0, int nsym,
                                               bool canonical) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(sba + (p & ~3u));
-    const int off = (int)(p & 3u);
-    uint64_t c0 = 0, c1 = 0;
-    uint32_t c2 = 0;
+    // five 16-byte loads from p & ~15 (80 bytes; 17 dword loads made every k-mer 17 scattered
+    // requests: C5's 113 M tie members took 19 ms)
+    const uint4 *w4 = reinterpret_cast<const uint4 *>(sba + (p & ~15u));
+    uint4 q[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) q[j] = w4[j];
+    const uint32_t w[20] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x, q[2].y,
+                            q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w, q[4].x, q[4].y, q[4].z, q[4].w};
+    uint64_t c0 = 0, c1 = 0, c2 = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) c0 = (c0 << 8) | codes4(w[j]);
 #pragma unroll
     for (int j = 8; j < 16; ++j) c1 = (c1 << 8) | codes4(w[j]);
-    c2 = codes4(w[16]);
-    // symbols 0 .. 63 from p: drop the first `off` symbols of the stream
-    const int sh = 2 * off;
+#pragma unroll
+    for (int j = 16; j < 20; ++j) c2 = (c2 << 8) | codes4(w[j]);
+    c2 <<= 32;  // symbols 64 .. 79 of the stream, on top
+    // symbols 0 .. 63 from p: drop the first `off` (< 16) symbols of the stream
+    const int sh = 2 * (int)(p & 15u);
     uint64_t fh = sh ? (c0 << sh) | (c1 >> (64 - sh)) : c0;
-    uint64_t fl = sh ? (c1 << sh) | ((uint64_t)c2 >> (8 - sh)) : c1;
+    uint64_t fl = sh ? (c1 << sh) | (c2 >> (64 - sh)) : c1;
     if (k < 64) {  // symbols past the k-mer read as 0
         if (k <= 32) {
             fh &= k == 32 ? ~0ull : ~(~0ull >> (2 * k));
@@ -2269,20 +2276,72 @@ __device__ __forceinline__ uint64_t tie_word2(const uint8_t *sba, uint32_t p, in
     return nb >= 64 ? x : x >> (64 - nb);
 }
 
-// Flat variant of tie_encode_kernel for many groups: every element in a group of >= 2 (a head
-// flag of 0 at it or at its successor) gets the next key word.
+// Flat variant of tie_encode_kernel for many groups: tie_members_kernel lists every element in a group
+// of >= 2 (a head flag of 0 at it or at its successor) -- 32 consecutive flags per thread from two
+// 16-byte loads and one byte; COUNT per 8,192-element tile, scan, STORE at the tile's offset (one
+// list append per wave on a global counter serialised 1.5 M atomics at C5: 16 ms) -- and
+// tie_encode_list_kernel gives each listed element its next key word, one element per thread.  (One
+// thread per element with a byte load per flag kept too few bytes in flight: 9.2 ms for C5's 3.1e9
+// flags; 32 flags per thread with the members encoded in place serialised the lanes of the long
+// runs of members a repeat leaves in the sorted order: 7.6 ms.)
+template <bool STORE>
+__global__ __launch_bounds__(256) void tie_members_kernel(const uint8_t *__restrict__ heads, uint64_t n,
+                                                          uint32_t *__restrict__ cnt, const uint32_t *__restrict__ off,
+                                                          uint32_t *__restrict__ list) {
+    __shared__ uint32_t s_m[4][64 * 32];  // per wave: its members, in element order
+    __shared__ uint32_t s_w[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kTieTile + threadIdx.x * 32;  // (as tie_bounds_kernel)
+    uint32_t mem = 0;
+    if (i0 + 33 <= n) {
+        const uint4 *h4 = reinterpret_cast<const uint4 *>(heads + i0);  // i0 % 32 == 0
+        const uint4 a = h4[0], b = h4[1];
+        const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t hb = 0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) hb |= (((wv[q >> 2] >> (8 * (q & 3))) & 0xFFu) != 0 ? 1u : 0u) << q;
+        const uint32_t nxt = (hb >> 1) | ((heads[i0 + 32] != 0 ? 1u : 0u) << 31);  // bit q: i0 + q + 1 is a head
+        mem = ~hb | ~nxt;
+    } else if (i0 < n) {
+        for (int q = 0; q < 32 && i0 + q < n; ++q) {
+            const uint64_t i = i0 + q;
+            mem |= (heads[i] == 0 || (i + 1 < n && heads[i + 1] == 0) ? 1u : 0u) << q;
+        }
+    }
+    const uint32_t c = (uint32_t)__popc(mem);
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    if (!STORE) {
+        if (threadIdx.x == 0) cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        return;
+    }
+    uint32_t base = off[blockIdx.x];
+    for (uint32_t w = 0; w < wave; ++w) base += s_w[w];
+    const uint32_t tot = s_w[wave];
+    if (tot == 0) return;  // (wave-uniform)
+    // the wave's members through LDS, stored by consecutive lanes (stored straight from the lanes,
+    // each lane's run of up to 32 made every store instruction 64 scattered partial lines)
+    uint32_t *sm = s_m[wave];
+    uint32_t at = incl - c;
+    for (; mem; mem &= mem - 1) sm[at++] = (uint32_t)(i0 + __ffs(mem) - 1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    for (uint32_t j = lane; j < tot; j += 64) list[base + j] = sm[j];
+}
+
 template <int BITS>
-__global__ __launch_bounds__(256) void tie_encode_flat_kernel(const uint8_t *__restrict__ sba,
-                                                              const uint8_t *__restrict__ heads, uint64_t n,
+__global__ __launch_bounds__(256) void tie_encode_list_kernel(const uint8_t *__restrict__ sba,
+                                                              const uint32_t *__restrict__ list, uint32_t m,
                                                               const uint32_t *__restrict__ vals,
                                                               uint64_t *__restrict__ keys, int sym0, int nsym, int k,
                                                               int canonical) {
     __shared__ uint8_t s_lut4[256];
     s_lut4[threadIdx.x] = c_code4_msd[threadIdx.x];
     __syncthreads();
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const bool tie = heads[i] == 0 || (i + 1 < n && heads[i + 1] == 0);
-        if (!tie) continue;
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
+        const uint32_t i = list[j];
         if (BITS == 2 && k <= 64) {
             keys[i] = tie_word2(sba, vals[i], k, sym0, nsym, canonical != 0);
             continue;
@@ -3254,13 +3313,25 @@ struct MsdDriver {
             for (uint32_t v : lens) tot += v;
             flat = tot > (1u << 20);
         }
-        if (flat) {  // many groups: one pass over the head flags, one thread per element
-            const unsigned fg = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 32);
+        if (flat) {  // many groups: the members listed from the head flags, then one thread per member
+            uint32_t *mlist;
+            // the list lives in the free key buffer (8 B per element; classify and the levels below
+            // reuse it only after the encode has read the list)
+            mlist = reinterpret_cast<uint32_t *>(c->keys[1]);
+            hipLaunchKernelGGL(tie_members_kernel<false>, dim3(ttiles), dim3(256), 0, c->stream, heads, n, cf, nullptr,
+                               nullptr);
+            GK_TRY_HIP(c, hipGetLastError());
+            uint64_t nm = 0;
+            GK_TRY_HIP(c, scan_u32_exclusive_pub(c, cf, ttiles, of, &nm));
+            hipLaunchKernelGGL(tie_members_kernel<true>, dim3(ttiles), dim3(256), 0, c->stream, heads, n, nullptr, of,
+                               mlist);
+            GK_TRY_HIP(c, hipGetLastError());
+            const unsigned eg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nm + 255) / 256, (uint64_t)cus * 16));
             if (ks.bits == 2)
-                hipLaunchKernelGGL(tie_encode_flat_kernel<2>, dim3(fg), dim3(256), 0, c->stream, c->sba, heads, n,
+                hipLaunchKernelGGL(tie_encode_list_kernel<2>, dim3(eg), dim3(256), 0, c->stream, c->sba, mlist, (uint32_t)nm,
                                    c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
             else
-                hipLaunchKernelGGL(tie_encode_flat_kernel<4>, dim3(fg), dim3(256), 0, c->stream, c->sba, heads, n,
+                hipLaunchKernelGGL(tie_encode_list_kernel<4>, dim3(eg), dim3(256), 0, c->stream, c->sba, mlist, (uint32_t)nm,
                                    c->vals[0], c->keys[0], sym0, nsym, ks.symbols, ks.canonical);
         } else if (ks.bits == 2)
             hipLaunchKernelGGL(tie_encode_kernel<2>, dim3(grid), dim3(256), 0, c->stream, c->sba, g_start, g_len,
@@ -3589,7 +3660,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     }
     uint64_t found = 0;
     // the packed L0 output (P88) when the level behind it writes packed pairs
-    d.p88 = nphase == 1 && d.p88_wanted();
+    d.p88 = d.p88_wanted();  // (multi-word keys: phase 0's first word; the tie phases read keys[0] / vals[0])
     d.p88_shi = 64 - (d.B - d.width(0) - 8);
     // The L0's output buffer: the one that makes the last global level write buffer 1, so that the
     // finishing kernels read buffer 1 and write buffer 0 instead of rewriting buffer 0 in place
@@ -3870,6 +3941,7 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = kGR;  // pieces are kGR-bit buckets
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
@@ -4012,6 +4084,9 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     d.B = ks.bits * std::min(ks.symbols, spw);
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
+    // packed-pair levels where the bits fit (the first level from the select's pieces has 55 bits
+    // left at C3: its L1 writes the pairs)
+    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
     d.wsched[0] = range_width(ks);
     timer_begin(c, "msd_total", &d.total_slot);
     GK_TRY_HIP(c, msd_tables());

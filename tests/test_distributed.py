@@ -384,6 +384,24 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
     assert uniq == ref.unique_count_only()
 
 
+# Round 5: the ranks' levels write packed pairs where the bits fit (msd_sort_range, msd_shard_sort);
+# at test sizes GKM_TEST_PAIRS=1 makes every level that can write them do so
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
+    (2, 1, 31, False, False), (3, 2, 31, True, False), (2, 2, 63, True, True), (8, 2, 31, True, True)])
+def test_gpu_key_ranges_packed_pairs(world, contigs, k, canonical, iupac, monkeypatch):
+    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [(2, 1, 31, False, False), (3, 2, 31, True, False),
+                                                             (2, 2, 63, True, True)])
+def test_gpu_shards_packed_pairs(world, contigs, k, canonical, iupac, monkeypatch):
+    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    test_gpu_shards_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,contigs,k,canonical", [
     (2, 2, 63, True), (2, 1, 40, False), (5, 3, 31, False), (8, 2, 31, True), (3, 1, 5, False), (4, 2, 6, False)])

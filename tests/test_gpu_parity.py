@@ -831,6 +831,53 @@ def test_packed_l0_canonical_vs_oracle(pairs, monkeypatch):
     np.testing.assert_array_equal(got, keys.reshape(got.shape))
 
 
+# The packed L0 under multi-word keys (round 5): phase 0 sorts the first word through it, the tie
+# phases then read keys[0] / vals[0] as usual.  Planted repeats tie first words (k = 45, 63), and an
+# N run makes the 4-bit split path sort its ACGT-only class on 2-bit keys through the packed L0.
+@pytest.mark.parametrize("pairs", [True, False], ids=["l1_pairs", "l1_plain"])
+@pytest.mark.parametrize("k", [45, 63])
+@pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
+def test_packed_l0_multiword_vs_oracle(pairs, k, canonical, monkeypatch):
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    if pairs:
+        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    rng = np.random.default_rng(k + 2 * canonical)
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 1_200_000)].copy()
+    rep = s[1000:1000 + 4000].copy()
+    for at in (100_000, 400_000, 800_000):
+        s[at:at + 4000] = rep
+    seg = np.array([0], dtype=np.uint32)
+    e = _native.Engine()
+    e.set_sequence(s, seg)
+    n = e.enumerate(k)
+    e.sort(k, canonical=canonical)
+    starts = oracle.enumerate_starts(s, seg, k)
+    want = oracle.canonical_sort(s, starts, k) if canonical else oracle.quicksort(s, starts, k, k, break_ties=True)
+    np.testing.assert_array_equal(e.copy_starts(np.empty(n, dtype=np.uint32)), want)
+    got = e.copy_keys()
+    keys = oracle.canonical_keys(s, want, k, 2) if canonical else oracle.encode_keys(s, want, *oracle.key_spec(True, k, k))
+    np.testing.assert_array_equal(got, keys.reshape(got.shape))
+
+
+@pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
+def test_packed_l0_split_vs_oracle(canonical, monkeypatch):
+    # an N run: 4-bit keys, the ACGT-only class sorted on 2-bit keys (63 symbols: two words)
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    rng = np.random.default_rng(11 + canonical)
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 900_000)].copy()
+    s[300_000:300_500] = ord("N")
+    s[600_000:600_003] = ord("R")
+    seg = np.array([0], dtype=np.uint32)
+    e = _native.Engine()
+    e.set_sequence(s, seg)
+    n = e.enumerate(63)
+    e.sort(63, canonical=canonical)
+    starts = oracle.enumerate_starts(s, seg, 63)
+    want = oracle.canonical_sort(s, starts, 63) if canonical else oracle.quicksort(s, starts, 63, 63, break_ties=True)
+    np.testing.assert_array_equal(e.copy_starts(np.empty(n, dtype=np.uint32)), want)
+
+
 # Whole-array sorts of encoded keys (bounded variable length, IUPAC 4-bit keys, the prefix-doubling
 # seeds and rank pairs) take the MSD levels over the keys from 2^20 keys on (msd_sort_keys);
 # GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes.

@@ -346,9 +346,11 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
             if constexpr (BITS == 2 && CANON && (R == 7 || R == 8)) {
                 uint32_t anystop = 0;
                 for (int j = t; j < P::kGroups; j += T) anystop |= s_dol[j];
+                // (ownership digits other than the L0 digit -- the key-range ranks' 12 bits -- take the
+                // per-position path below)
                 fast = __syncthreads_or(anystop != 0) == 0 && P0 + TILE <= a.hi &&
                        (d0.mask == 0x7Fu || d0.mask == 0xFFu) && (int)d0.shift == a.total_bits - R &&
-                       a.symbols >= 4;
+                       a.symbols >= 4 && (a.own_span == 0xFFFFFFFFu || a.own_bits == R);
                 if (fast) {
                     for (uint32_t g = t; g < TILE / 8; g += T) {
                         const uint32_t q0 = g * 8;
@@ -378,8 +380,10 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
 #pragma unroll UNR
                 for (int i = 0; i < I; ++i) {
                     const uint32_t p = i * T + t;
-                    const uint32_t d = dg_of(l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols), d0);
-                    if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned(d, a)) atomicAdd(&s_hist[d * NC], 1u);
+                    const uint64_t key = l0_key_of<BITS, CANON>(s_code, p, a.total_bits, a.symbols);
+                    const uint32_t d = dg_of(key, d0);
+                    if (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi && l0_owned_key(key, a))
+                        atomicAdd(&s_hist[d * NC], 1u);
                 }
             }
         }
@@ -418,7 +422,11 @@ constexpr int kP0Tile = kP0T * kP0I;     // 24,576 (< 65,536: positions staged a
 // P88 (the packed L0, round 5): each element leaves as the level-1 digit byte (nd), the key bits below
 // it above the start's high bits (u64: key << shi | start >> (32 - shi)) and the start's low bits
 // (u16 in nd.out16) -- 11 B instead of 13 (key, start, digit); the level behind reads it (INP = 2)
-template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false, bool P88 = false>
+// OWN (the key-range ranks' fused select, round 5): only k-mers whose ownership digit (the top
+// a.own_bits key bits) is in the rank's range are partitioned -- the select pass and its 13-byte
+// round trip per kept k-mer fall away
+template <int BITS, int T, int I, int R, bool ND, bool CANON = false, bool PROF = false, bool P88 = false,
+          bool OWN = false>
 __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const uint32_t *__restrict__ tile_off,
                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t ntiles, uint64_t sink, NextDigits nd) {
@@ -528,9 +536,11 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const uint32_t p = p0 + i * 64;
-            const bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
+            const uint64_t key = l0_key_of<BITS, CANON>(s_code[b], p, a.total_bits, a.symbols);
+            bool valid = clean || (l0_valid(s_dol, p, a.symbols) && P0 + p < a.hi);
+            if (OWN) valid = valid && l0_owned_key(key, a);
             validm |= (valid ? 1u : 0u) << i;
-            const uint32_t dig = dg_of(l0_key_of<BITS, CANON>(s_code[b], p, a.total_bits, a.symbols), d0);
+            const uint32_t dig = dg_of(key, d0);
             // stable rank by one returning LDS atomic (rank_atomic, gkm_partition.h); the LDS-mask
             // round trip it replaces took C3 L0 14.0 -> 12.9 ms against R + 1 ballots per item
             dr[i] = dig | (rank_atomic(wc, dig, valid) << 8);
@@ -2707,7 +2717,7 @@ struct MsdDriver {
 
     // L0 kernels: count (per-tile digit histograms) or partition; bits x digit width x next digits
     // x canonical
-    template <int BITS, int R, bool ND, bool CANON, bool P88 = false>
+    template <int BITS, int R, bool ND, bool CANON, bool P88 = false, bool OWN = false>
     void l0_launch(bool count, const L0Args &a, Dig d0, unsigned nt0, uint64_t *kout, uint32_t *vout, uint32_t nt,
                    uint64_t sink, const NextDigits &ndg) {
         // the count pass streams the sequence: 256-thread workgroups, eight per CU, each holding a
@@ -2732,8 +2742,8 @@ struct MsdDriver {
         else if (BITS == 2 && R == 7 && !CANON && !P88 && l0_prof())
             l0_prof_launch<ND>(a, d0, kout, vout, nt, sink, ndg);
         else
-            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kP0T, kP0I, R, ND, CANON, false, P88>), dim3(pgrid), dim3(kP0T), 0,
-                               c->stream, a, d0, tile_hist, kout, vout, nt, sink, ndg);
+            hipLaunchKernelGGL((msd0_pipe_kernel<BITS, kP0T, kP0I, R, ND, CANON, false, P88, OWN>), dim3(pgrid),
+                               dim3(kP0T), 0, c->stream, a, d0, tile_hist, kout, vout, nt, sink, ndg);
     }
 
     // timing only (GKM_L0_PROF=1): the L0 partition with per-phase clocks, printed to stderr
@@ -2785,6 +2795,16 @@ struct MsdDriver {
             return;
         }
         const bool pk = !count && nd_ && ndg.out16 != nullptr;  // the packed L0 (P88)
+        if (!count && ks.bits == 2 && nd_ && a.own_span != 0xFFFFFFFFu) {  // a key-range rank's fused select
+            if (w0 == 7) {
+                if (pk) l0_launch<2, 7, true, CANON, true, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+                else l0_launch<2, 7, true, CANON, false, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            } else {
+                if (pk) l0_launch<2, kGR, true, CANON, true, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+                else l0_launch<2, kGR, true, CANON, false, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            }
+            return;
+        }
         if (ks.bits == 2 && w0 == 7) {
             if (pk) l0_launch<2, 7, true, CANON, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
@@ -2820,7 +2840,7 @@ struct MsdDriver {
 
     // L0 count pass: per-tile digit histograms of the kept k-mers starting in [lo, hi), their
     // column scan (seg_base / seg_cnt), *count = k-mers kept
-    int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count) {
+    int l0_count(uint64_t lo, uint64_t hi, uint32_t own_lo, uint32_t own_span, uint64_t *count, int own_bits = 0) {
         const uint64_t span = hi > lo ? hi - lo : 0;
         const uint64_t tile = wsched[0] == kWideL0 ? (uint64_t)kWT * kWI : (uint64_t)kP0Tile;  // (the wide L0's own)
         const uint64_t nt0 = std::max<uint64_t>((span + tile - 1) / tile, 1);
@@ -2845,6 +2865,7 @@ struct MsdDriver {
         L0Args a{c->sba, lo, hi, ks.symbols, B, ks.acgt_only};
         a.own_lo = own_lo;
         a.own_span = own_span;
+        if (own_bits) a.own_bits = own_bits;
         a.pk_code = pk_code;
         a.pk_dol = pk_dol;
         l0a = a;
@@ -4022,6 +4043,12 @@ int msd_sort_groups(gk_ctx *c, const uint8_t *flags, int bkey) {
 int msd_radix_bits() { return kGR; }
 hipError_t rank_mode_msd(int ballot) { return set_rank_ballot_here(ballot); }
 
+// the key-range ranks fuse their select into the L0 when their digit share is >= 1 / this: the
+// emulated C3 rank (tools/range_emulate.py, profiles/r5/emu_fused_ab.txt) ran 42.3 against 45.0 ms
+// fused at N = 2, but 26.0 against 23.7 at N = 4 and 18.1 against 13.5 at N = 8 -- the L0 over the
+// whole sequence costs ~7.7 ms even when it stores an eighth of it
+constexpr uint64_t kFusedMaxRanks = 2;
+
 // L0 digit width of the key-range shards: 7 bits for 2-bit keys (as msd_sort), 8 otherwise
 static int range_width(const KeySpec &ks) { return ks.bits == 2 ? 7 : kGR; }
 
@@ -4111,6 +4138,54 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
             if (rp != GK_OK) return rp;
         }
         c->pk_fresh = false;
+    }
+    // Fused select (round 5): when the rank keeps a large share of the k-mers, its L0 count and
+    // partition run over the whole sequence and keep only the owned k-mers (msd0_pipe_kernel<...,
+    // OWN>), as msd_sort's L0 does for all of them -- no select pass, no 13-byte write and re-read
+    // per kept k-mer, and the packed L0 output.  With a small share the whole-sequence L0 (count,
+    // packing and ranking of every position) costs more than the select it replaces.  The share is
+    // estimated from the digit range; GKM_RANGE_FUSED=0/1 forces either path.
+    {
+        const int ob = range_own_bits(ks);
+        const uint32_t span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
+        bool fused = ks.bits == 2 && span > 0 && (uint64_t)span * kFusedMaxRanks >= (1ull << ob);
+        if (const char *e = std::getenv("GKM_RANGE_FUSED")) fused = ks.bits == 2 && span > 0 && e[0] == '1';
+        if (fused) {
+            c->n = 0;
+            c->cur = 0;
+            uint64_t found = 0;
+            int rc = d.l0_count(0, L, digit_lo, span, &found, ob);
+            if (rc != GK_OK) return rc;
+            if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
+            *n_kept = found;
+            if (found == 0) {
+                timer_end(c, d.total_slot);
+                return GK_OK;
+            }
+            rc = ensure_elems(c, found + 1, 1);
+            if (rc != GK_OK) return rc;
+            c->n = found;
+            rc = d.init(found);
+            if (rc != GK_OK) return rc;
+            d.p88 = d.p88_wanted();
+            d.p88_shi = 64 - (d.B - d.width(0) - 8);
+            int l0b = 0;  // (as msd_sort: the last global level writes buffer 1)
+            {
+                uint64_t mean = found >> d.width(0);
+                int lev = 0;
+                for (int l = 1; mean > (uint64_t)kBlockMax && l < kMaxLevels; ++l, ++lev) mean >>= d.width(l);
+                l0b = 1 ^ (lev & 1);
+            }
+            rc = d.l0_partition(c->keys[l0b], c->vals[l0b], c->elem_cap + 64, found);
+            if (rc == GK_OK) rc = d.classify(1u << d.width(0), d.width(0), l0b, 0, nullptr, nullptr, 1, nullptr, d.width(0));
+            if (rc == GK_OK && d.p88_in) rc = d.expand_p88_locals(l0b);
+            if (rc == GK_OK) rc = d.levels(1, d.width(0), l0b);
+            if (rc == GK_OK) rc = d.finish();
+            for (int ph = 1; ph < nphase && rc == GK_OK; ++ph)
+                rc = d.next_phase(ph * spw, std::min(spw, ks.symbols - ph * spw));
+            timer_end(c, d.total_slot);
+            return rc;
+        }
     }
     const Dig d0 = dig_at(d.B, 0, d.width(0));
     const bool two_pass = select_two_pass();

@@ -394,6 +394,27 @@ def test_gpu_key_ranges_packed_pairs(world, contigs, k, canonical, iupac, monkey
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
+# Round 5: a rank keeping a large share (<= 4 ranks by default) fuses its select into the L0
+# (msd0_pipe_kernel<..., OWN>); GKM_RANGE_FUSED=0/1 forces either path at any world size
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", ["0", "1"], ids=["select", "fused"])
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
+    (2, 1, 31, False, False), (8, 1, 31, False, False), (3, 2, 31, True, False), (2, 2, 63, True, True),
+    (5, 3, 31, False, True), (3, 1, 5, False, True), (4, 2, 21, False, False)])
+def test_gpu_key_ranges_fused_select(fused, world, contigs, k, canonical, iupac, monkeypatch):
+    monkeypatch.setenv("GKM_RANGE_FUSED", fused)
+    test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,k,canonical", [(2, 31, False), (2, 63, True)])
+def test_gpu_key_ranges_fused_packed_l0(world, k, canonical, monkeypatch):
+    monkeypatch.setenv("GKM_RANGE_FUSED", "1")
+    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    test_gpu_key_ranges_concatenate_to_single_sort(world, 1, k, canonical, False)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,contigs,k,canonical,iupac", [(2, 1, 31, False, False), (3, 2, 31, True, False),
                                                              (2, 2, 63, True, True)])

@@ -482,14 +482,6 @@ __global__ __launch_bounds__(256) void encode_generic_kernel(const uint8_t *__re
 // 4-bit keys expand the 2-bit codes nibble by nibble (A 1, C 3, G 5, T 12: 2 s + 1, + 5 for T).
 // Windows with another byte take the per-byte path below.
 
-// 2-bit codes (A0 C1 G2 T3) of 8 bytes as 16 bits, byte 0 in the most significant pair
-__device__ __forceinline__ uint32_t pack2_8e(uint64_t x) {
-    uint64_t t = __builtin_bswap64(((x >> 1) ^ (x >> 2)) & 0x0303030303030303ull);
-    t = (t | (t >> 6)) & 0x000F000F000F000Full;
-    t = (t | (t >> 12)) & 0x000000FF000000FFull;
-    return (uint32_t)((t | (t >> 24)) & 0xFFFFu);
-}
-
 // the k (<= 64) symbols from sba[s] as a right-aligned 2k-bit value (hi:lo); false if a window
 // byte is not A, C, G or T (reads up to 72 bytes from s & ~7: the sba carries a '$' pad)
 __device__ __forceinline__ bool window2_acgt(const uint8_t *sba, uint64_t s, int k, uint64_t &hi, uint64_t &lo) {
@@ -513,48 +505,6 @@ __device__ __forceinline__ bool window2_acgt(const uint8_t *sba, uint64_t s, int
         lo = (lo << (2 * nb)) | v;
     }
     return bad == 0;
-}
-
-// the 32 2-bit groups of x in reverse order
-__device__ __forceinline__ uint64_t rev_pairs(uint64_t x) {
-    x = __builtin_bswap64(x);
-    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
-    return ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
-}
-
-// canonical = min(k-mer, reverse complement) of a right-aligned 2k-bit value, in place
-__device__ __forceinline__ void canon2(int k, uint64_t &hi, uint64_t &lo) {
-    uint64_t rh = rev_pairs(~lo), rl = rev_pairs(~hi);  // complement, 64 groups reversed (left-aligned)
-    const int s = 128 - 2 * k;
-    if (s >= 64) {
-        rl = rh >> (s - 64);
-        rh = 0;
-    } else if (s > 0) {
-        rl = (rl >> s) | (rh << (64 - s));
-        rh >>= s;
-    }
-    if (rh < hi || (rh == hi && rl < lo)) {
-        hi = rh;
-        lo = rl;
-    }
-}
-
-// the W key words (BITS-bit symbols) of a k-symbol ACGT k-mer given as a right-aligned 2k-bit value
-template <int W, int BITS>
-__device__ __forceinline__ void key_from_2bit(uint64_t hi, uint64_t lo, int k, uint64_t (&w)[W]) {
-    if (BITS == 2) {
-        w[W - 1] = lo;
-        if (W > 1) w[0] = hi;
-    } else {
-        const uint64_t part[4] = {lo & 0xFFFFFFFFull, lo >> 32, hi & 0xFFFFFFFFull, hi >> 32};
-#pragma unroll
-        for (int q = 0; q < W; ++q) {  // q: word from the least significant end
-            uint64_t e = expand4_16((uint32_t)part[q]);
-            const int left = k - 16 * q;  // symbols in this word
-            if (left < 16) e &= left <= 0 ? 0ull : (~0ull >> (64 - 4 * left));
-            w[W - 1 - q] = e;
-        }
-    }
 }
 
 // the W key words of the fixed-length k-mer at st: SWAR for windows of A/C/G/T, per symbol otherwise

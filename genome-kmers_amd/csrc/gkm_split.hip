@@ -419,14 +419,75 @@ __device__ __forceinline__ void put_key4(const uint64_t *a_keys, uint64_t i, int
     for (int q = 0; q < W; ++q) out_keys[(uint64_t)q * n + o] = w[q];
 }
 
+// k > 32 (round 5, C5): the A k-mer at start s has no one-word MSD key to expand; its 2k-bit key is
+// read from the 2-bit packed sequence (split_pack_kernel: 32 positions per word, position 0 on top)
+// -- three consecutive words from two aligned 16-byte loads -- made canonical when asked and expanded to
+// its W 4-bit words at the merged position.  The merge moves every A start anyway, so this replaces
+// the separate key pass over the merged order (a 16-B row per position of the sequence, written in
+// full, then one random row per k-mer: 11.5 + 85 ms at C5) with the random read alone.
+// The three words come from two aligned 16-byte loads (words 2 j .. 2 j + 3, j = g / 2), issued by
+// the caller for several k-mers before any is used (loads in flight, as the row gather of round 3).
+#ifndef GKM_MERGE_PK16
+#define GKM_MERGE_PK16 0
+#endif
+__device__ __forceinline__ void packed_pair_load(const uint64_t *__restrict__ pk, uint32_t s, uint4 &a, uint4 &b) {
+    if (GKM_MERGE_PK16) {  // (A/B: two aligned 16-byte loads -- 97.5 against 86-87 ms of C5 merge)
+        const uint4 *p4 = reinterpret_cast<const uint4 *>(pk) + ((s >> 5) >> 1);
+        a = p4[0];
+        b = p4[1];
+        return;
+    }
+    // the three words g .. g + 2, placed where put_key4_packed looks for them
+    const uint64_t g = s >> 5;
+    const uint64_t x0 = pk[g], x1 = pk[g + 1], x2 = pk[g + 2];
+    const bool odd = (g & 1) != 0;
+    const uint64_t w0 = odd ? 0 : x0, w1 = odd ? x0 : x1, w2 = odd ? x1 : x2, w3 = odd ? x2 : 0;
+    a = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+    b = make_uint4((uint32_t)w2, (uint32_t)(w2 >> 32), (uint32_t)w3, (uint32_t)(w3 >> 32));
+}
+
 template <int W>
+__device__ __forceinline__ void put_key4_packed(const uint4 &qa, const uint4 &qb, uint32_t s, int k, bool canonical,
+                                                uint64_t *out_keys, uint64_t n, uint64_t o) {
+    const uint64_t w0 = ((uint64_t)qa.y << 32) | qa.x, w1 = ((uint64_t)qa.w << 32) | qa.z;
+    const uint64_t w2 = ((uint64_t)qb.y << 32) | qb.x, w3 = ((uint64_t)qb.w << 32) | qb.z;
+    const bool odd = ((s >> 5) & 1u) != 0;
+    const uint64_t c0 = odd ? w1 : w0, c1 = odd ? w2 : w1, c2 = odd ? w3 : w2;
+    const int sh = 2 * (int)(s & 31u);
+    uint64_t hi = sh ? (c0 << sh) | (c1 >> (64 - sh)) : c0;  // symbols s .. s + 63, left-aligned
+    uint64_t lo = sh ? (c1 << sh) | (c2 >> (64 - sh)) : c1;
+    const int r = 128 - 2 * k;  // right-align the k symbols (33 <= k <= 63: 2 <= r <= 62)
+    lo = (lo >> r) | (hi << (64 - r));
+    hi >>= r;
+    if (canonical) canon2(k, hi, lo);
+    uint64_t w[W];
+    key_from_2bit<W, 4>(hi, lo, k, w);
+#pragma unroll
+    for (int q = 0; q < W; ++q) out_keys[(uint64_t)q * n + o] = w[q];
+}
+
+// 2-bit codes of the sequence, 32 positions per word (bytes other than A/C/G/T get some code: only
+// ACGT-only windows are read back)
+__global__ __launch_bounds__(256) void split_pack_kernel(const uint8_t *__restrict__ sba, uint64_t nwords,
+                                                         uint64_t *__restrict__ code) {
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < nwords; g += (uint64_t)gridDim.x * 256) {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(sba + 32 * g);
+        const uint64_t a = p[0], b = p[1], c = p[2], d = p[3];
+        code[g] = ((uint64_t)pack2_8e(a) << 48) | ((uint64_t)pack2_8e(b) << 32) | ((uint64_t)pack2_8e(c) << 16) |
+                  pack2_8e(d);
+    }
+}
+
+// PK: the A keys come from the packed sequence (put_key4_packed), not from a_keys
+template <int W, bool PK = false>
 __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict__ a_starts,
                                                       const uint8_t *__restrict__ a_heads, uint64_t nA,
                                                       const uint32_t *__restrict__ pos,
                                                       const uint32_t *__restrict__ g_first, uint64_t G, uint64_t nB,
                                                       uint32_t *__restrict__ out, uint8_t *__restrict__ out_heads,
                                                       const uint64_t *__restrict__ a_keys, int k,
-                                                      uint64_t *__restrict__ out_keys) {
+                                                      uint64_t *__restrict__ out_keys,
+                                                      const uint64_t *__restrict__ pk = nullptr, int canonical = 0) {
     __shared__ uint64_t s_g[3];  // ub(i0), lb(i0), groups with pos < i1
     const uint64_t i0 = (uint64_t)blockIdx.x * kMTile;
     const uint64_t i1 = min(i0 + kMTile, nA);
@@ -439,6 +500,29 @@ __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict
     const uint64_t g0 = s_g[0], lb0 = s_g[1], g1 = s_g[2];
     if (g1 == g0) {  // no B group lands inside (i0, i1): one shift for the whole range
         const uint64_t shift = g0 < G ? g_first[g0] : nB;
+        if (PK) {  // kU k-mers per thread at a time: their starts, then all their sequence reads
+#ifndef GKM_MERGE_U
+#define GKM_MERGE_U 2  // (A/B at C5, profiles/r5/ab_merge_keys.txt: 1 / 2 / 4 -> 85.9-86.4 / 85.5 / 86.9-87.4 ms)
+#endif
+            constexpr int kU = GKM_MERGE_U;
+            for (uint64_t i = i0 + threadIdx.x; i < i1; i += kMT * kU) {
+                uint32_t st[kU];
+                uint4 qa[kU], qb[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) st[u] = i + u * kMT < i1 ? a_starts[i + u * kMT] : a_starts[i];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) packed_pair_load(pk, st[u], qa[u], qb[u]);
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const uint64_t j = i + u * kMT;
+                    if (j >= i1) continue;
+                    out[j + shift] = st[u];
+                    out_heads[j + shift] = (a_heads[j] || (j == i0 && g0 > lb0)) ? 1 : 0;
+                    put_key4_packed<(W ? W : 1)>(qa[u], qb[u], st[u], k, canonical != 0, out_keys, nA + nB, j + shift);
+                }
+            }
+            return;
+        }
         for (uint64_t i = i0 + threadIdx.x; i < i1; i += kMT) {
             out[i + shift] = a_starts[i];
             out_heads[i + shift] = (a_heads[i] || (i == i0 && g0 > lb0)) ? 1 : 0;
@@ -450,9 +534,16 @@ __global__ __launch_bounds__(kMT) void merge_a_kernel(const uint32_t *__restrict
         const uint64_t ub = bound_in(pos, g0, g1, i, true);
         const uint64_t lb = i == i0 ? lb0 : bound_in(pos, g0, ub, i, false);
         const uint64_t shift = ub < G ? g_first[ub] : nB;
-        out[i + shift] = a_starts[i];
+        const uint32_t st = a_starts[i];
+        out[i + shift] = st;
         out_heads[i + shift] = (a_heads[i] || ub > lb) ? 1 : 0;
-        if (W) put_key4<(W ? W : 1)>(a_keys, i, k, out_keys, nA + nB, i + shift);
+        if (PK) {
+            uint4 qa, qb;
+            packed_pair_load(pk, st, qa, qb);
+            put_key4_packed<(W ? W : 1)>(qa, qb, st, k, canonical != 0, out_keys, nA + nB, i + shift);
+        } else if (W) {
+            put_key4<(W ? W : 1)>(a_keys, i, k, out_keys, nA + nB, i + shift);
+        }
     }
 }
 
@@ -602,9 +693,12 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     if (rg && k < rg->pns) return fail(c, GK_E_ARG, "split: key-range shards need k >= the prefix length");
     GK_TRY_HIP(c, split_tables());
     c->split_keys_final = false;
-    // final keys: with one-word 2-bit class-A keys (k <= 32) the sorted order leaves with its W-word
-    // 4-bit keys -- A's expanded in the merge, B's from their own sort -- and needs no re-encode
-    const int WK = k <= 32 ? ks.words : 0;
+    // final keys: the sorted order leaves with its W-word 4-bit keys -- B's from their own sort, A's
+    // written by the merge: expanded from the one-word 2-bit MSD keys (k <= 32), or read from a
+    // 2-bit packed copy of the sequence (k <= 63, round 5; GKM_NO_MERGE_KEYS=1: the re-encode after
+    // the sort instead) -- and needs no re-encode
+    const bool a_packed = k > 32 && k <= 63 && !std::getenv("GKM_NO_MERGE_KEYS");
+    const int WK = k <= 32 || a_packed ? ks.words : 0;
     int slot;
     // 1. class B starts: homopolymers (one letter k times) apart from the rest
     uint32_t *b_st[2], *h_st;
@@ -842,15 +936,15 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     ka.words = (ka.total_bits + 63) / 64;
     ka.acgt_only = 1;
     int rc;
-    const uint64_t *a_keys = nullptr;  // A's final 2-bit keys (WK)
-    c->msd_force_keys = WK > 0;
+    const uint64_t *a_keys = nullptr;  // A's final 2-bit keys (WK, k <= 32)
+    c->msd_force_keys = WK > 0 && !a_packed;
     if (rg) {  // the rank's ACGT-only k-mers: select + MSD (gkm_msd.hip); room for the merge after
         rc = msd_sort_range(c, ka, rg->d_lo, rg->d_hi, &nA);
         c->msd_force_keys = false;
         if (rc != GK_OK) return rc;
         c->have_starts = true;
-        a_keys = c->keys[0];
-        if (WK && nA + nB + 1 > c->elem_cap) {  // growing the buffers below does not keep the keys
+        a_keys = a_packed ? nullptr : c->keys[0];
+        if (WK && !a_packed && nA + nB + 1 > c->elem_cap) {  // growing the buffers below does not keep the keys
             uint64_t *ak;
             GK_TRY_HIP(c, scratch(c, "split_a_keys", nA + 64, &ak));
             GK_TRY_HIP(c, hipMemcpyAsync(ak, c->keys[0], 8 * nA, hipMemcpyDeviceToDevice, c->stream));
@@ -867,7 +961,8 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         // both key buffers at the final key width before the A sort (which uses word 0 of each):
         // nothing is freed or re-allocated between the A sort and the merge
         if (WK) {
-            if (int r = grow_key_buffer(c, 0, WK)) return r;
+            if (!a_packed)
+                if (int r = grow_key_buffer(c, 0, WK)) return r;
             if (int r = grow_key_buffer(c, 1, WK)) return r;
         }
         c->n = nA;
@@ -875,14 +970,14 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         c->msd_force_keys = false;
         c->n = n;
         if (rc != GK_OK) return rc;
-        a_keys = c->keys[0];
+        a_keys = a_packed ? nullptr : c->keys[0];
     }
     if (nA == 0) {  // all B: the B order is the order
         GK_TRY_HIP(c, hipMemcpyAsync(c->vals[0], b_st[bres], 4 * nB, hipMemcpyDeviceToDevice, c->stream));
         uint8_t *hd;
         GK_TRY_HIP(c, scratch(c, "split_heads", n + 64, &hd));
         GK_TRY_HIP(c, hipMemcpyAsync(hd, b_heads, nB, hipMemcpyDeviceToDevice, c->stream));
-        if (WK) {
+        if (WK) {  // (the B keys alone: A's packed-sequence path is not involved)
             if (b_keys == c->keys[0]) return fail(c, GK_E_STATE, "split sort: B keys alias the key buffer");
             if (int r = grow_key_buffer(c, 0, WK)) return r;
             GK_TRY_HIP(c, hipMemcpyAsync(c->keys[0], b_keys, 8 * (uint64_t)WK * nB, hipMemcpyDeviceToDevice,
@@ -895,7 +990,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         return GK_OK;
     }
     if (nB == 0) {  // msd_sort left vals[0] / heads in place; A's keys expanded next to them
-        if (WK) {
+        if (WK && !a_packed) {  // (k > 32: the keys are re-encoded after the sort)
             if (a_keys == c->keys[1]) return fail(c, GK_E_STATE, "split sort: A keys alias the output buffer");
             if (int r = grow_key_buffer(c, 1, WK)) return r;
             const uint64_t nn = nA;
@@ -933,6 +1028,33 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     }
     const dim3 ga((unsigned)((nA + kMTile - 1) / kMTile)), gb((unsigned)((nB + kMTile - 1) / kMTile));
     uint64_t *ok = c->keys[1];
+    if (a_packed) {
+        // the 2-bit packed sequence: three words past every start (the sba's '$' pad covers them)
+        const uint64_t nwords = (L + kSbaPad) / 32;
+        uint64_t *pk;
+        GK_TRY_HIP(c, scratch(c, "split_pk", nwords, &pk));
+        hipLaunchKernelGGL(split_pack_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)),
+                           dim3(256), 0, c->stream, c->sba, nwords, pk);
+        GK_TRY_HIP(c, hipGetLastError());
+#define GK_MERGE_PK(W_)                                                                                         \
+    do {                                                                                                        \
+        hipLaunchKernelGGL((merge_a_kernel<W_, true>), ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA,     \
+                           pos, g_first, G, nB, c->vals[1], hd, nullptr, k, ok, pk, ks.canonical);               \
+        hipLaunchKernelGGL(merge_b_kernel<W_>, gb, dim3(kMT), 0, c->stream, b_st[bres], b_heads, nB, pos,         \
+                           g_first, G, c->vals[1], hd, b_keys, nA + nB, ok);                                     \
+    } while (0)
+        if (WK == 3) GK_MERGE_PK(3);
+        else if (WK == 4) GK_MERGE_PK(4);
+        else return fail(c, GK_E_STATE, "split sort: packed-sequence keys need 3 or 4 key words");
+#undef GK_MERGE_PK
+        GK_TRY_HIP(c, hipGetLastError());
+        c->split_keys_final = true;
+        timer_end(c, slot);
+        c->cur = 1;
+        c->heads = hd;
+        c->heads_valid = true;
+        return GK_OK;
+    }
     switch (WK) {
     case 0:
         hipLaunchKernelGGL(merge_a_kernel<0>, ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA, pos, g_first, G,

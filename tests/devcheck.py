@@ -231,10 +231,25 @@ class SortedOutputCheck:
         return groups, hist.cpu().numpy()
 
 
-def oracle_windows(km, sba: np.ndarray, k: int, offsets, width: int = 4096, canonical: bool = False):
+def window_keys(eng, off: int, m: int) -> np.ndarray:
+    """(m, words) product keys at sorted offsets [off, off + m), read from the device key array
+    (word-major, stride n) word by word with hipMemcpy D2H -- no full-size host copy."""
+    _, keys_ptr, n, words = eng.device_views()
+    out = np.empty((m, words), dtype=np.uint64)
+    tmp = np.empty(m, dtype=np.uint64)
+    for q in range(words):
+        rc = hip().hipMemcpy(tmp.ctypes.data, keys_ptr + 8 * (q * n + off), 8 * m, 2)
+        assert rc == 0, f"hipMemcpy failed ({rc})"
+        out[:, q] = tmp
+    return out
+
+
+def oracle_windows(km, sba: np.ndarray, k: int, offsets, width: int = 4096, canonical: bool = False,
+                   keys: bool = False):
     """Host windows of the sorted starts at the given sorted offsets, checked with the CPU oracle's
     restatement of the reference comparator (kmers.py:306-397) pair by pair: each window must be
-    non-decreasing, with equal k-mers in ascending start order."""
+    non-decreasing, with equal k-mers in ascending start order.  keys: the product's keys of the
+    window must equal the oracle's keys of its starts (4-bit, or 2-bit on an ACGT-only sba)."""
     from oracle import oracle
 
     eng = km._engine
@@ -242,6 +257,12 @@ def oracle_windows(km, sba: np.ndarray, k: int, offsets, width: int = 4096, cano
     for off in offsets:
         off = int(min(max(off, 0), max(n - width, 0)))
         w = eng.start_range(off, min(width, n - off))
+        if keys:
+            bits = 2 if eng.is_acgt() else 4
+            got = window_keys(eng, off, len(w))
+            want = (oracle.canonical_keys(sba, w, k, bits) if canonical
+                    else oracle.encode_keys(sba, w, *oracle.key_spec(bits == 2, k, k)))
+            np.testing.assert_array_equal(got, want.reshape(got.shape), err_msg=f"keys at sorted index {off}")
         if canonical:
             canon, _ = oracle.canonical_windows(sba, w, k)
             for i in range(len(w) - 1):

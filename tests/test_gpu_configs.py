@@ -124,12 +124,37 @@ def test_c3_full_size_properties():
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("k,canonical", [(31, False), (63, True)], ids=["c4_k31", "c5_k63_canonical"])
-def test_grch38_surrogate_full_size_properties(k, canonical):
+def test_grch38_surrogate_full_size_properties(k, canonical, monkeypatch):
+    # canonical k = 63 checks the order without the product keys: since round 5 the split sort's
+    # merge writes them (4 words, 99 GB), which does not fit beside the property check's own
+    # per-position keys -- test_c5_full_size_merge_keys_windows checks them at this size
+    if canonical:
+        monkeypatch.setenv("GKM_NO_MERGE_KEYS", "1")
     _log("GRCh38 surrogate: generating")
     sba, seg = synthetic.grch38_surrogate(2)
     assert len(seg) == 24
     expect = sum(max(0, n - k + 1) for n in synthetic.GRCH38_LENGTHS)
     _full_size_check(sba, seg, k, canonical, not canonical, expect)
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_merge_keys_windows():
+    """C5 at full size: the canonical 63-mer keys the split sort's merge writes from the packed
+    sequence (gkm_split.hip put_key4_packed), read back in windows of the sorted order across the
+    whole array (both ends, past 2^31, random offsets) and compared with the oracle's keys of the
+    window's starts; the order inside every window is checked too."""
+    import devcheck
+
+    _log("GRCh38 surrogate: generating")
+    sba, seg = synthetic.grch38_surrogate(2)
+    sc = _collection(sba, seg)
+    km = gk.Kmers(sc, min_kmer_len=63, max_kmer_len=63)
+    km.sort(canonical=True)
+    n = km._engine.n
+    offs = [0, 2**31 - 2048, 2**31 + 1, n // 3, (2**31 + n) // 2, n - 4096]
+    offs += list(np.random.default_rng(63).integers(0, n, 4))
+    devcheck.oracle_windows(km, sba, 63, offs, width=4096, canonical=True, keys=True)
+    _log("C5 merge-key windows done")
 
 
 # ---------------------------------------------------------------------------------------------

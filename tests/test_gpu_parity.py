@@ -878,6 +878,42 @@ def test_packed_l0_split_vs_oracle(canonical, monkeypatch):
     np.testing.assert_array_equal(e.copy_starts(np.empty(n, dtype=np.uint32)), want)
 
 
+# Round 5: on a mixed sba the split sort's merge writes the 4-bit keys of the ACGT-only k-mers of
+# k = 33..63 from a 2-bit packed copy of the sequence (gkm_split.hip put_key4_packed) instead of a
+# re-encode after the sort; W = 3 (k <= 48) and 4 words, forward and canonical, N runs (homopolymer
+# groups) and scattered IUPAC letters (the class-B rest), several contigs
+@pytest.mark.parametrize("k", [33, 40, 48, 49, 63])
+@pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
+def test_split_merge_packed_keys_vs_oracle(k, canonical, monkeypatch):
+    rng = np.random.default_rng(100 + k + canonical)
+    s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 700_000)].copy()
+    s[100_000:100_400] = ord("N")
+    s[300_000:300_090] = ord("N")
+    s[450_000:450_200:13] = ord("R")
+    s[520_000:520_004] = ord("Y")
+    s[600_000:604_000] = s[10_000:14_000]  # repeats: ties in the first word
+    s[250_000] = ord("$")
+    s[500_000] = ord("$")
+    seg = np.array([0, 250_001, 500_001], dtype=np.uint32)
+    e = _native.Engine()
+    e.set_sequence(s, seg)
+    n = e.enumerate(k)
+    e.sort(k, canonical=canonical)
+    starts = oracle.enumerate_starts(s, seg, k)
+    want = oracle.canonical_sort(s, starts, k) if canonical else oracle.quicksort(s, starts, k, k, break_ties=True)
+    np.testing.assert_array_equal(e.copy_starts(np.empty(n, dtype=np.uint32)), want)
+    got = e.copy_keys()
+    keys = oracle.canonical_keys(s, want, k, 4) if canonical else oracle.encode_keys(s, want, *oracle.key_spec(False, k, k))
+    np.testing.assert_array_equal(got, keys.reshape(got.shape))
+    # the same keys through the re-encode after the sort
+    monkeypatch.setenv("GKM_NO_MERGE_KEYS", "1")
+    e2 = _native.Engine()
+    e2.set_sequence(s, seg)
+    e2.enumerate(k)
+    e2.sort(k, canonical=canonical)
+    np.testing.assert_array_equal(e2.copy_keys(), got)
+
+
 # Whole-array sorts of encoded keys (bounded variable length, IUPAC 4-bit keys, the prefix-doubling
 # seeds and rank pairs) take the MSD levels over the keys from 2^20 keys on (msd_sort_keys);
 # GKM_MSD_KEYS_MIN lowers that bound so these sizes run it, GKM_SORT_KEYS_LSD=1 the LSD passes.

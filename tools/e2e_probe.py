@@ -1,6 +1,7 @@
 """Where the end-to-end interval of a C3 sort goes (sort hint on / off): wall time of gk_set_sequence,
 of the device catching up after it (a sync), and of the step, with the profile's stage times.
-Tuning only.  Usage: python tools/e2e_probe.py [--regions 16,32] [--reps 3] [--genome-len N]"""
+Tuning only.  Usage: python tools/e2e_probe.py [--regions 16,32] [--reps 3] [--genome-len N] [--pageable]
+(--pageable: the source is the caller's pageable numpy array instead of pinned memory)"""
 
 import argparse
 import json
@@ -19,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--genome-len", type=int, default=3_100_000_000)
     ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--pageable", action="store_true")
     a = ap.parse_args()
     import torch
     from genome_kmers import _native, synthetic
@@ -26,7 +28,7 @@ def main():
     sba, seg = synthetic.c3_genome(a.genome_len, 42)
     pinned = torch.empty(len(sba), dtype=torch.uint8).pin_memory()
     pinned.numpy()[:] = sba
-    src = pinned.numpy()
+    src = sba if a.pageable else pinned.numpy()
     eng = _native.Engine(0)
     k = a.k
 
@@ -56,7 +58,7 @@ def main():
             r = eng.profile_report()
             eng.profile_enable(False)
             st = {n: round(v["total_ms"], 2) for n, v in sorted(r.items()) if v["total_ms"] > 0.3}
-            print(json.dumps({"regions": regions, "set_sequence_ms": round((t1 - t0) * 1e3, 2),
+            print(json.dumps({"source": "pageable" if a.pageable else "pinned", "regions": regions, "set_sequence_ms": round((t1 - t0) * 1e3, 2),
                               "catch_up_ms": round((t2 - t1) * 1e3, 2), "step_ms": round((t3 - t2) * 1e3, 2),
                               "e2e_with_sync_ms": round((t3 - t0) * 1e3, 2), "stages": st}), flush=True)
     eng.sort_hint(0)

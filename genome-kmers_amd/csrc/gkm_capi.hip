@@ -443,7 +443,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     for (hipEvent_t e : c->pre_ev) hipEventDestroy(e);
     if (c->pre_done) hipEventDestroy(c->pre_done);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);
-    void *bufs[] = {c->sba, c->seg, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
+    void *bufs[] = {c->sba, c->seg, c->res_code, c->res_dol, c->vals[0], c->vals[1], c->keys[0], c->keys[1], c->status, c->counters,
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
                     c->dhist, c->mask, c->hmask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
@@ -527,6 +527,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
     c->have_starts = c->sorted = c->keys_valid = c->enumerated = c->unique_valid = c->heads_valid = c->canonical = false;
     c->enum_sorted = false;
     c->pk_fresh = false;
+    if (len < packed_transfer_min()) c->res_pk = false;  // (the packed transfer sets it)
     c->n = 0;
     if (h[0] & 4u) return fail(c, GK_E_ALPHABET, "Sequence contains non-allowed characters!");
     c->acgt = (h[0] & 2u) ? 0 : 1;

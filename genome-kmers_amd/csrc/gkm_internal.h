@@ -74,6 +74,13 @@ struct gk_ctx {
     uint64_t nseg = 0, seg_cap = 0;
     uint64_t max_seg_len = 0;
     int acgt = 1;
+    // the 2-bit packed copy of the sequence (pack2_kernel layout) that the packed transfer writes
+    // beside the resident sba; res_pk: it is complete and current (the last gk_set_sequence went
+    // through the packed transfer, every chunk unpacked on the device)
+    uint64_t *res_code = nullptr;
+    uint32_t *res_dol = nullptr;
+    uint64_t res_code_cap = 0, res_dol_cap = 0;
+    bool res_pk = false;
     bool pk_fresh = false;  // the packed sequence (scratch "pk_code" / "pk_dol") is current for
                             // the next gk_shard_sort_range (set by gk_shard_histogram)
 
@@ -187,6 +194,8 @@ struct gk_ctx {
 namespace gkm {
 
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
+// pack2_kernel (gkm_msd.hip) over nwords words of 32 bytes from `from`
+hipError_t launch_pack2(const uint8_t *from, uint64_t nwords, uint64_t *code, uint32_t *dol, hipStream_t s);
 // grow-only named device scratch buffer of at least `bytes` (contents not preserved on growth)
 template <typename T>
 inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) {

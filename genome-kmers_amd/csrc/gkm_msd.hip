@@ -1001,22 +1001,20 @@ __global__ __launch_bounds__(kST) void own_hist_kernel(L0Args a, uint32_t ntiles
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void pack2_kernel(const uint8_t *__restrict__ sba, uint64_t nwords,
                                                     uint64_t *__restrict__ code, uint32_t *__restrict__ dol) {
-    constexpr uint64_t kOnes = 0x0101010101010101ull;
     for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < nwords; g += (uint64_t)gridDim.x * 256) {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(sba + 32 * g);
-        const uint4 ra = s4[0], rb = s4[1];
-        const uint64_t x[4] = {((uint64_t)ra.y << 32) | ra.x, ((uint64_t)ra.w << 32) | ra.z,
-                               ((uint64_t)rb.y << 32) | rb.x, ((uint64_t)rb.w << 32) | rb.z};
-        uint64_t cw = 0;
-        uint32_t dw = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            cw = (cw << 16) | pack2_8(x[j]);
-            dw = (dw << 8) | gather_flags8(zero_bytes(x[j] ^ (kOnes * GK_DOLLAR)));
-        }
+        uint64_t cw;
+        uint32_t dw;
+        pack2_word(sba + 32 * g, cw, dw);
         code[g] = cw;
         dol[g] = dw;
     }
+}
+
+hipError_t launch_pack2(const uint8_t *from, uint64_t nwords, uint64_t *code, uint32_t *dol, hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    hipLaunchKernelGGL(pack2_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256), 0, s,
+                       from, nwords, code, dol);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3678,6 +3676,11 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         rc = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rc != GK_OK) return rc;
         c->pk_fresh = false;
+    } else if (c->res_pk && c->acgt && ks.bits == 2 && !ks.acgt_only) {
+        // the packed copy the transfer left beside the sba (gkm_xfer.hip): both L0 passes read 0.37 B
+        // per position instead of packing the bytes in every tile
+        d.pk_code = c->res_code;
+        d.pk_dol = c->res_dol;
     }
     uint64_t found = 0;
     // the packed L0 output (P88) when the level behind it writes packed pairs

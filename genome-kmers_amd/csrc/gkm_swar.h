@@ -106,4 +106,22 @@ __device__ __forceinline__ void key_from_2bit(uint64_t hi, uint64_t lo, int k, u
     }
 }
 
+// One word of the 2-bit packed sequence layout (gkm_msd.hip pack2_kernel, the L0 kernels' LDS
+// tiles): 32 bytes from p (16-byte aligned) -> their 2-bit codes (A0 C1 G2 T3, position 0 in the
+// most significant pair; other bytes get some code) and their '$' flags (position 0 in bit 31)
+__device__ __forceinline__ void pack2_word(const uint8_t *p, uint64_t &cw, uint32_t &dw) {
+    constexpr uint64_t kOnes = 0x0101010101010101ull;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(p);
+    const uint4 ra = s4[0], rb = s4[1];
+    const uint64_t x[4] = {((uint64_t)ra.y << 32) | ra.x, ((uint64_t)ra.w << 32) | ra.z,
+                           ((uint64_t)rb.y << 32) | rb.x, ((uint64_t)rb.w << 32) | rb.z};
+    cw = 0;
+    dw = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cw = (cw << 16) | pack2_8e(x[j]);
+        dw = (dw << 8) | gather_flags8(zero_bytes(x[j] ^ (kOnes * 0x24u)));  // '$'
+    }
+}
+
 }  // namespace gkm

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "gkm_internal.h"
+#include "gkm_swar.h"
 
 namespace gkm {
 
@@ -48,8 +49,14 @@ constexpr int kRawDepth = 4;             // raw chunk copies in flight (pinned s
 // device
 // ---------------------------------------------------------------------------------------------
 // packed byte b (bases 4j..4j+3 at bits 2i) -> 4 ASCII bytes, A0 C1 G2 T3
+// pkc / pkd (null: none): the chunk's words of the 2-bit packed copy (pack2_kernel layout, 32
+// positions per word): a packed block's codes are its own bytes with the base order of each
+// 32-base half reversed (rev_pairs), no '$'; a raw block is packed from its bytes (pack2_word).
+// Words of a partial last block are left to the caller (the tail pack after the transfer).
 __global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__restrict__ slot,
-                                                           uint8_t *__restrict__ dst, uint64_t chunk_len) {
+                                                           uint8_t *__restrict__ dst, uint64_t chunk_len,
+                                                           uint64_t *__restrict__ pkc = nullptr,
+                                                           uint32_t *__restrict__ pkd = nullptr) {
     __shared__ uint32_t s_lut[256];
     const int t = threadIdx.x;
     {
@@ -70,6 +77,15 @@ __global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__rest
         for (uint64_t i = t; i < q; i += 256)
             reinterpret_cast<uint4 *>(out)[i] = reinterpret_cast<const uint4 *>(src)[i];
         for (uint64_t i = q * 16 + t; i < blen; i += 256) out[i] = src[i];
+        if (pkc) {
+            for (uint64_t u = t; u < blen / 32; u += 256) {
+                uint64_t cw;
+                uint32_t dw;
+                pack2_word(src + 32 * u, cw, dw);
+                pkc[b0 / 32 + u] = cw;
+                pkd[b0 / 32 + u] = dw;
+            }
+        }
         return;
     }
     // 16 packed bytes -> 64 bases per lane step
@@ -86,6 +102,13 @@ __global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__rest
             uint4 *q = reinterpret_cast<uint4 *>(out + g * 64);
 #pragma unroll
             for (int k = 0; k < 4; ++k) q[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+            if (pkc) {
+                const uint64_t w = (b0 + g * 64) / 32;
+                const uint64_t c0 = rev_pairs(((uint64_t)p.y << 32) | p.x), c1 = rev_pairs(((uint64_t)p.w << 32) | p.z);
+                reinterpret_cast<uint4 *>(pkc + w)[0] =
+                    make_uint4((uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)c1, (uint32_t)(c1 >> 32));
+                reinterpret_cast<uint2 *>(pkd + w)[0] = make_uint2(0, 0);
+            }
         } else {  // the sba's last, partial group
             for (uint64_t i = g * 64; i < blen; ++i) out[i] = (uint8_t)(o[(i - g * 64) >> 2] >> (8 * (i & 3)));
         }
@@ -403,6 +426,16 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
         GK_TRY_HIP(c, hipEventCreateWithFlags(&c->unpack_done, hipEventDisableTiming));
     }
     hipStream_t us = c->unpack_stream;  // (everything before on c->stream is done: synchronised above)
+    // the packed copy of the sequence beside it (c->res_code / res_dol, valid once the transfer is
+    // complete: gk_set_sequence); the raw DMA of the hybrid mode skips the unpack, so not there.
+    // GKM_NO_RESIDENT_PACK=1: none (the L0 passes pack the bytes per tile)
+    c->res_pk = false;
+    const bool res = !hybrid && !std::getenv("GKM_NO_RESIDENT_PACK");
+    const uint64_t res_words = c->sba_cap / 32;
+    if (res) {
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->res_code), &c->res_code_cap, 8 * res_words + 64));
+        GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->res_dol), &c->res_dol_cap, 4 * res_words + 64));
+    }
     hipEvent_t *ev_copy = c->xfer_ev.data(), *ev_done = c->xfer_ev.data() + S;
     hipEvent_t *ev_raw = c->xfer_ev.data() + 2 * S;
     uint32_t *d_census = reinterpret_cast<uint32_t *>(c->scalars + 24);
@@ -495,7 +528,8 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             if (err == hipSuccess) err = hipStreamWaitEvent(us, ev_copy[s], 0);
             if (err == hipSuccess) {
                 hipLaunchKernelGGL(unpack_chunk_kernel, dim3((unsigned)((m + kXBlock - 1) / kXBlock)), dim3(256), 0,
-                                   us, ds, c->sba + k * chunk, m);
+                                   us, ds, c->sba + k * chunk, m, res ? c->res_code + k * chunk / 32 : nullptr,
+                                   res ? c->res_dol + k * chunk / 32 : nullptr);
                 err = hipGetLastError();
             }
             if (err == hipSuccess) err = hipEventRecord(ev_done[s], us);
@@ -579,6 +613,13 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // the context's stream (the sort's kernels, the census copy) after every unpack
     if (err == hipSuccess) err = hipEventRecord(c->unpack_done, us);
     if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, c->unpack_done, 0);
+    // the packed copy's last words -- the sequence's partial last 32 bytes and the '$' pad -- from
+    // the unpacked bytes
+    if (err == hipSuccess && res) {
+        const uint64_t w0 = (len & ~63ull) / 32;  // (from the last partial group of 64: the unpack skips it)
+        err = launch_pack2(c->sba + 32 * w0, res_words - w0, c->res_code + w0, c->res_dol + w0, c->stream);
+        if (err == hipSuccess) c->res_pk = true;  // (gk_set_sequence keeps it for an ACGT census)
+    }
     if (pf) {
         const int rc = prefetch_finish(c, pf, pf_ok && err == hipSuccess && prefix == C);
         if (err == hipSuccess && rc != GK_OK) return rc;

@@ -227,3 +227,31 @@ def test_packer_implementations_agree(impl, monkeypatch):
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(Path(__file__).resolve().parent.parent),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+# Round 5: the packed transfer leaves a 2-bit packed copy beside the resident sba (packed blocks'
+# codes reordered, raw blocks packed from their bytes, the partial last word and the '$' pad packed
+# after the transfer); msd_sort's L0 passes read it on an ACGT sba.  The sorted starts must equal
+# the oracle's and the same sort without the copy (GKM_NO_RESIDENT_PACK=1), whatever the lengths,
+# contig separators (raw blocks) and block / chunk boundaries.
+@pytest.mark.parametrize("L,contigs", [(3 * B + 999, 3), (5 * B + 17, 1), (9 * B, 4), (B + 33, 2), (700_001, 1)])
+@pytest.mark.parametrize("k,canonical", [(5, False), (21, False), (31, False), (32, True), (45, False), (45, True)])
+def test_resident_packed_copy_sorts_like_the_oracle(L, contigs, k, canonical, monkeypatch):
+    rng = np.random.default_rng(L + k)
+    sba, seg = genome(rng, L, contigs=contigs)
+    if L > 50_400 and not (sba[50_000:50_400] == ord("$")).any() and not (sba[1000:1400] == ord("$")).any():
+        sba[1000:1400] = sba[50_000:50_400]  # a repeat: ties
+    outs = []
+    for res in (True, False):
+        if not res:
+            monkeypatch.setenv("GKM_NO_RESIDENT_PACK", "1")
+        eng = load(sba, seg, monkeypatch, True, blocks=1, threads=2)
+        assert eng.is_acgt()
+        n = eng.enumerate(k)
+        eng.sort(k, canonical=canonical)
+        outs.append(eng.copy_starts(np.empty(n, dtype=np.uint32)))
+        monkeypatch.delenv("GKM_NO_RESIDENT_PACK", raising=False)
+    starts = oracle.enumerate_starts(sba, seg, k)
+    want = oracle.canonical_sort(sba, starts, k) if canonical else oracle.quicksort(sba, starts, k, k, break_ties=True)
+    np.testing.assert_array_equal(outs[0], want)
+    np.testing.assert_array_equal(outs[1], want)

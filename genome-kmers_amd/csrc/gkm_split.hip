@@ -1030,12 +1030,17 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     uint64_t *ok = c->keys[1];
     if (a_packed) {
         // the 2-bit packed sequence: three words past every start (the sba's '$' pad covers them)
+        // (the transfer's resident packed copy when there is one: the same codes at every position)
         const uint64_t nwords = (L + kSbaPad) / 32;
-        uint64_t *pk;
-        GK_TRY_HIP(c, scratch(c, "split_pk", nwords, &pk));
-        hipLaunchKernelGGL(split_pack_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)),
-                           dim3(256), 0, c->stream, c->sba, nwords, pk);
-        GK_TRY_HIP(c, hipGetLastError());
+        const uint64_t *pk = c->res_pk ? c->res_code : nullptr;
+        if (!pk) {
+            uint64_t *own;
+            GK_TRY_HIP(c, scratch(c, "split_pk", nwords, &own));
+            hipLaunchKernelGGL(split_pack_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)),
+                               dim3(256), 0, c->stream, c->sba, nwords, own);
+            GK_TRY_HIP(c, hipGetLastError());
+            pk = own;
+        }
 #define GK_MERGE_PK(W_)                                                                                         \
     do {                                                                                                        \
         hipLaunchKernelGGL((merge_a_kernel<W_, true>), ga, dim3(kMT), 0, c->stream, c->vals[0], c->heads, nA,     \

@@ -884,7 +884,13 @@ def test_packed_l0_split_vs_oracle(canonical, monkeypatch):
 # groups) and scattered IUPAC letters (the class-B rest), several contigs
 @pytest.mark.parametrize("k", [33, 40, 48, 49, 63])
 @pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
-def test_split_merge_packed_keys_vs_oracle(k, canonical, monkeypatch):
+@pytest.mark.parametrize("transfer", ["plain", "packed"])
+def test_split_merge_packed_keys_vs_oracle(k, canonical, transfer, monkeypatch):
+    # transfer "packed": the sequence goes through the packed transfer (GKM_PACK_MIN=0), whose
+    # resident packed copy the merge then reads instead of packing the sequence itself
+    if transfer == "packed":
+        monkeypatch.setenv("GKM_PACK_MIN", "0")
+        monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
     rng = np.random.default_rng(100 + k + canonical)
     s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 700_000)].copy()
     s[100_000:100_400] = ord("N")

@@ -999,21 +999,23 @@ __global__ __launch_bounds__(kST) void own_hist_kernel(L0Args a, uint32_t ntiles
 // read by every full-sequence pass (L0 count and partition; histogram, select count and store of
 // the key-range shards) instead of each pass re-packing the bytes: 0.28 B per position.
 // ---------------------------------------------------------------------------------------------
+template <bool NONACGT = false>
 __global__ __launch_bounds__(256) void pack2_kernel(const uint8_t *__restrict__ sba, uint64_t nwords,
                                                     uint64_t *__restrict__ code, uint32_t *__restrict__ dol) {
     for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < nwords; g += (uint64_t)gridDim.x * 256) {
         uint64_t cw;
         uint32_t dw;
-        pack2_word(sba + 32 * g, cw, dw);
+        pack2_word<NONACGT>(sba + 32 * g, cw, dw);
         code[g] = cw;
         dol[g] = dw;
     }
 }
 
+// (the transfer's resident copy: stops at every non-ACGT byte, pack2_word<true>)
 hipError_t launch_pack2(const uint8_t *from, uint64_t nwords, uint64_t *code, uint32_t *dol, hipStream_t s) {
     if (nwords == 0) return hipSuccess;
-    hipLaunchKernelGGL(pack2_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256), 0, s,
-                       from, nwords, code, dol);
+    hipLaunchKernelGGL(pack2_kernel<true>, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256),
+                       0, s, from, nwords, code, dol);
     return hipGetLastError();
 }
 
@@ -2525,8 +2527,8 @@ static int pack_sequence(gk_ctx *c, const uint64_t **code, const uint32_t **dol)
     int slot;
     timer_begin(c, "msd_pack", &slot);
     timer_units(c, slot, c->sba_len);
-    hipLaunchKernelGGL(pack2_kernel, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256), 0,
-                       c->stream, c->sba, nwords, pc, pd);
+    hipLaunchKernelGGL(pack2_kernel<false>, dim3((unsigned)std::min<uint64_t>((nwords + 255) / 256, 65536)), dim3(256),
+                       0, c->stream, c->sba, nwords, pc, pd);
     GK_TRY_HIP(c, hipGetLastError());
     timer_end(c, slot);
     *code = pc;
@@ -3676,9 +3678,10 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         rc = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rc != GK_OK) return rc;
         c->pk_fresh = false;
-    } else if (c->res_pk && c->acgt && ks.bits == 2 && !ks.acgt_only) {
+    } else if (c->res_pk && ks.bits == 2 && (c->acgt || ks.acgt_only)) {
         // the packed copy the transfer left beside the sba (gkm_xfer.hip): both L0 passes read 0.37 B
-        // per position instead of packing the bytes in every tile
+        // per position instead of packing the bytes in every tile.  Its stops are the non-ACGT bytes:
+        // '$' on an ACGT sba, every byte that ends the ACGT-only k-mers of a mixed one (class A)
         d.pk_code = c->res_code;
         d.pk_dol = c->res_dol;
     }

@@ -109,6 +109,9 @@ __device__ __forceinline__ void key_from_2bit(uint64_t hi, uint64_t lo, int k, u
 // One word of the 2-bit packed sequence layout (gkm_msd.hip pack2_kernel, the L0 kernels' LDS
 // tiles): 32 bytes from p (16-byte aligned) -> their 2-bit codes (A0 C1 G2 T3, position 0 in the
 // most significant pair; other bytes get some code) and their '$' flags (position 0 in bit 31)
+// NONACGT: the flags mark every byte other than A/C/G/T ('$' included) -- the stops of the class-A
+// (ACGT-only) k-mers of a mixed sba, and on an ACGT sba the same bits as the '$' flags
+template <bool NONACGT = false>
 __device__ __forceinline__ void pack2_word(const uint8_t *p, uint64_t &cw, uint32_t &dw) {
     constexpr uint64_t kOnes = 0x0101010101010101ull;
     const uint4 *s4 = reinterpret_cast<const uint4 *>(p);
@@ -120,7 +123,8 @@ __device__ __forceinline__ void pack2_word(const uint8_t *p, uint64_t &cw, uint3
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         cw = (cw << 16) | pack2_8e(x[j]);
-        dw = (dw << 8) | gather_flags8(zero_bytes(x[j] ^ (kOnes * 0x24u)));  // '$'
+        const uint64_t f = NONACGT ? non_acgt_bytes(x[j]) : zero_bytes(x[j] ^ (kOnes * 0x24u));  // ('$')
+        dw = (dw << 8) | gather_flags8(f);
     }
 }
 

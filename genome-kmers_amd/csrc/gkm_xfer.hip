@@ -51,7 +51,8 @@ constexpr int kRawDepth = 4;             // raw chunk copies in flight (pinned s
 // packed byte b (bases 4j..4j+3 at bits 2i) -> 4 ASCII bytes, A0 C1 G2 T3
 // pkc / pkd (null: none): the chunk's words of the 2-bit packed copy (pack2_kernel layout, 32
 // positions per word): a packed block's codes are its own bytes with the base order of each
-// 32-base half reversed (rev_pairs), no '$'; a raw block is packed from its bytes (pack2_word).
+// 32-base half reversed (rev_pairs), no stops; a raw block is packed from its bytes, its stops the
+// bytes other than A/C/G/T (pack2_word<true>).
 // Words of a partial last block are left to the caller (the tail pack after the transfer).
 __global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__restrict__ slot,
                                                            uint8_t *__restrict__ dst, uint64_t chunk_len,
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(256) void unpack_chunk_kernel(const uint8_t *__rest
             for (uint64_t u = t; u < blen / 32; u += 256) {
                 uint64_t cw;
                 uint32_t dw;
-                pack2_word(src + 32 * u, cw, dw);
+                pack2_word<true>(src + 32 * u, cw, dw);
                 pkc[b0 / 32 + u] = cw;
                 pkd[b0 / 32 + u] = dw;
             }

@@ -4075,6 +4075,9 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
     if (use_pack() && c->acgt && ks.bits == 2) {
         int rp = pack_sequence(c, &d.pk_code, &d.pk_dol);
         if (rp != GK_OK) return rp;
+    } else if (c->res_pk && ks.bits == 2 && (c->acgt || ks.acgt_only)) {  // the transfer's packed copy
+        d.pk_code = c->res_code;
+        d.pk_dol = c->res_dol;
     }
     const int ob = range_own_bits(ks);
     L0Args a{c->sba, lo, std::max(hi, lo), ks.symbols, d.B, ks.acgt_only};
@@ -4144,6 +4147,11 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
             if (rp != GK_OK) return rp;
         }
         c->pk_fresh = false;
+    } else if (c->res_pk && ks.bits == 2 && (c->acgt || ks.acgt_only)) {  // the transfer's packed copy
+        a.pk_code = c->res_code;
+        a.pk_dol = c->res_dol;
+        d.pk_code = c->res_code;
+        d.pk_dol = c->res_dol;
     }
     // Fused select (round 5): when the rank keeps a large share of the k-mers, its L0 count and
     // partition run over the whole sequence and keep only the owned k-mers (msd0_pipe_kernel<...,

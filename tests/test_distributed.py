@@ -406,6 +406,18 @@ def test_gpu_key_ranges_fused_select(fused, world, contigs, k, canonical, iupac,
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
+# Round 5: through the packed transfer (GKM_PACK_MIN=0) the ranks' select, histogram and fused L0
+# read the resident 2-bit packed copy of the sequence (stops = non-ACGT bytes: class A of a mixed sba)
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
+    (2, 1, 31, False, False), (5, 3, 31, False, True), (8, 2, 31, True, True), (2, 2, 63, True, True),
+    (3, 1, 21, False, False)])
+def test_gpu_key_ranges_resident_packed_copy(world, contigs, k, canonical, iupac, monkeypatch):
+    monkeypatch.setenv("GKM_PACK_MIN", "0")
+    monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
+    test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,k,canonical", [(2, 31, False), (2, 63, True)])
 def test_gpu_key_ranges_fused_packed_l0(world, k, canonical, monkeypatch):

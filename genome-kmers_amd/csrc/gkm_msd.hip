@@ -4273,6 +4273,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         timer_begin(c, "msd_select", &slot);
         timer_units(c, slot, L);
         launch(2);
+        const uint64_t stride = (uint64_t)tpw * kSTile;  // each chunk's region (launch sets tpw)
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
         std::vector<uint32_t> kc(nchunk);
@@ -4280,7 +4281,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         for (uint32_t w = 0; w < nchunk; ++w) {
             if (!kc[w]) continue;
-            poff.push_back((uint64_t)w * tpw * kSTile);
+            poff.push_back((uint64_t)w * stride);
             plen.push_back(kc[w]);
             found += kc[w];
         }

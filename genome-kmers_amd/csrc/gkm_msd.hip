@@ -2907,11 +2907,27 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "msd_nd", n + 64, &nd));
             ndg.out = nd;
         }
-        static const bool exp_l0 = std::getenv("GKM_EXP_L0") != nullptr;  // timing experiments only
-        if (exp_l0 && with_nd && w0 == 7)
-            hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 7>), dim3(pgrid), dim3(kP0T), 0, c->stream, c->sba,
-                               count, (uint32_t)l0_tiles, kout, vout, nd);
-        else
+        // timing experiments only (wrong output): GKM_EXP_L0=1 the scatter floor at 2^7 runs per tile,
+        // =4 / 5 / 6 / 8 at 2^R runs (the same bytes in fewer or more write streams)
+        static const char *exp_l0 = std::getenv("GKM_EXP_L0");
+        const int exp_r = exp_l0 ? (exp_l0[0] == '1' ? 7 : exp_l0[0] - '0') : 0;
+        if (exp_r && with_nd && w0 == 7) {
+            if (exp_r == 4)
+                hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 4>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+            else if (exp_r == 5)
+                hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 5>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+            else if (exp_r == 6)
+                hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 6>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+            else if (exp_r == 8)
+                hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 8>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+            else
+                hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 7>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+        } else
             l0_dispatch(false, w0, with_nd, l0a, d0, (unsigned)l0_tiles, kout, vout, (uint32_t)l0_tiles, count, ndg);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);

@@ -628,6 +628,38 @@ __global__ __launch_bounds__(T) void l0_scatter_floor_kernel(const uint8_t *__re
     }
 }
 
+// TIMING EXPERIMENTS ONLY (GKM_EXP_L0=v, wrong output): the scatter floor above with each lane
+// writing 4 consecutive slots of one run by vector stores (two 16-byte stores of keys, one of starts,
+// one 4-byte store of digits) -- how much of the floor is the store width rather than the stream?
+template <int T, int I, int R>
+__global__ __launch_bounds__(T) void l0_scatter_floor4_kernel(const uint8_t *__restrict__ sba, uint64_t n,
+                                                              uint32_t ntiles, uint64_t *__restrict__ kout,
+                                                              uint32_t *__restrict__ vout, uint8_t *__restrict__ nd) {
+    constexpr int TILE = T * I, RUN = TILE >> R;
+    static_assert(RUN % 4 == 0 && I % 4 == 0, "whole 4-slot groups per run");
+    const TileWalk walk(ntiles);
+    const uint64_t bsz = (n >> R) & ~3ull;
+    for (uint32_t t = walk.first; t < walk.end; t += walk.step) {
+        const uint64_t P0 = (uint64_t)t * TILE;
+        const uint32_t x = reinterpret_cast<const uint32_t *>(sba + P0)[threadIdx.x];
+#pragma unroll 2
+        for (int g = 0; g < I / 4; ++g) {
+            const uint32_t s = 4 * (threadIdx.x + g * T), d = s / RUN, j = s - d * RUN;
+            const uint64_t o = min((uint64_t)d * bsz + (uint64_t)t * RUN + j, (n - 4) & ~3ull);
+            uint64_t h[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) h[u] = (P0 + s + u + (x & 1u)) * 0x9E3779B97F4A7C15ull;
+            uint4 *k4 = reinterpret_cast<uint4 *>(kout + o);
+            k4[0] = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
+            k4[1] = make_uint4((uint32_t)h[2], (uint32_t)(h[2] >> 32), (uint32_t)h[3], (uint32_t)(h[3] >> 32));
+            reinterpret_cast<uint4 *>(vout + o)[0] =
+                make_uint4((uint32_t)(P0 + s), (uint32_t)(P0 + s + 1), (uint32_t)(P0 + s + 2), (uint32_t)(P0 + s + 3));
+            reinterpret_cast<uint32_t *>(nd + o)[0] = (uint32_t)(h[0] >> 49 & 0xFF) | (uint32_t)(h[1] >> 49 & 0xFF) << 8 |
+                                                      (uint32_t)(h[2] >> 49 & 0xFF) << 16 | (uint32_t)(h[3] >> 49 & 0xFF) << 24;
+        }
+    }
+}
+
 // Wide L0 partition (R = 10 or 11 bits; 2-bit keys of one word, forward, no profile): the
 // position-staged, software-pipelined scheme of msd0_pipe_kernel with a digit space the 7-bit one
 // cannot hold -- per-wave u16 counters, two per word (rank_atomic16), K = RADIX / T digits per
@@ -2908,9 +2940,10 @@ struct MsdDriver {
             ndg.out = nd;
         }
         // timing experiments only (wrong output): GKM_EXP_L0=1 the scatter floor at 2^7 runs per tile,
-        // =4 / 5 / 6 / 8 at 2^R runs (the same bytes in fewer or more write streams)
+        // =4 / 5 / 6 / 8 at 2^R runs (the same bytes in fewer or more write streams), =v at 2^7 runs
+        // with 4-slot vector stores
         static const char *exp_l0 = std::getenv("GKM_EXP_L0");
-        const int exp_r = exp_l0 ? (exp_l0[0] == '1' ? 7 : exp_l0[0] - '0') : 0;
+        const int exp_r = exp_l0 ? (exp_l0[0] == '1' || exp_l0[0] == 'v' ? 7 : exp_l0[0] - '0') : 0;
         if (exp_r && with_nd && w0 == 7) {
             if (exp_r == 4)
                 hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 4>), dim3(pgrid), dim3(kP0T), 0, c->stream,
@@ -2920,6 +2953,9 @@ struct MsdDriver {
                                    c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
             else if (exp_r == 6)
                 hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 6>), dim3(pgrid), dim3(kP0T), 0, c->stream,
+                                   c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
+            else if (exp_l0[0] == 'v')
+                hipLaunchKernelGGL((l0_scatter_floor4_kernel<kP0T, kP0I, 7>), dim3(pgrid), dim3(kP0T), 0, c->stream,
                                    c->sba, count, (uint32_t)l0_tiles, kout, vout, nd);
             else if (exp_r == 8)
                 hipLaunchKernelGGL((l0_scatter_floor_kernel<kP0T, kP0I, 8>), dim3(pgrid), dim3(kP0T), 0, c->stream,

@@ -953,13 +953,26 @@ __global__ __launch_bounds__(256) void qs_pack_kernel(const uint32_t *__restrict
 // copy taken before the sort), then numba's quicksort on the host over those words with rank
 // comparisons (gkm_qsort.cpp); the result replaces the sorted starts.  Only members of a group
 // change places, so keys, head flags and unique counts stay valid.  Host memory: 8 B per k-mer.
-static int apply_quicksort_order(gk_ctx *c, const uint32_t *orig) {
+static int apply_quicksort_order(gk_ctx *c, std::vector<uint32_t> &orig_host) {
     const uint64_t n = c->n;
     uint64_t G = 0;
     if (int rc = gk_unique_counts(c, &G)) return rc;
     if (int rc = materialize_starts(c)) return rc;
-    uint32_t *rank_of_pos;
+    // the one-off buffers below (4 B per position + 12 B per k-mer) are released on every return
+    struct Release {
+        gk_ctx *c;
+        ~Release() {
+            scratch_release(c, "qs_orig");
+            scratch_release(c, "qs_rank");
+            scratch_release(c, "qs_words");
+        }
+    } release{c};
+    uint32_t *orig, *rank_of_pos;
     uint64_t *words;
+    GK_TRY_HIP(c, scratch(c, "qs_orig", n, &orig));
+    GK_TRY_HIP(c, hipMemcpyAsync(orig, orig_host.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+    GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t>().swap(orig_host);  // (host peak: the 8 B per k-mer below)
     GK_TRY_HIP(c, scratch(c, "qs_rank", c->sba_len + 1, &rank_of_pos));
     GK_TRY_HIP(c, scratch(c, "qs_words", n, &words));
     hipLaunchKernelGGL(qs_rank_scatter_kernel, dim3(grid_of(n)), dim3(256), 0, c->stream, c->vals[c->cur], n, c->idx_b,
@@ -972,9 +985,14 @@ static int apply_quicksort_order(gk_ctx *c, const uint32_t *orig) {
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     if (quicksort_by_rank(A.data(), n) != 0)
         return fail(c, GK_E_UNSUPPORTED, "numba quicksort stack limit (MAX_STACK = 100) exceeded");
-    std::vector<uint32_t> S(n);
-    for (uint64_t i = 0; i < n; ++i) S[i] = (uint32_t)A[i];
-    GK_TRY_HIP(c, hipMemcpyAsync(c->vals[c->cur], S.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+    // the starts (low halves) packed in place into the first 4 n bytes of A: element i is read
+    // before bytes [4 i, 4 i + 4) are written, and those lie inside elements already read
+    unsigned char *S = reinterpret_cast<unsigned char *>(A.data());
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t s = (uint32_t)A[i];
+        std::memcpy(S + 4 * i, &s, 4);
+    }
+    GK_TRY_HIP(c, hipMemcpyAsync(c->vals[c->cur], S, 4 * n, hipMemcpyHostToDevice, c->stream));
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     return GK_OK;
 }
@@ -1009,11 +1027,14 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     // only the fixed-length forward sort of the whole enumeration uses a prefetched L0 (sort_direct)
     if (canonical || qorder || max_kmer_len != c->min_k || !from_enum) pre_drop(c);
     int rc;
-    uint32_t *orig = nullptr;  // the start order the reference's quicksort starts from (device copy)
+    // the start order the reference's quicksort starts from: a host copy (4 B per k-mer), so the
+    // device sort's memory peak is not raised by it
+    std::vector<uint32_t> orig;
     if (qorder && c->n >= 2) {
         if ((rc = materialize_starts(c))) return rc;
-        GK_TRY_HIP(c, scratch(c, "qs_orig", c->n, &orig));
-        GK_TRY_HIP(c, hipMemcpyAsync(orig, c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToDevice, c->stream));
+        orig.resize(c->n);
+        GK_TRY_HIP(c, hipMemcpyAsync(orig.data(), c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
     }
     if (c->n < 2) {
         rc = materialize_starts(c);

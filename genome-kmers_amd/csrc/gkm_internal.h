@@ -204,6 +204,13 @@ inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) 
     *out = static_cast<T *>(e.first);
     return r;
 }
+// frees a named scratch buffer (one-off large buffers that must not stay for the context's life)
+inline void scratch_release(gk_ctx *c, const char *name) {
+    auto it = c->scratch.find(name);
+    if (it == c->scratch.end()) return;
+    if (it->second.first) (void)hipFree(it->second.first);
+    c->scratch.erase(it);
+}
 // re-encode keys[cur] from vals[cur] when the sort left them stale (gk_ctx::keys_stale)
 int ensure_keys(gk_ctx *c);
 // MSD sort of fixed-length keys from the enumerated positions (gkm_msd.hip)

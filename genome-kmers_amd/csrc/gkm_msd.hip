@@ -992,6 +992,116 @@ __global__ __launch_bounds__(kST, CANON ? 1 : GKM_SEL_MINW) void msd0_select_ker
     if (MODE == 2 && tid == 0 && blockIdx.x * tpw < ntiles) wave_cnt[blockIdx.x] = (uint32_t)run;
 }
 
+// Key-range select from the packed copy, SWAR (round 6): forward 2-bit keys of <= 32 symbols whose
+// sequence has a 2-bit packed copy (a.pk_code / a.pk_dol: 32 positions per u64 of codes and u32 of
+// stops).  No LDS tile, no barrier: each WAVE walks its own chunk of gpw consecutive 32-position
+// groups, 64 groups (2,048 positions) per step, one group per lane, and appends its kept k-mers at
+// a running offset into its own region of the output, [first group * 32, + gpw * 32) -- the pieces
+// of one bucket in position order, as the workgroup chunks of msd0_select_kernel<..., 2> are.
+// Per lane and group (w = the group's codes, x2 = the top half of the next group's codes):
+//   ownership digit of position j = the top own_bits bits of the 32-bit window at bit 2 j of
+//   w:x2 (one funnel shift); the range test is one subtract and one compare against the range
+//   shifted to the window's top, so the digit is never extracted (~4 VALU per position; the tile
+//   select spent ~20 per position, VALU-bound at 2.8 ms per C3 rank);
+//   stops: a lane with a stop in its 64-position window smears them over S positions in 5
+//   doubling steps (all 32 positions at once).
+// The kept positions are staged per wave as group-relative u16 in position order (a loop over the
+// set bits of the keep mask), the step's 65 code words beside them, and the k-mers leave as one
+// coalesced run: key (re-derived from the staged words), start, L0 digit byte.
+constexpr int kRselW = 4;  // waves per workgroup (independent: no barrier)
+__global__ __launch_bounds__(kRselW * 64) void msd0_rsel_kernel(L0Args a, Dig d0, uint64_t ngroups, uint64_t gpw,
+                                                                 uint32_t lo_w, uint32_t spm1_w,
+                                                                 uint32_t *__restrict__ wave_cnt,
+                                                                 uint64_t *__restrict__ kout,
+                                                                 uint32_t *__restrict__ vout,
+                                                                 uint8_t *__restrict__ nd_out) {
+    __shared__ uint16_t s_pos[kRselW][2048];
+    __shared__ uint64_t s_w[kRselW][65];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t gw = (uint64_t)blockIdx.x * kRselW + wave;
+    const uint64_t g0 = gw * gpw, g1 = min(g0 + gpw, ngroups);
+    uint16_t *sp = s_pos[wave];
+    uint64_t *sw = s_w[wave];
+    const int S = a.symbols, B = a.total_bits;
+    uint64_t run = 0;
+    const uint64_t out0 = g0 * 32;
+    // software pipeline: the next step's words fly while this one is processed
+    uint64_t w = 0, w1 = 0;
+    uint32_t d = 0, d1 = 0;
+    auto load = [&](uint64_t base) {
+        const uint64_t g = min(base + (uint64_t)lane, ngroups - 1);
+        w = a.pk_code[g];
+        w1 = a.pk_code[g + 1];
+        d = a.pk_dol[g];
+        d1 = a.pk_dol[g + 1];
+    };
+    if (g0 < g1) load(g0);
+    for (uint64_t base = g0; base < g1; base += 64) {
+        const uint64_t W0 = w, W1 = w1;
+        const uint32_t D0 = d, D1 = d1;
+        const bool live = base + (uint64_t)lane < g1;
+        if (base + 64 < g1) load(base + 64);
+        // ownership: position j <-> bit 31 - j of m (MSB first, the order of the staging loop)
+        const uint32_t x0 = (uint32_t)(W0 >> 32), x1 = (uint32_t)W0, x2 = (uint32_t)(W1 >> 32);
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int r = (2 * j) & 31;
+            const uint32_t hi = j < 16 ? x0 : x1, lo = j < 16 ? x1 : x2;
+            const uint32_t win = r ? __builtin_amdgcn_alignbit(hi, lo, 32 - r) : hi;
+            m = (m << 1) | (uint32_t)(win - lo_w <= spm1_w);
+        }
+        // stops: invalid where a stop lies in [j, j + S); D0 / D1 bit 31 - i = position i
+        if (__ballot((D0 | D1) != 0)) {
+            uint64_t x = ((uint64_t)D0 << 32) | D1;
+            uint64_t sm = x;  // sm: a stop in [j, j + len)
+            int len = 1;
+#pragma unroll
+            for (int s = 1; s < 32; s <<= 1) {
+                if (2 * len <= S) {
+                    sm |= sm << len;
+                    len *= 2;
+                }
+            }
+            if (len < S) sm |= sm << (S - len);
+            m &= ~(uint32_t)(sm >> 32);
+        }
+        if (!live) m = 0;
+        const uint32_t cnt = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        if (total == 0) continue;
+        // stage: the group-relative positions of the kept k-mers in position order, the words
+        uint32_t j = incl - cnt;
+        while (m) {
+            const uint32_t b = __clz(m);
+            sp[j++] = (uint16_t)(lane * 32 + b);
+            m ^= 0x80000000u >> b;
+        }
+        sw[lane] = W0;
+        if (lane == 63) sw[64] = W1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        const uint64_t o = out0 + run, P0 = base * 32;
+        for (uint32_t e = lane; e < total; e += 64) {
+            const uint32_t p = sp[e], q = p >> 5, s = (p & 31) * 2;
+            const uint64_t A = sw[q];
+            const uint64_t T = s ? (A << s) | (sw[q + 1] >> (64 - s)) : A;
+            const uint64_t k = T >> (64 - B);
+            kout[o + e] = k;
+            vout[o + e] = (uint32_t)(P0 + p);
+            nd_out[o + e] = (uint8_t)dg_of(k, d0);
+        }
+        run += total;
+        // the next step's staging overwrites these slots: every lane has read them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+    if (lane == 0 && g0 < ngroups) wave_cnt[gw] = (uint32_t)run;
+}
+
 // Ownership-digit histogram of a key-range shard's position share: the top own_bits (<= 12) bits
 // of every k-mer starting in [a.lo, a.hi), one LDS table per workgroup flushed into ghist.
 template <int BITS, bool CANON>
@@ -3903,7 +4013,12 @@ int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     // for them
     GK_TRY_HIP(c, hipEventRecord(c->pre_ev[p->next], c->unpack_stream ? c->unpack_stream : c->stream));
     GK_TRY_HIP(c, hipStreamWaitEvent(c->pre_stream, c->pre_ev[p->next], 0));
-    hipStream_t keep = c->stream;
+    // the regions run on the prefetch stream; every return below restores the context's stream
+    struct StreamSwap {
+        gk_ctx *c;
+        hipStream_t keep;
+        ~StreamSwap() { c->stream = keep; }
+    } swap{c, c->stream};
     c->stream = c->pre_stream;
     MsdDriver d(c, p->ks);
     if (p->p88) {  // the regions' low start bits and digit bytes in vals[1] (p88_place)
@@ -3927,7 +4042,6 @@ int prefetch_launch(gk_ctx *c, L0Prefetch *p, uint64_t landed) {
     }
     timer_units(c, slot, units);
     timer_end(c, slot);
-    c->stream = keep;
     return rc;
 }
 
@@ -4316,6 +4430,48 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         launch(1);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
+    } else if (ks.bits == 2 && !ks.canonical && a.pk_code && ks.symbols <= 32 && a.own_bits <= 32 &&
+               !std::getenv("GKM_RSEL_OFF")) {
+        // the SWAR select over the packed copy: one region per wave (msd0_rsel_kernel)
+        const uint64_t ngroups = (L + 31) / 32;
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, msd0_rsel_kernel, kRselW * 64, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        uint64_t nwv = (uint64_t)d.cus * (unsigned)per_cu * kRselW;
+        const uint64_t gpw = ((ngroups + nwv - 1) / nwv + 63) / 64 * 64;  // whole 64-group steps per wave
+        nwv = (ngroups + gpw - 1) / gpw;
+        const unsigned nblk = (unsigned)((nwv + kRselW - 1) / kRselW);
+        const uint64_t cap = (uint64_t)nblk * kRselW * gpw * 32;  // every wave region is full-size
+        if (cap > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "sequence too long for uint32 start indices");
+        int rc = ensure_elems(c, cap, 1);
+        if (rc != GK_OK) return rc;
+        GK_TRY_HIP(c, scratch(c, "msd_nd", cap + 64, &d.nd));
+        GK_TRY_HIP(c, scratch(c, "sel_wave_cnt", (uint64_t)nblk * kRselW + 1, &wave_cnt));
+        const int sh = 32 - a.own_bits;
+        const uint32_t lo_w = (uint32_t)((uint64_t)a.own_lo << sh);
+        const uint32_t spm1_w = (uint32_t)(((uint64_t)std::min<uint64_t>(a.own_span, 1ull << a.own_bits) << sh) - 1);
+        timer_begin(c, "msd_select", &slot);
+        timer_units(c, slot, L);
+        if (a.own_span == 0) {
+            GK_TRY_HIP(c, hipMemsetAsync(wave_cnt, 0, 4 * nwv, c->stream));
+        } else {
+            hipLaunchKernelGGL(msd0_rsel_kernel, dim3(nblk), dim3(kRselW * 64), 0, c->stream, a, d0, ngroups, gpw, lo_w,
+                               spm1_w, wave_cnt, c->keys[1], c->vals[1], d.nd);
+        }
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        std::vector<uint32_t> kc(nwv);
+        GK_TRY_HIP(c, hipMemcpyAsync(kc.data(), wave_cnt, 4 * nwv, hipMemcpyDeviceToHost, c->stream));
+        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        for (uint64_t w = 0; w < nwv; ++w) {
+            if (!kc[w]) continue;
+            poff.push_back(w * gpw * 32);
+            plen.push_back(kc[w]);
+            found += kc[w];
+        }
+        timer_units(c, slot, found);
+        if (found > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
     } else {
         const uint64_t cap = (uint64_t)ntiles * kSTile;  // every chunk region is full-size
         if (cap > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "sequence too long for uint32 start indices");

@@ -455,6 +455,7 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     std::vector<char> chunk_issued(C, 0);    // chunk k's unpack is enqueued
     uint64_t prefix = 0;                     // chunks [0, prefix) issued
     bool pf_ok = pf != nullptr;
+    int pf_rc = GK_OK;
     bool abort = false;
     for (int i = 0; i < S; ++i) free_slots.push_back(i);
     std::atomic<uint32_t> cls{0};
@@ -551,8 +552,8 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
                 pf_ok = false;
             } else if (int rc = prefetch_launch(c, pf, std::min(prefix * chunk, len))) {
                 pf_ok = false;
+                pf_rc = rc;
                 err = hipErrorUnknown;
-                (void)rc;
             }
         }
         // recycle slots whose unpack has run
@@ -614,6 +615,12 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // the context's stream (the sort's kernels, the census copy) after every unpack
     if (err == hipSuccess) err = hipEventRecord(c->unpack_done, us);
     if (err == hipSuccess) err = hipStreamWaitEvent(c->stream, c->unpack_done, 0);
+    if (err != hipSuccess) {
+        // an error leaves unpack (and prefetch) kernels in flight that still read the staging slots
+        // and write the sba and the packed copy: drain both streams before the slots can be reused
+        (void)hipStreamSynchronize(us);
+        if (c->pre_stream) (void)hipStreamSynchronize(c->pre_stream);
+    }
     // the packed copy's last words -- the sequence's partial last 32 bytes and the '$' pad -- from
     // the unpacked bytes
     if (err == hipSuccess && res) {
@@ -625,6 +632,7 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
         const int rc = prefetch_finish(c, pf, pf_ok && err == hipSuccess && prefix == C);
         if (err == hipSuccess && rc != GK_OK) return rc;
     }
+    if (pf_rc != GK_OK) return pf_rc;  // (prefetch_launch's own error; it set the message)
     if (err != hipSuccess) return hip_fail(c, err, "packed sba transfer");
     uint32_t cen[2] = {0, 0};
     if (hybrid && raw_chunks) {  // the device census of the raw chunks (waits for them to land)

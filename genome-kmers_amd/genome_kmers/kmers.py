@@ -386,6 +386,10 @@ _UNSORTED_GROUP_MSG = (
 class Kmers:
     """Memory-efficient k-mer calculations on a genome, resident on one MI355X."""
 
+    # fixed-length Kmers run the first pass of the forward sort while the sequence is transferred
+    # (gk_sort_hint); False skips it (see _get_engine for its cost)
+    sort_prefetch = True
+
     def __init__(self, seq_coll: Union[SequenceCollection, None] = None, min_kmer_len: int = 1,
                  max_kmer_len: Union[int, None] = None, source_strand: str = "forward",
                  track_strands_separately: bool = False, method: str = "single_pass") -> None:
@@ -485,8 +489,11 @@ class Kmers:
     def _get_engine(self) -> "_native.Engine":
         if self._engine is None:
             eng = _native.Engine()
-            # a fixed k-mer length: the transfer also runs the first pass of sort(k) (gk_sort_hint)
-            if self.min_kmer_len is not None and self.min_kmer_len == self.max_kmer_len:
+            # a fixed k-mer length: the transfer also runs the first pass of sort(k) (gk_sort_hint).
+            # That pass costs device memory for every position (~13 B) and its work at load time;
+            # a canonical, reference-order or unsorted workflow drops it, so such callers can set
+            # Kmers.sort_prefetch = False (class- or instance-wide) before the first device call
+            if self.sort_prefetch and self.min_kmer_len is not None and self.min_kmer_len == self.max_kmer_len:
                 eng.sort_hint(self.min_kmer_len)
             eng.set_sequence(self.seq_coll.forward_sba, self.seq_coll._forward_sba_seg_starts)
             self._engine = eng

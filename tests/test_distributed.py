@@ -394,7 +394,7 @@ def test_gpu_key_ranges_packed_pairs(world, contigs, k, canonical, iupac, monkey
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
-# Round 5: a rank keeping a large share (<= 4 ranks by default) fuses its select into the L0
+# Round 5: a rank keeping at least half of the ownership digits (<= 2 ranks by default) fuses its select into the L0
 # (msd0_pipe_kernel<..., OWN>); GKM_RANGE_FUSED=0/1 forces either path at any world size
 @pytest.mark.gpu
 @pytest.mark.parametrize("fused", ["0", "1"], ids=["select", "fused"])
@@ -407,11 +407,13 @@ def test_gpu_key_ranges_fused_select(fused, world, contigs, k, canonical, iupac,
 
 
 # Round 5: through the packed transfer (GKM_PACK_MIN=0) the ranks' select, histogram and fused L0
-# read the resident 2-bit packed copy of the sequence (stops = non-ACGT bytes: class A of a mixed sba)
+# read the resident 2-bit packed copy of the sequence (stops = non-ACGT bytes: class A of a mixed sba);
+# round 6: forward keys of <= 32 symbols take the SWAR select over it (msd0_rsel_kernel)
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
     (2, 1, 31, False, False), (5, 3, 31, False, True), (8, 2, 31, True, True), (2, 2, 63, True, True),
-    (3, 1, 21, False, False)])
+    (3, 1, 21, False, False), (8, 1, 31, False, False), (3, 1, 5, False, True), (4, 2, 32, False, False),
+    (7, 2, 16, False, True), (6, 3, 3, False, False)])
 def test_gpu_key_ranges_resident_packed_copy(world, contigs, k, canonical, iupac, monkeypatch):
     monkeypatch.setenv("GKM_PACK_MIN", "0")
     monkeypatch.setenv("GKM_PACK_BLOCKS", "1")

@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--exchange", choices=("range", "a2a"), default="range",
                     help="multi-GPU scheme: key ranges re-derived from the resident sequence (no k-mer "
                          "exchange) or one all-to-all of the encoded k-mers")
+    ap.add_argument("--opt", action="append", default=[], metavar="GKM_NAME=VALUE",
+                    help="a libgkm test/tuning override (gk_set_option), for A/B runs; repeatable")
     ap.add_argument("--traffic", type=str, default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="per-launch HBM bytes of the dominant kernel from rocprofv3 --pmc (if present)")
     return ap.parse_args()
@@ -388,6 +390,11 @@ def run_ref_profile(args, torch, result_out, log):
     checked = order_check(eng, sba, M)
     words, bits, _ = eng.key_layout()
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
+    # the whole step against the HBM peak: the algorithmic bytes of every priced stage per step over
+    # the step's wall time (the dominant kernel's `frac` is one kernel; this is all of them, and the
+    # step's unpriced remainder -- scans, classify, host round trips -- counts as time)
+    step_bytes = sum(stage_bytes(n, v) for n, v in report.items() if v.get("total_ms", 0) > 0) / args.steps
+    step_frac = step_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9)
     msd = "radix_pass" not in report and any(k.startswith("msd_") for k in report)
     if not msd:
         # dominant kernel: the LSD onesweep pass (every radix_pass launch: keys W words + start in and out)
@@ -492,6 +499,9 @@ def main():
 
     from genome_kmers import _native, synthetic
 
+    for o in args.opt:
+        name, _, v = o.partition("=")
+        _native.options[name] = v
     if args.config == "ref_profile":
         if world != 1:
             raise SystemExit("--config ref_profile runs on one GPU")
@@ -604,8 +614,12 @@ def main():
         e2e_ms = ms_per_step + boundary["set_sequence_ms"]
     value_e2e = n_units / (e2e_ms * 1e-3) if e2e_ms else None
 
-    # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4
-    seq_bytes = L if dist is None or args.exchange == "range" else job.hi - job.lo
+    # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4.  The L0 passes read
+    # the sequence: its resident 2-bit packed copy when gk_set_sequence left one (0.375 B per
+    # position: a u64 of codes and a u32 of stop flags per 32 positions), else the ASCII bytes
+    packed_in = eng.resident_packed() and eng.is_acgt()
+    seq_positions = L if dist is None or args.exchange == "range" else job.hi - job.lo
+    seq_bytes = seq_positions * (0.375 if packed_in else 1.0)
 
     range_mode = dist is not None and args.exchange == "range"
     # the last global level was compact: the wave-local round reads 9 B per element, not 12; a
@@ -621,7 +635,13 @@ def main():
         if name == "msd_select_count":
             return u  # key-range shards: the whole sequence, 1 B per position
         if name == "msd_select":
-            return L * v["count"] + 13 * u  # the whole sequence in; kept (key, start, digit) out (units: kept)
+            return seq_bytes * v["count"] + 13 * u  # the whole sequence in; kept (key, start, digit) out (units: kept)
+        if name == "msd_l0_count":
+            return seq_bytes * v["count"]  # the sequence in (per-tile digit counts out: negligible)
+        if name == "histogram":
+            return seq_bytes / max(world, 1) * v["count"]  # the rank's position share of the sequence
+        if name == "msd_count_nd":
+            return u  # 1 digit byte per element in
         if name == "msd_pass_l0" and not range_mode:
             return seq_bytes * v["count"] + 13 * u  # sequence bytes in, (key, start, next digit) out
         if name == "msd_pass_l0k" and not range_mode:
@@ -682,6 +702,11 @@ def main():
     bytes_per_launch = dom_bytes / max(rp["count"], 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     stages = {name: round(v["total_ms"] / args.steps, 3) for name, v in report.items()}
+    # the whole step against the HBM peak: the algorithmic bytes of every priced stage per step over
+    # the step's wall time (the dominant kernel's `frac` is one kernel; this is all of them, and the
+    # step's unpriced remainder -- scans, classify, host round trips -- counts as time)
+    step_bytes = sum(stage_bytes(n, v) for n, v in report.items() if v.get("total_ms", 0) > 0) / args.steps
+    step_frac = step_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9)
     traffic, traffic_src = load_traffic(args.traffic, kdesc)
     # BASELINE.md section 3, verbatim: the step's read roofline n * 105 B / t (device boundary and
     # end to end), and the total-traffic fraction n * 201 B / t -- a model of the whole step, beside
@@ -695,6 +720,12 @@ def main():
                               "ms_per_step (device) or e2e_ms (end to end) / 8 TB/s"}
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "step_hbm_frac": round(step_frac, 4), "step_algorithmic_bytes": int(step_bytes),
+                "step_model": "sum of every priced stage's algorithmic bytes (DESIGN.md section 4; the L0 "
+                              "input priced as the " + ("0.375 B/position resident packed copy" if packed_in else
+                                                        "1 B/position sequence bytes") +
+                              ") per step / ms_per_step / 8 TB/s -- the measured whole-step HBM fraction, beside "
+                              "BASELINE.md's 8-pass LSD model (baseline_read_frac)",
                 **base,
                 "kernel": f"{kdesc} ({dom}: {what})",
                 "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
@@ -718,9 +749,12 @@ def main():
                         "interval from the sba in pinned host memory to that product in HBM (gk_set_sequence's "
                         "packed / raw transfer + one step; BASELINE.md section 3); the D2H of the "
                         "sorted starts is reported apart (d2h_starts_ms)",
-            "value_boundary": "device: the sba resident in HBM when the timed region starts (the bench contract); "
-                              "the end-to-end figure of BASELINE.md section 3, pinned host sba -> product in HBM, "
-                              "is value_e2e",
+            "value_boundary": "device: the sba resident in HBM when the timed region starts (the bench contract)"
+                              + ("; with it the 2-bit packed copy of the sequence (1.17 GB at C3) that "
+                                 "gk_set_sequence's packed transfer writes beside the sba outside the timed region "
+                                 "-- the L0 passes read it (0.375 B/position)" if packed_in else "") +
+                              "; the end-to-end figure of BASELINE.md section 3, pinned host sba -> product in HBM "
+                              "(transfer + packed copy + step), is value_e2e",
             "value_e2e": round(value_e2e, 1) if value_e2e else None, "e2e_ms": round(e2e_ms, 2) if e2e_ms else None,
             **({} if e2e is None else {"e2e": e2e}),
             "set_sequence_ms": boundary["set_sequence_ms"], "d2h_starts_ms": boundary["d2h_starts_ms"],

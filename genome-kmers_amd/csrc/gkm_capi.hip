@@ -18,6 +18,30 @@
 
 namespace gkm {
 
+// ---------------------------------------------------------------------------------------------
+// options (gk_set_option): test and tuning overrides of the GKM_* knobs, process-wide
+// ---------------------------------------------------------------------------------------------
+namespace {
+std::mutex g_opt_mu;
+std::map<std::string, std::string> g_opts;
+// the operational knobs the environment may still set (transfer, packer, rank fallback, prefetch,
+// tracing); everything else needs gk_set_option
+const char *const kEnvKnobs[] = {"GKM_RANK_BALLOT", "GKM_PACK_IMPL",       "GKM_PACK_MIN",        "GKM_PACK_BLOCKS",
+                                 "GKM_XFER_THREADS", "GKM_XFER_HYBRID",    "GKM_XFER_NUMA",       "GKM_NO_RESIDENT_PACK",
+                                 "GKM_PREFETCH_REGIONS", "GKM_MSD_TRACE"};
+}  // namespace
+
+const char *opt(const char *name) {
+    {
+        std::lock_guard<std::mutex> lk(g_opt_mu);
+        auto it = g_opts.find(name);
+        if (it != g_opts.end()) return it->second.c_str();  // (stable until the option is set again)
+    }
+    for (const char *e : kEnvKnobs)
+        if (std::strcmp(e, name) == 0) return std::getenv(name);
+    return nullptr;
+}
+
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes) {
     if (bytes == 0) bytes = 16;
     if (*p && *cap >= bytes) return hipSuccess;
@@ -355,7 +379,7 @@ std::mutex g_rank_mu;
 std::map<int, RankState> g_rank;  // per device (hipGetDeviceCount-sized by use)
 
 bool env_force_ballot() {
-    const char *v = std::getenv("GKM_RANK_BALLOT");
+    const char *v = opt("GKM_RANK_BALLOT");
     return v && *v && std::strcmp(v, "0") != 0;
 }
 
@@ -508,7 +532,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
         uint64_t dollars = 0;
         // (A/B: GKM_EARLY_ELEMS=1 -- the k-mer buffers for every position allocated here, before the
         // transfer's staging slots, as the prefetch path does)
-        static const bool early = std::getenv("GKM_EARLY_ELEMS") != nullptr;
+        static const bool early = opt("GKM_EARLY_ELEMS") != nullptr;
         if (early)
             if (int rc = ensure_elems(c, len, 1)) return rc;
         // a sort hint (gk_sort_hint): the L0 pass of gk_sort(k) runs as the sequence lands
@@ -555,6 +579,20 @@ extern "C" int gk_copy_sequence(gk_ctx *c, uint8_t *dst, uint64_t len) {
 extern "C" int gk_alphabet_is_acgt(gk_ctx *c, int *is_acgt) {
     if (!c || !is_acgt) return GK_E_ARG;
     *is_acgt = c->acgt;
+    return GK_OK;
+}
+
+extern "C" int gk_resident_packed(gk_ctx *c, int *on) {
+    if (!c || !on) return GK_E_ARG;
+    *on = c->res_pk ? 1 : 0;
+    return GK_OK;
+}
+
+extern "C" int gk_set_option(const char *name, const char *value) {
+    if (!name || std::strncmp(name, "GKM_", 4) != 0) return GK_E_ARG;
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    if (value) g_opts[name] = value;
+    else g_opts.erase(name);
     return GK_OK;
 }
 
@@ -647,7 +685,7 @@ int gkm::ensure_keys(gk_ctx *c) {
     timer_begin(c, "reencode_keys", &slot);
     // multi-word keys of a sorted enumeration: through an enumeration-order table in the free key
     // buffer (one aligned row per k-mer instead of a ~70-byte window at a random position)
-    static const bool no_table = std::getenv("GKM_NO_KEY_TABLE") != nullptr;  // (A/B)
+    static const bool no_table = opt("GKM_NO_KEY_TABLE") != nullptr;  // (A/B)
     const KeySpec &ks = c->spec;
     // (the table path answers hipErrorNotSupported when it does not apply -- e.g. per-contig k-mer
     // counts that do not add up to n -- and the window gather, always correct, runs instead)
@@ -668,14 +706,14 @@ int gkm::ensure_keys(gk_ctx *c) {
 
 static int sort_direct(gk_ctx *c, const KeySpec &ks) {
     // fixed-length keys (k <= 64) from the enumerated starts: stable MSD in one-word phases (gkm_msd.hip)
-    static const bool force_lsd = std::getenv("GKM_SORT_LSD") != nullptr;
+    static const bool force_lsd = opt("GKM_SORT_LSD") != nullptr;
     const bool msd =
         c->enumerated && ks.symbols == ks.min_len && ks.symbols <= 64 && (ks.bits == 2 || ks.bits == 4) && !force_lsd;
     int rc = ensure_elems(c, c->n, msd ? 1 : ks.words);
     if (rc != GK_OK) return rc;
     if (msd) {
         // a mixed sba (N runs, IUPAC letters): ACGT-only k-mers on 2-bit keys, the rest apart
-        static const bool no_split = std::getenv("GKM_NO_SPLIT") != nullptr;
+        static const bool no_split = opt("GKM_NO_SPLIT") != nullptr;
         bool split = false;
         if (!c->acgt && !no_split) {
             rc = split_sort(c, ks, &split);
@@ -749,7 +787,7 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     // keys of the bounded sort: the same order as '$'-terminated 3-bit codes, 29 symbols instead of
     // 21, and every key bit carries information for the MSD levels; GKM_SEED3=1 keeps the 3-bit
     // seeds); other data as 16 symbols of 4 bits
-    static const bool seed3 = std::getenv("GKM_SEED3") != nullptr;
+    static const bool seed3 = opt("GKM_SEED3") != nullptr;
     KeySpec seed{};
     seed.bits = c->acgt ? (seed3 ? 3 : 2) : 4;
     seed.symbols = c->acgt ? (seed3 ? 21 : 29) : 16;
@@ -762,7 +800,7 @@ static int sort_doubling(gk_ctx *c, uint32_t M) {
     int slot;
     // large universes: the rounds sort only the groups still tied (MSD, msd_sort_groups); small ones
     // re-sort the whole array by rank pairs each round (LSD)
-    const bool by_groups = sort_keys_msd(c, n1, 1, 64) && std::getenv("GKM_DOUBLING_FULL") == nullptr;
+    const bool by_groups = sort_keys_msd(c, n1, 1, 64) && opt("GKM_DOUBLING_FULL") == nullptr;
     timer_begin(c, "encode", &slot);
     timer_units(c, slot, n1);
     const bool seed_hist = !sort_keys_msd(c, n1, 1, seed.total_bits);
@@ -1073,7 +1111,7 @@ extern "C" int gk_sort(gk_ctx *c, uint32_t max_kmer_len, uint32_t flags) {
     // when asked for (keys_stale)
     const bool reroute = direct && ks.words >= 2 && !canonical && max_kmer_len != c->min_k && c->acgt &&
                          (from_enum || 2 * c->n >= c->sba_len) && sort_keys_msd(c, c->n, 1, 64) &&
-                         std::getenv("GKM_BOUNDED_DIRECT") == nullptr;
+                         opt("GKM_BOUNDED_DIRECT") == nullptr;
     if (reroute) direct = false;
     rc = direct ? sort_direct(c, ks) : sort_doubling(c, max_kmer_len);
     if (rc != GK_OK) return rc;

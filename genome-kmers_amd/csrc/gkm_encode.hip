@@ -976,8 +976,8 @@ hipError_t launch_encode_positions(gk_ctx *c, const KeySpec &ks, uint64_t *keys,
                                c->seg, (uint32_t)c->nseg, k, keys, vals, hist);
         return hipGetLastError();
     }
-    static const bool no_roll = std::getenv("GKM_NO_ROLL_BOUNDED") != nullptr;  // (A/B)
-    static const bool no_roll_hist = std::getenv("GKM_NO_ROLL_HIST") != nullptr;  // (A/B)
+    static const bool no_roll = opt("GKM_NO_ROLL_BOUNDED") != nullptr;  // (A/B)
+    static const bool no_roll_hist = opt("GKM_NO_ROLL_HIST") != nullptr;  // (A/B)
     if (bounded && (hist == nullptr || (!no_roll_hist && k.digits <= 8)) && ks.words == 1 &&
         (ks.bits == 2 || ks.bits == 3) && ks.symbols <= 32 && ks.min_len >= 1 && !no_roll) {
         auto go = [&](auto fn) {
@@ -1046,7 +1046,7 @@ template <int W, int BITS, bool BOUNDED>
 static hipError_t gather_w(gk_ctx *c, const KS &k, const uint32_t *starts, uint64_t n, uint64_t *keys) {
     int grid = (int)std::min<uint64_t>((n + 255) / 256, 8192);
     if (grid < 1) grid = 1;
-    static const bool slow = std::getenv("GKM_GATHER_SLOW") != nullptr;  // A/B of the per-byte path
+    static const bool slow = opt("GKM_GATHER_SLOW") != nullptr;  // A/B of the per-byte path
     if constexpr (!BOUNDED && (BITS == 2 || BITS == 4))
         if (k.symbols <= 64 && !slow) {
             hipLaunchKernelGGL((encode_gather_fast_kernel<W, BITS>), dim3(grid), dim3(256), 0, c->stream, c->sba, k,
@@ -1075,7 +1075,7 @@ hipError_t launch_encode_table_gather(gk_ctx *c, const KeySpec &ks, const uint32
     if (e != hipSuccess) return e;
     KS k = pod(ks);
     // the position-indexed 2-bit rows when they fit the table buffer (k <= 63)
-    static const bool enum_rows = std::getenv("GKM_KEY_TABLE_ENUM") != nullptr;  // (A/B: the W-word rows)
+    static const bool enum_rows = opt("GKM_KEY_TABLE_ENUM") != nullptr;  // (A/B: the W-word rows)
     // (the rows, then the fix-up list of marker entries -- at most n -- in the same buffer)
     const uint64_t rows_bytes = 16 * (((uint64_t)c->sba_len + kRowPos - 1) / kRowPos * kRowPos);
     if (!enum_rows && ks.symbols <= 63 && rows_bytes + 4 * (n + 64) <= table_bytes) {

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void chunk_add_kernel(uint32_t *__restrict__ s
 // scan chunk: kScanChunk, or (test-only) a smaller multiple of 1024 so that the parity tests reach
 // the chunked branch, which otherwise runs only above 65536 tiles (about 268 M elements)
 static uint32_t scan_chunk() {
-    if (const char *e = std::getenv("GKM_TEST_SCAN_CHUNK")) {
+    if (const char *e = opt("GKM_TEST_SCAN_CHUNK")) {
         const int v = std::atoi(e);
         if (v >= 1024) return (uint32_t)(v / 1024 * 1024);
     }
@@ -680,7 +680,7 @@ static int group_front(gk_ctx *c, int is_sorted, int64_t kmer_len, const gk_filt
         // GKM_FILTER_PER_KMER=1 (A/B) evaluates every k-mer's window in sorted order
         // The per-position pass costs O(sba_len) whatever n is: used when the k-mers are a sizeable
         // share of the positions (a full enumeration), not for a small user-assigned start subset
-        static const bool per_kmer = std::getenv("GKM_FILTER_PER_KMER") != nullptr;
+        static const bool per_kmer = opt("GKM_FILTER_PER_KMER") != nullptr;
         if (kind != GK_FILTER_MASK && !per_kmer && c->sba_len > 0 && n * 8 >= c->sba_len) {
             uint64_t *words;
             GK_TRY_HIP(c, scratch(c, "filter_pos", (c->sba_len + 63) / 64 * 2, &words));

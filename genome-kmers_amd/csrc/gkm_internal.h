@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <utility>
@@ -192,6 +193,20 @@ struct gk_ctx {
 // launchers (implemented in gkm_encode.hip / gkm_sort.hip / gkm_group.hip)
 // ---------------------------------------------------------------------------------------------
 namespace gkm {
+
+// Test and tuning overrides (GKM_* names, gkm_capi.hip): the value gk_set_option gave `name`, else
+// -- for the few operational knobs listed in gkm_capi.hip (transfer threads and chunking, the
+// packer, the rank fallback, prefetch regions, tracing) -- the environment variable; nullptr when
+// unset.  Every other knob (alternative sort paths, test-only chunk sizes and forced formats) is
+// reachable only through gk_set_option, so no user environment can change the sort path silently.
+const char *opt(const char *name);
+// timing experiments that write wrong output on purpose (GKM_EXP_*, GKM_L0_PROF): only in builds
+// with -DGKM_EXPERIMENTS (tools/build_variant.sh), never in the product library
+#ifdef GKM_EXPERIMENTS
+inline const char *exp_opt(const char *name) { return std::getenv(name); }
+#else
+inline const char *exp_opt(const char *) { return nullptr; }
+#endif
 
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
 // pack2_kernel (gkm_msd.hip) over nwords words of 32 bytes from `from`

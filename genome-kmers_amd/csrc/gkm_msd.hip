@@ -375,8 +375,10 @@ __global__ __launch_bounds__(T) void msd0_count_kernel(L0Args a, Dig d0, uint32_
                 // (tiles with stops, or the sequence end).  Canonical keys: two windows and a
                 // reverse complement per position -- a loop, not unrolled, so the fast path above
                 // keeps its registers (unrolled over the 96 positions it took 256 VGPRs, spilled
-                // to scratch and ran the whole kernel at one wave per SIMD)
-                constexpr int UNR = CANON ? 1 : I;
+                // to scratch and ran the whole kernel at one wave per SIMD).  4-bit forward keys
+                // (every tile takes this path): unrolled by 4 (fully unrolled: 256 VGPRs + 206
+                // AGPRs, one wave per SIMD)
+                constexpr int UNR = CANON ? 1 : 4;
 #pragma unroll UNR
                 for (int i = 0; i < I; ++i) {
                     const uint32_t p = i * T + t;
@@ -1100,6 +1102,59 @@ __global__ __launch_bounds__(kRselW * 64) void msd0_rsel_kernel(L0Args a, Dig d0
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
     if (lane == 0 && g0 < ngroups) wave_cnt[gw] = (uint32_t)run;
+}
+
+// The same histogram from the packed copy, SWAR (round 6; forward 2-bit keys of <= 32 symbols, as
+// msd0_rsel_kernel): one 32-position group per lane, the digit of position j the top own_bits bits
+// of the 32-bit window at bit 2 j of the group's codes; positions that start no k-mer (a stop in
+// [j, j + S), or outside [lo, hi)) count into a second table (bins 4096 + digit) instead of being
+// branched around.  One 8,192-bin LDS table per workgroup, its waves walking the chunk together.
+__global__ __launch_bounds__(kRselW * 64) void own_hist_rsel_kernel(L0Args a, uint64_t gpb,
+                                                                     uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t s_hist[8192];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 8192; i += kRselW * 64) s_hist[i] = 0;
+    __syncthreads();
+    const uint64_t G0 = a.lo / 32, G1 = (a.hi + 31) / 32;
+    const uint64_t g0 = G0 + blockIdx.x * gpb, g1 = min(g0 + gpb, G1);
+    const int S = a.symbols, osh = 32 - a.own_bits;
+    for (uint64_t base = g0 + wave * 64; base < g1; base += kRselW * 64) {
+        const uint64_t g = base + lane;
+        const bool live = g < g1;
+        const uint64_t gc = live ? g : g1 - 1;
+        const uint64_t W0 = a.pk_code[gc], W1 = a.pk_code[gc + 1];
+        const uint32_t D0 = a.pk_dol[gc], D1 = a.pk_dol[gc + 1];
+        // valid positions, bit 31 - j = position j: inside [lo, hi) ...
+        const uint64_t P0 = gc * 32;
+        const uint64_t jb = a.lo > P0 ? a.lo - P0 : 0, je = a.hi - P0 < 32 ? a.hi - P0 : 32;
+        uint32_t m = live && jb < je ? (uint32_t)((0xFFFFFFFFull >> jb) & ~(0xFFFFFFFFull >> je)) : 0u;
+        // ... and no stop in [j, j + S)
+        if (__ballot((D0 | D1) != 0)) {
+            uint64_t sm = ((uint64_t)D0 << 32) | D1;
+            int len = 1;
+#pragma unroll
+            for (int s = 1; s < 32; s <<= 1) {
+                if (2 * len <= S) {
+                    sm |= sm << len;
+                    len *= 2;
+                }
+            }
+            if (len < S) sm |= sm << (S - len);
+            m &= ~(uint32_t)(sm >> 32);
+        }
+        const uint32_t x0 = (uint32_t)(W0 >> 32), x1 = (uint32_t)W0, x2 = (uint32_t)(W1 >> 32), inv = ~m;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int r = (2 * j) & 31;
+            const uint32_t hi = j < 16 ? x0 : x1, lo = j < 16 ? x1 : x2;
+            const uint32_t win = r ? __builtin_amdgcn_alignbit(hi, lo, 32 - r) : hi;
+            const uint32_t bin = (win >> osh) | (((inv >> (31 - j)) & 1u) << 12);
+            atomicAdd(&s_hist[bin], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (1 << a.own_bits); i += kRselW * 64)
+        if (s_hist[i]) atomicAdd(&ghist[i], s_hist[i]);
 }
 
 // Ownership-digit histogram of a key-range shard's position share: the top own_bits (<= 12) bits
@@ -2236,7 +2291,7 @@ __global__ __launch_bounds__(256) void stream_copy_kernel(uint64_t n, const uint
     }
 }
 
-static bool exp_wave_copy() { return std::getenv("GKM_EXP_WAVECOPY") != nullptr; }
+static bool exp_wave_copy() { return exp_opt("GKM_EXP_WAVECOPY") != nullptr; }
 
 // one round's lists, copied to device memory for the wave kernels
 __global__ void lists_store_kernel(Lists L, Lists *__restrict__ dst) { *dst = L; }
@@ -2634,28 +2689,28 @@ static unsigned cu_count(gk_ctx *c) {
 // tuning only (A/B runs): GKM_SELECT_2PASS=1 selects a key-range shard's k-mers by a count pass,
 // a scan and a store pass (the single chunked pass is the default)
 static bool select_two_pass() {
-    static const bool v = std::getenv("GKM_SELECT_2PASS") != nullptr;
+    static const bool v = opt("GKM_SELECT_2PASS") != nullptr;
     return v;
 }
 
 // tuning only (A/B runs): GKM_XCD_WALK_OFF=1 gives the wave kernels a grid that is not a multiple
 // of 8 (plain strided walk of the bucket list)
 static bool xcd_walk_off() {
-    static const bool v = std::getenv("GKM_XCD_WALK_OFF") != nullptr;
+    static const bool v = opt("GKM_XCD_WALK_OFF") != nullptr;
     return v;
 }
 
 // tuning only (A/B runs): GKM_NO_COMPACT=1 keeps 64-bit keys in every level's output
-static bool no_compact() { return std::getenv("GKM_NO_COMPACT") != nullptr; }  // (read per level: tests flip it)
+static bool no_compact() { return opt("GKM_NO_COMPACT") != nullptr; }  // (read per level: tests flip it)
 
 // timing only: GKM_L0_PROF=1 times the phases of the 2-bit L0 partition (tools)
 static bool l0_prof() {
-    static const bool v = std::getenv("GKM_L0_PROF") != nullptr;
+    static const bool v = exp_opt("GKM_L0_PROF") != nullptr;
     return v;
 }
 
 static bool use_pack() {
-    static const bool on = std::getenv("GKM_PACK") != nullptr;
+    static const bool on = opt("GKM_PACK") != nullptr;
     return on;
 }
 
@@ -2749,17 +2804,17 @@ struct MsdDriver {
     MsdDriver(gk_ctx *c_, const KeySpec &ks_) : c(c_), ks(ks_), B(ks_.total_bits) {
         cus = cu_count(c);
         pgrid = cus * 4;  // 4 workgroups per CU, one resident at a time (LDS); measured faster than 1
-        set_widths(std::getenv("GKM_LEVEL_BITS"));
+        set_widths(opt("GKM_LEVEL_BITS"));
         // test-only: small scan chunks so that parity tests reach the multi-chunk branches of the
         // column scan and tile tables (otherwise only buckets > 2.9 M keys have more than one chunk)
-        if (const char *e = std::getenv("GKM_TEST_CHUNK_TILES")) ctiles = (uint32_t)std::max(1, std::atoi(e));
+        if (const char *e = opt("GKM_TEST_CHUNK_TILES")) ctiles = (uint32_t)std::max(1, std::atoi(e));
     }
 
     // the whole sort of forward 2-bit one-word keys (msd_sort's phase 0): an 11-bit L0
     // (msd0_wide_kernel) when GKM_WIDE_L0=1 (A/B), so that 11 + 8 bits leave C3-sized buckets for
     // one block-local round
     void enable_wide_l0() {
-        const char *e = std::getenv("GKM_WIDE_L0");  // (read per sort: tests flip it)
+        const char *e = opt("GKM_WIDE_L0");  // (read per sort: tests flip it)
         const bool want = e && *e && std::strcmp(e, "0") != 0;
         if (want && ks.bits == 2 && !ks.canonical && !ks.acgt_only && B > kWideL0 + 8) wsched[0] = kWideL0;
     }
@@ -2864,12 +2919,8 @@ struct MsdDriver {
                    uint64_t sink, const NextDigits &ndg) {
         // the count pass streams the sequence: 256-thread workgroups, eight per CU, each holding a
         // whole tile of loads in flight (1,024-thread ones, two per CU, kept a quarter as many
-        // bytes in flight; GKM_L0_COUNT_1024=1 runs them for A/B)
-        static const bool count1024 = std::getenv("GKM_L0_COUNT_1024") != nullptr;
-        if (count && count1024)
-            hipLaunchKernelGGL((msd0_count_kernel<BITS, kP0T, kP0I, R, CANON>),
-                               dim3(std::min<unsigned>(nt0, cus * 2)), dim3(kP0T), 0, c->stream, a, d0, tile_hist, nt0);
-        else if (count) {
+        // bytes in flight and measured slower)
+        if (count) {
             static int per_cu = 0;  // resident workgroups (the grid is persistent)
             if (!per_cu &&
                 (hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -2892,6 +2943,9 @@ struct MsdDriver {
     template <bool ND>
     void l0_prof_launch(L0Args a, Dig d0, uint64_t *kout, uint32_t *vout, uint32_t nt, uint64_t sink,
                         const NextDigits &ndg) {
+#ifndef GKM_EXPERIMENTS
+        (void)a, (void)d0, (void)kout, (void)vout, (void)nt, (void)sink, (void)ndg;  // (timing builds only)
+#else
         unsigned long long *pr = nullptr;
         if (scratch(c, "l0_prof", 2 * kL0Phases, &pr) != hipSuccess) return;
         hipMemsetAsync(pr, 0, 16 * kL0Phases, c->stream);
@@ -2911,6 +2965,7 @@ struct MsdDriver {
                 std::fprintf(stderr, " %s %.1f%%", names[k], tot ? 100.0 * h[w * kL0Phases + k] / tot : 0.0);
             std::fprintf(stderr, " (ticks per tile: %.0f)\n", (double)tot / std::max<uint32_t>(nt, 1));
         }
+#endif
     }
 
     template <bool CANON>
@@ -3037,7 +3092,7 @@ struct MsdDriver {
         timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
-        const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !std::getenv("GKM_L0_NO_ND");  // (tuning knob)
+        const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !opt("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
         if (with_nd && p88) {  // the packed L0: digit bytes and low start bits in the free start buffer
             p88_place(vout == c->vals[0] ? 0 : 1);
@@ -3052,7 +3107,7 @@ struct MsdDriver {
         // timing experiments only (wrong output): GKM_EXP_L0=1 the scatter floor at 2^7 runs per tile,
         // =4 / 5 / 6 / 8 at 2^R runs (the same bytes in fewer or more write streams), =v at 2^7 runs
         // with 4-slot vector stores
-        static const char *exp_l0 = std::getenv("GKM_EXP_L0");
+        static const char *exp_l0 = exp_opt("GKM_EXP_L0");
         const int exp_r = exp_l0 ? (exp_l0[0] == '1' || exp_l0[0] == 'v' ? 7 : exp_l0[0] - '0') : 0;
         if (exp_r && with_nd && w0 == 7) {
             if (exp_r == 4)
@@ -3087,10 +3142,10 @@ struct MsdDriver {
     // L1 digit being the digit byte (8 bits).  GKM_NO_P88=1: off; GKM_TEST_P88=1 (tests): wherever
     // the bits fit.  C3: 62 - 7 = 55 bits after the L0, 47 of them in the pair (shi 17).
     bool p88_wanted() const {
-        if (std::getenv("GKM_NO_P88") || !allow_c79 || ks.bits != 2 || phase != 0 || no_compact()) return false;
+        if (opt("GKM_NO_P88") || !allow_c79 || ks.bits != 2 || phase != 0 || no_compact()) return false;
         const int w0 = width(0), w1 = width(1), w2 = width(2), rem = B - w0;
         if ((w0 != 7 && w0 != kGR) || w1 != 8 || rem - 8 < 33 || rem - 8 > 48) return false;
-        if (std::getenv("GKM_TEST_P88")) return true;
+        if (opt("GKM_TEST_P88")) return true;
         const uint64_t m1 = (n >> w0) >> w1;  // mean L1 sub-bucket
         const int rem2 = rem - w1 - w2;
         return m1 >= (uint64_t)kBlockMax && (m1 >> w2) < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 && w2 == 8 &&
@@ -3291,7 +3346,7 @@ struct MsdDriver {
         f.compact = phase == 0 && !f.nd_next && rem >= 9 && rem <= 40 && width(level + 1) == 8 && !no_compact();
         const uint64_t next_mean = nseg ? (elems / nseg >> width(level)) >> width(level + 1) : 0;
         const int rem2 = rem - width(level + 1);
-        const bool force = std::getenv("GKM_TEST_PAIRS") != nullptr;  // (read per level: tests flip it)
+        const bool force = opt("GKM_TEST_PAIRS") != nullptr;  // (read per level: tests flip it)
         f.pairs = allow_c79 && !c79_in && phase == 0 && !f.compact && rem >= 33 && rem <= 48 && !no_compact() &&
                   (force || (f.nd_next && next_mean < (uint64_t)kBlockMax && rem2 >= 9 && rem2 <= 40 &&
                              width(level + 2) == 8 && width(level + 1) == 8));
@@ -3680,25 +3735,25 @@ struct MsdDriver {
             wave(msd_wave_kernel<4, kWaveOcc4, true, kWaveR4>, msd_wave_kernel<4, kWaveOcc4, false, kWaveR4>);
             break;
         case 1:
-            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '2') {  // timing only
+            if (exp_wave_copy() && exp_opt("GKM_EXP_WAVECOPY")[0] == '2') {  // timing only
                 hipLaunchKernelGGL((msd_wave_copy2_kernel<8, kWaveOcc8>),
                                    grid((const void *)msd_wave_copy2_kernel<8, kWaveOcc8>, 64), dim3(64), 0,
                                    c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
                 break;
             }
-            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '3') {  // timing only
+            if (exp_wave_copy() && exp_opt("GKM_EXP_WAVECOPY")[0] == '3') {  // timing only
                 hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8, 1>),
                                    grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8, 1>, 64), dim3(64), 0,
                                    c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
                 break;
             }
-            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '4') {  // timing only
+            if (exp_wave_copy() && exp_opt("GKM_EXP_WAVECOPY")[0] == '4') {  // timing only
                 hipLaunchKernelGGL((msd_wave_copy_kernel<8, kWaveOcc8, 2>),
                                    grid((const void *)msd_wave_copy_kernel<8, kWaveOcc8, 2>, 64), dim3(64), 0,
                                    c->stream, lst, cnt, B, k0, v0, k1, v1, heads, ci.pref, ci.nd);
                 break;
             }
-            if (exp_wave_copy() && std::getenv("GKM_EXP_WAVECOPY")[0] == '5') {  // timing only
+            if (exp_wave_copy() && exp_opt("GKM_EXP_WAVECOPY")[0] == '5') {  // timing only
                 hipLaunchKernelGGL(stream_copy_kernel, dim3(cus * 8), dim3(256), 0, c->stream, n, k1, nd, k0, v0, heads);
                 break;
             }
@@ -3722,7 +3777,7 @@ struct MsdDriver {
         case 5: {
             // (A/B: GKM_BLOCK32_T512=1 -- 512 threads x 16 keys: half the per-wave counters to
             // zero and scan per bucket, half the waves)
-            static const bool t512 = std::getenv("GKM_BLOCK32_T512") != nullptr;
+            static const bool t512 = opt("GKM_BLOCK32_T512") != nullptr;
             if (t512)
                 hipLaunchKernelGGL((msd_local_kernel<kBT, 2 * kBI, kBR2>),
                                    grid((const void *)msd_local_kernel<kBT, 2 * kBI, kBR2>, kBT), dim3(kBT), 0,
@@ -3771,7 +3826,7 @@ struct MsdDriver {
                 uint64_t *k0 = c->keys[0], *k1 = c->keys[1];
                 uint32_t *v0 = c->vals[0], *v1 = c->vals[1];
                 const uint2 *lst = loc[k][g];
-                static const bool trace = std::getenv("GKM_MSD_TRACE") != nullptr;
+                static const bool trace = opt("GKM_MSD_TRACE") != nullptr;
                 hipEvent_t t0 = nullptr, t1 = nullptr;
                 if (trace) {
                     hipEventCreate(&t0);
@@ -3829,8 +3884,8 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
     // behind the next level -- packed pairs there and a compact level after them, which the 7-bit
     // L0's 49 and 41 bits do not allow (C5 219-221 -> 216.7-216.9 ms, profiles/r4/l08_ab.txt; the
     // same change made C4, 62-bit keys, 5 ms slower)
-    if (ks.bits == 2 && ks.canonical && d.B == 64 && !std::getenv("GKM_LEVEL_BITS")) d.wsched[0] = 8;
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    if (ks.bits == 2 && ks.canonical && d.B == 64 && !opt("GKM_LEVEL_BITS")) d.wsched[0] = 8;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);
@@ -3861,7 +3916,7 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
         int lev = 0;
         for (int l = 1; mean > (uint64_t)kBlockMax && l < kMaxLevels; ++l, ++lev) mean >>= d.width(l);
         l0b = 1 ^ (lev & 1);
-        if (const char *e = std::getenv("GKM_L0_BUF")) l0b = std::atoi(e) & 1;
+        if (const char *e = opt("GKM_L0_BUF")) l0b = std::atoi(e) & 1;
     }
     rc = d.run_l0(0, c->sba_len, c->keys[l0b], c->vals[l0b], c->elem_cap + 64, &found);
     if (rc != GK_OK) return rc;
@@ -3939,14 +3994,14 @@ int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     p->n = len - k + 1;
     p->w0 = d.width(0);
     p->w1 = d.width(1);
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     d.n = p->n;
     p->p88 = d.p88_wanted();
     p->p88_shi = 64 - (d.B - p->w0 - 8);
     const uint64_t nt = (p->n + kP0Tile - 1) / kP0Tile;
     // regions: GKM_PREFETCH_REGIONS (default 16); the last region's pass is what the transfer
     // cannot hide
-    const char *e = std::getenv("GKM_PREFETCH_REGIONS");
+    const char *e = opt("GKM_PREFETCH_REGIONS");
     const uint64_t want = std::max<uint64_t>(1, e && *e ? std::strtoull(e, nullptr, 10) : 16);
     // equal regions, but the last one's share is cut into halving pieces (1/2, 1/4, 1/8, 1/8 of it):
     // the pass of the last region to land is what the transfer cannot hide
@@ -4069,7 +4124,7 @@ int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
     MsdDriver d(c, ks);
     d.B = ks.total_bits;
     if (d.width(0) != c->pre_w0 || d.width(1) != c->pre_w1) return msd_sort(c, ks);  // (widths changed)
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     d.wkeys = 1;  // one-word keys end final in keys[0]
     c->msd_keys_final = true;
     timer_begin(c, "msd_total", &d.total_slot);
@@ -4134,7 +4189,7 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     d.wkeys = (nphase == 1 && (!ks.acgt_only || c->msd_force_keys)) ? 1 : 0;  // one-word keys end final in keys[0]
     c->msd_keys_final = d.wkeys != 0;
     d.wsched[0] = kGR;  // pieces are kGR-bit buckets
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
@@ -4165,11 +4220,11 @@ int msd_sort_keys(gk_ctx *c, int total_bits) {
     MsdDriver d(c, kk);
     d.B = total_bits;
     d.wkeys = 1;
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     // digit widths: as few global levels as leave buckets of <= ~400 keys for the one-wave
     // finishing classes (1e8 keys: 6 + 6 + 6 bits, buckets of ~380), the bits spread evenly; two
     // 8-bit levels left 1.5 K-key buckets to the block-local class, which ran 3.6 ms for 1e8 keys
-    if (!std::getenv("GKM_LEVEL_BITS")) {
+    if (!opt("GKM_LEVEL_BITS")) {
         int b = 0;
         while (b < total_bits && (c->n >> b) > 400) ++b;
         const int L = std::max(1, (b + 7) / 8);
@@ -4266,7 +4321,16 @@ int msd_l0_histogram(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uin
         const unsigned g = std::min<unsigned>(ntiles, d.cus * (unsigned)per_cu);                               \
         hipLaunchKernelGGL((own_hist_kernel<B_, C_>), dim3(g), dim3(kST), 0, c->stream, a, ntiles, gh);        \
     } while (0)
-    if (ks.bits == 2) { if (ks.canonical) GK_HIST(2, true); else GK_HIST(2, false); }
+    if (ks.bits == 2 && !ks.canonical && a.pk_code && ks.symbols <= 32 && a.hi > lo && !opt("GKM_RSEL_OFF")) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, own_hist_rsel_kernel, kRselW * 64, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        const uint64_t G = (a.hi + 31) / 32 - lo / 32;
+        const uint64_t gpb = std::max<uint64_t>((G + (uint64_t)d.cus * per_cu - 1) / ((uint64_t)d.cus * per_cu), 1);
+        hipLaunchKernelGGL(own_hist_rsel_kernel, dim3((unsigned)((G + gpb - 1) / gpb)), dim3(kRselW * 64), 0, c->stream,
+                           a, gpb, gh);
+    } else if (ks.bits == 2) { if (ks.canonical) GK_HIST(2, true); else GK_HIST(2, false); }
     else { if (ks.canonical) GK_HIST(4, true); else GK_HIST(4, false); }
 #undef GK_HIST
     GK_TRY_HIP(c, hipGetLastError());
@@ -4288,7 +4352,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     c->msd_keys_final = d.wkeys != 0;
     // packed-pair levels where the bits fit (the first level from the select's pieces has 55 bits
     // left at C3: its L1 writes the pairs)
-    d.allow_c79 = std::getenv("GKM_NO_PAIRS") == nullptr;
+    d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
     d.wsched[0] = range_width(ks);
     timer_begin(c, "msd_total", &d.total_slot);
     GK_TRY_HIP(c, msd_tables());
@@ -4329,7 +4393,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         const int ob = range_own_bits(ks);
         const uint32_t span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
         bool fused = ks.bits == 2 && span > 0 && (uint64_t)span * kFusedMaxRanks >= (1ull << ob);
-        if (const char *e = std::getenv("GKM_RANGE_FUSED")) fused = ks.bits == 2 && span > 0 && e[0] == '1';
+        if (const char *e = opt("GKM_RANGE_FUSED")) fused = ks.bits == 2 && span > 0 && e[0] == '1';
         if (fused) {
             c->n = 0;
             c->cur = 0;
@@ -4431,7 +4495,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
     } else if (ks.bits == 2 && !ks.canonical && a.pk_code && ks.symbols <= 32 && a.own_bits <= 32 &&
-               !std::getenv("GKM_RSEL_OFF")) {
+               !opt("GKM_RSEL_OFF")) {
         // the SWAR select over the packed copy: one region per wave (msd0_rsel_kernel)
         const uint64_t ngroups = (L + 31) / 32;
         int per_cu = 0;

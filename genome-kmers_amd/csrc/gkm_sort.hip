@@ -150,8 +150,8 @@ int radix_sort(gk_ctx *c, int words, int total_bits, bool hist_ready) {
 // radix_sort.  GKM_SORT_KEYS_LSD=1 keeps the LSD passes (A/B, tests).  Result in keys / vals[cur]
 // either way; the MSD path also writes the group heads.
 bool sort_keys_msd(const gk_ctx *c, uint64_t n, int words, int total_bits) {
-    const bool lsd = std::getenv("GKM_SORT_KEYS_LSD") != nullptr;  // (read per call: tests flip it)
-    const char *tm = std::getenv("GKM_MSD_KEYS_MIN");                // (tests: the MSD path at small n)
+    const bool lsd = opt("GKM_SORT_KEYS_LSD") != nullptr;  // (read per call: tests flip it)
+    const char *tm = opt("GKM_MSD_KEYS_MIN");                // (tests: the MSD path at small n)
     const uint64_t nmin = tm ? std::strtoull(tm, nullptr, 10) : kMsdKeysMin;
     if (!(words == 1 && n >= nmin && n <= 0xFFFFFFFFull && !lsd)) return false;
     // the MSD levels pay off where the LSD passes (one per 8 bits) outnumber them by two or more:

@@ -697,7 +697,7 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
     // written by the merge: expanded from the one-word 2-bit MSD keys (k <= 32), or read from a
     // 2-bit packed copy of the sequence (k <= 63, round 5; GKM_NO_MERGE_KEYS=1: the re-encode after
     // the sort instead) -- and needs no re-encode
-    const bool a_packed = k > 32 && k <= 63 && !std::getenv("GKM_NO_MERGE_KEYS");
+    const bool a_packed = k > 32 && k <= 63 && !opt("GKM_NO_MERGE_KEYS");
     const int WK = k <= 32 || a_packed ? ks.words : 0;
     int slot;
     // 1. class B starts: homopolymers (one letter k times) apart from the rest

@@ -225,7 +225,7 @@ bool have_avx2() {
 // (profiles/r5/xfer_probe.txt) -- the packing is bound by host memory, not by instructions
 int pack_impl() {
     static const int v = [] {
-        const char *e = std::getenv("GKM_PACK_IMPL");
+        const char *e = opt("GKM_PACK_IMPL");
         const bool a512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512f");
         if (e && !std::strcmp(e, "scalar")) return 0;
         if (e && !std::strcmp(e, "avx512")) return a512 ? 2 : have_avx2() ? 1 : 0;
@@ -324,7 +324,7 @@ static int buffer_node(const uint8_t *p, uint64_t len) {
 }
 
 uint64_t env_u64(const char *name, uint64_t dflt) {
-    const char *v = std::getenv(name);
+    const char *v = opt(name);
     return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
 }
 
@@ -431,7 +431,7 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     // complete: gk_set_sequence); the raw DMA of the hybrid mode skips the unpack, so not there.
     // GKM_NO_RESIDENT_PACK=1: none (the L0 passes pack the bytes per tile)
     c->res_pk = false;
-    const bool res = !hybrid && !std::getenv("GKM_NO_RESIDENT_PACK");
+    const bool res = !hybrid && !opt("GKM_NO_RESIDENT_PACK");
     const uint64_t res_words = c->sba_cap / 32;
     if (res) {
         GK_TRY_HIP(c, ensure(reinterpret_cast<void **>(&c->res_code), &c->res_code_cap, 8 * res_words + 64));

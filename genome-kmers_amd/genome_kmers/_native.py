@@ -56,7 +56,7 @@ EXPORTED = (
     "gk_shard_sort", "gk_fasta_open", "gk_fasta_fill", "gk_fasta_close", "gk_locate", "gk_copy_strands",
     "gk_shard_histogram", "gk_shard_sort_range", "gk_shard_class_b", "gk_shard_class_b_copy",
     "gk_shard_sort_range_b", "gk_rank_mode", "gk_reference_random_bases",
-    "gk_copy_sequence", "gk_sort_hint",
+    "gk_copy_sequence", "gk_sort_hint", "gk_resident_packed", "gk_set_option",
 )
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
@@ -148,6 +148,8 @@ _SIGS = {
     "gk_rank_mode": ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "gk_reference_random_bases": ([_U8P, ctypes.c_uint64, ctypes.c_uint32], ctypes.c_int),
     "gk_copy_sequence": ([_P, _U8P, ctypes.c_uint64], ctypes.c_int),
+    "gk_resident_packed": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "gk_set_option": ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
 }
 
 
@@ -252,6 +254,25 @@ def reference_random_bases(n: int, seed: int) -> np.ndarray:
     return out
 
 
+class _Options(dict):
+    """libgkm's test and tuning overrides (gk_set_option), as a dict: ``options["GKM_X"] = "1"`` sets
+    one, ``del options["GKM_X"]`` clears it -- so pytest's ``monkeypatch.setitem(options, ...)``
+    restores the library state after a test.  Process-wide; names start with GKM_."""
+
+    def __setitem__(self, name, value):
+        rc = load_library().gk_set_option(name.encode(), str(value).encode())
+        if rc != GK_OK:
+            raise GkError(rc, f"gk_set_option({name!r}) failed")
+        super().__setitem__(name, str(value))
+
+    def __delitem__(self, name):
+        super().__delitem__(name)  # (KeyError if unset, as a dict)
+        load_library().gk_set_option(name.encode(), None)
+
+
+options = _Options()
+
+
 def _ptr(arr: np.ndarray, ctype):
     return arr.ctypes.data_as(ctypes.POINTER(ctype))
 
@@ -316,6 +337,12 @@ class Engine:
     def is_acgt(self) -> bool:
         v = ctypes.c_int(0)
         self._check(self.lib.gk_alphabet_is_acgt(self.ctx, ctypes.byref(v)))
+        return bool(v.value)
+
+    def resident_packed(self) -> bool:
+        """The 2-bit packed copy of the sequence is resident (gk_resident_packed)."""
+        v = ctypes.c_int(0)
+        self._check(self.lib.gk_resident_packed(self.ctx, ctypes.byref(v)))
         return bool(v.value)
 
     def enumerate(self, min_kmer_len: int) -> int:

@@ -134,6 +134,17 @@ int gk_copy_sequence(gk_ctx *ctx, uint8_t *dst, uint64_t len);
 int gk_sort_hint(gk_ctx *ctx, uint32_t k, uint32_t flags);
 /* 1 if the loaded sba holds only {A,C,G,T,$} (2-bit keys), 0 otherwise (4-bit keys) */
 int gk_alphabet_is_acgt(gk_ctx *ctx, int *is_acgt);
+/* 1 if the last gk_set_sequence left the 2-bit packed copy of the sequence resident beside the sba
+ * (the packed transfer: the L0 passes of the sort read it, 0.375 B per position), else 0.  No
+ * reference counterpart (the reference has no transfer). */
+int gk_resident_packed(gk_ctx *ctx, int *on);
+/* Test and tuning overrides of the library's GKM_* knobs, process-wide (no reference counterpart):
+ * value NULL clears the override.  Only the operational knobs (GKM_XFER_THREADS, GKM_XFER_NUMA,
+ * GKM_XFER_HYBRID, GKM_PACK_IMPL, GKM_PACK_MIN, GKM_PACK_BLOCKS, GKM_NO_RESIDENT_PACK,
+ * GKM_RANK_BALLOT, GKM_PREFETCH_REGIONS, GKM_MSD_TRACE; and GKM_FASTA_CHUNK of the FASTA parser)
+ * are also read from the environment; every other knob -- alternative sort paths, forced formats,
+ * test-only chunk sizes -- is reachable only through this call. */
+int gk_set_option(const char *name, const char *value);
 
 /* ---- enumerate / sort ------------------------------------------------------------------------ */
 /* every start with >= min_kmer_len bases before '$' / end, contig by contig, ascending */

@@ -132,6 +132,163 @@ class SortedOutputCheck:
             del raw, fw
         return out
 
+    def _word_of(self, codes: torch.Tensor, m: int, reverse: bool, w: int):
+        """Key word w (most significant first) of positions 0..m-1, from the symbols that land in it."""
+        k, bits = self.k, self.bits
+        lw = self.words - 1 - w  # LSW-first index
+        out = torch.zeros(m, dtype=torch.int64, device=self.dev)
+        for t in range(k):
+            off = bits * (k - 1 - t)
+            q, sh = divmod(off, 64)
+            if q != lw and not (q + 1 == lw and sh + bits > 64):
+                continue
+            src = codes[k - 1 - t: k - 1 - t + m] if reverse else codes[t: t + m]
+            out |= (src << sh) if q == lw else (src >> (64 - sh))
+        return out
+
+    def _orientation(self, chunk: int):
+        """canonical: uint8[L], 1 where the reverse complement is the smaller k-mer (all words compared)."""
+        orient = torch.zeros(self.L, dtype=torch.uint8, device=self.dev)
+        lut = self.c2 if self.bits == 2 else self.c4
+        for a in range(0, self.L, chunk):
+            m = min(chunk, self.L - a)
+            raw = self.sba[a: a + m + self.k]
+            fw = self._words_of(lut[raw.long()], m, False)
+            rc = self._words_of(lut[self.comp[raw.long()].long()], m, True)
+            lt = torch.zeros(m, dtype=torch.bool, device=self.dev)
+            eq = torch.ones(m, dtype=torch.bool, device=self.dev)
+            for f, r in zip(fw, rc):
+                f, r = f ^ _MIN64, r ^ _MIN64
+                lt |= eq & (r < f)
+                eq &= r == f
+            orient[a: a + m] = lt.to(torch.uint8)
+            del raw, fw, rc
+        return orient
+
+    def position_word(self, w: int, orient, chunk: int = 1 << 27):
+        """int64[L]: key word w of the k-mer at every position (sign flipped: signed order = unsigned)."""
+        out = torch.empty(self.L, dtype=torch.int64, device=self.dev)
+        lut = self.c2 if self.bits == 2 else self.c4
+        for a in range(0, self.L, chunk):
+            m = min(chunk, self.L - a)
+            raw = self.sba[a: a + m + self.k]
+            f = self._word_of(lut[raw.long()], m, False, w)
+            if orient is not None:
+                r = self._word_of(lut[self.comp[raw.long()].long()], m, True, w)
+                f = torch.where(orient[a: a + m].bool(), r, f)
+            out[a: a + m] = f ^ _MIN64
+            del raw, f
+        return out
+
+    def check_sorted_wordwise(self, starts_ptr, n: int, keys_ptr=0, key_words: int = 0,
+                              max_counts_bin: int = 64, chunk: int = 1 << 27, unique=None):
+        """check_sorted for keys too large to recompute whole (C5: 4 words x 3.09 G k-mers = 99 GB
+        beside the product's own 99 GB): ONE word of every position's key at a time (25 GB), the
+        canonical orientation of every position decided first over all words (1 B each).  Each
+        word pass compares the product's word with the recomputed one and advances a per-pair
+        state (0 equal so far, 1 ordered, 2 out of order); a last pass over the sorted starts
+        checks tie order, group heads, multiplicities, the histogram and the permutation."""
+        ubuf = torch.empty(chunk + 1, dtype=torch.int32, device=self.dev)
+
+        def read_u32(src, a, m):
+            if isinstance(src, np.ndarray):
+                ubuf[:m] = torch.from_numpy(src[a:a + m].astype(np.uint32).view(np.int32))
+            else:
+                d2d(ubuf, src + 4 * a, 4 * m)
+            return ubuf[:m].to(torch.int64) & 0xFFFFFFFF
+
+        s32 = torch.empty(chunk + 1, dtype=torch.int32, device=self.dev)
+
+        def starts(a, m):
+            if isinstance(starts_ptr, np.ndarray):
+                s32[:m] = torch.from_numpy(starts_ptr[a:a + m].view(np.int32))
+            else:
+                d2d(s32, starts_ptr + 4 * a, 4 * m)
+            return s32[:m].to(torch.int64) & 0xFFFFFFFF
+
+        orient = self._orientation(chunk) if self.canonical else None
+        state = torch.zeros(max(n - 1, 0), dtype=torch.uint8, device=self.dev)  # pair (i - 1, i) at i - 1
+        kbuf = torch.empty(chunk, dtype=torch.int64, device=self.dev)
+        for w in range(self.words):
+            pw = self.position_word(w, orient, chunk)
+            prev = None
+            for a in range(0, n, chunk):
+                m = min(chunk, n - a)
+                g = pw[starts(a, m)]
+                if isinstance(keys_ptr, np.ndarray) or keys_ptr:
+                    assert key_words == self.words
+                    if isinstance(keys_ptr, np.ndarray):
+                        kbuf[:m] = torch.from_numpy(keys_ptr[a:a + m, w].view(np.int64))
+                    else:
+                        d2d(kbuf, keys_ptr + 8 * (w * n + a), 8 * m)
+                    assert torch.equal(kbuf[:m] ^ _MIN64, g), f"product key word {w} differs in [{a}, {a + m})"
+                gg = g if prev is None else torch.cat([prev.view(1), g])
+                lo = a if prev is None else a - 1  # first pair index covered
+                st = state[lo: lo + gg.numel() - 1]
+                und = st == 0
+                st[und & (gg[1:] < gg[:-1])] = 2
+                st[und & (gg[1:] > gg[:-1])] = 1
+                prev = g[-1].clone()
+                del g, gg
+            del pw
+            torch.cuda.empty_cache() if self.dev.type == "cuda" else None
+        assert not bool((state == 2).any().item()), "keys out of order"
+        del orient
+        valid = self.valid_starts()
+        n_valid = int(valid.sum().item())
+        assert n == n_valid, f"{n} sorted starts but {n_valid} enumerated k-mers"
+        seen = torch.zeros(self.L, dtype=torch.uint8, device=self.dev)
+        hist = torch.zeros(max_counts_bin + 1, dtype=torch.int64, device=self.dev)
+        prev_start, last_head, groups = None, 0, 0
+        for a in range(0, n, chunk):
+            m = min(chunk, n - a)
+            s = starts(a, m)
+            assert int(s.max().item()) < self.L, "start index out of range"
+            assert bool(valid[s].all().item()), "a sorted start is not an enumerated k-mer start"
+            seen[s] = 1
+            if prev_start is not None:
+                s = torch.cat([prev_start.view(1), s])
+            base = a if prev_start is None else a - 1
+            eq = state[base: base + s.numel() - 1] == 0
+            assert bool((s[1:][eq] > s[:-1][eq]).all().item()), f"equal k-mers not in start order near {a}"
+            heads = torch.nonzero(~eq).flatten() + base + 1
+            if prev_start is None:
+                heads = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.dev), heads])
+            if unique is not None and heads.numel():
+                assert groups + heads.numel() <= unique[2], "fewer unique k-mers in the product than groups"
+                got = read_u32(unique[0], groups, heads.numel())
+                assert torch.equal(got, heads), f"product group starts differ from the groups near {a}"
+            if heads.numel():
+                bounds = torch.cat([torch.tensor([last_head], device=self.dev), heads])
+                sizes = bounds[1:] - bounds[:-1]
+                if prev_start is None:
+                    sizes = sizes[1:]
+                hist += torch.bincount(sizes.clamp(max=max_counts_bin), minlength=max_counts_bin + 1)
+                groups += heads.numel()
+                last_head = int(heads[-1].item())
+            prev_start = s[-1].clone()
+        if n:
+            hist[min(n - last_head, max_counts_bin)] += 1
+        if unique is not None:
+            G = unique[2]
+            assert G == groups, f"product has {G} unique k-mers, the sorted order {groups} groups"
+            total = 0
+            for a in range(0, G, chunk):
+                m = min(chunk, G - a)
+                gs = read_u32(unique[0], a, m).clone()
+                nxt = read_u32(unique[0], a + 1, m - 1) if m > 1 else gs[:0]
+                end = n if a + m >= G else int(read_u32(unique[0], a + m, 1)[0].item())
+                want = torch.cat([nxt, torch.tensor([end], device=self.dev)]) - gs
+                cnt = read_u32(unique[1], a, m)
+                assert torch.equal(cnt, want), f"product multiplicities differ near unique k-mer {a}"
+                total += int(cnt.sum().item())
+            assert total == n, "multiplicities do not sum to the number of k-mers"
+        assert torch.equal(seen.bool(), valid), "sorted starts are not a permutation of the enumerated starts"
+        del seen, valid, state
+        if self.dev.type == "cuda":
+            torch.cuda.empty_cache()
+        return groups, hist.cpu().numpy()
+
     # ------------------------------------------------------------------------------------------
     def check_sorted(self, starts_ptr, n: int, keys_ptr=0, key_words: int = 0,
                      max_counts_bin: int = 64, chunk: int = 1 << 27, unique=None):

@@ -115,3 +115,45 @@ def test_rejects_wrong_product_key():
 def test_rejects_missing_kmer():
     sba, srt, keys, _ = _case()
     _expect_fail(sba, srt[:-1], keys[:-1], match="enumerated")
+
+
+# the word-wise checker (multi-word keys at full size, devcheck.check_sorted_wordwise)
+@pytest.mark.parametrize("k,canonical", [(9, False), (20, False), (9, True), (17, True), (33, True)])
+def test_wordwise_accepts_oracle_output(k, canonical):
+    sba, srt, keys, hist = _case(k, canonical)
+    chk = devcheck.SortedOutputCheck(sba, k, 4, canonical=canonical, device="cpu")
+    gs, cnt = _unique(keys)
+    groups, h = chk.check_sorted_wordwise(srt, len(srt), keys_ptr=keys, key_words=keys.shape[1], max_counts_bin=8,
+                                          chunk=257, unique=(gs, cnt, len(gs)))
+    np.testing.assert_array_equal(h, hist)
+    assert groups == int(hist.sum())
+
+
+@pytest.mark.parametrize("what", ["key", "order", "ties", "dup", "mult"])
+def test_wordwise_rejects(what):
+    sba, srt, keys, _ = _case(20, True)
+    gs, cnt = _unique(keys)
+    srt, keys, cnt = srt.copy(), keys.copy(), cnt.copy()
+    if what == "key":
+        keys[500, 1] ^= 1
+        match = "product key word 1"
+    elif what == "order":  # two distinct neighbours swapped, keys with them
+        i = int(np.flatnonzero((keys[1:] != keys[:-1]).any(axis=1))[10])
+        srt[[i, i + 1]] = srt[[i + 1, i]]
+        keys[[i, i + 1]] = keys[[i + 1, i]]
+        match = "out of order"
+    elif what == "ties":  # two members of a tie group swapped
+        i = int(np.flatnonzero((keys[1:] == keys[:-1]).all(axis=1))[0])
+        srt[[i, i + 1]] = srt[[i + 1, i]]
+        match = "start order"
+    elif what == "dup":
+        srt[10] = srt[11]
+        keys[10] = keys[11]
+        match = None
+    else:
+        cnt[int(np.argmax(cnt > 1))] -= 1
+        match = "multiplicities"
+    chk = devcheck.SortedOutputCheck(sba, 20, 4, canonical=True, device="cpu")
+    with pytest.raises(AssertionError, match=match):
+        chk.check_sorted_wordwise(srt, len(srt), keys_ptr=keys, key_words=keys.shape[1], max_counts_bin=8,
+                                  chunk=257, unique=(gs, cnt, len(gs)))

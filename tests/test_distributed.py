@@ -16,6 +16,7 @@ import pytest
 
 from genome_kmers import distributed as D
 from oracle import oracle
+from genome_kmers import _native  # noqa: E402 (gk_set_option overrides)
 
 K = 11
 
@@ -390,7 +391,7 @@ def test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical,
 @pytest.mark.parametrize("world,contigs,k,canonical,iupac", [
     (2, 1, 31, False, False), (3, 2, 31, True, False), (2, 2, 63, True, True), (8, 2, 31, True, True)])
 def test_gpu_key_ranges_packed_pairs(world, contigs, k, canonical, iupac, monkeypatch):
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
@@ -402,7 +403,7 @@ def test_gpu_key_ranges_packed_pairs(world, contigs, k, canonical, iupac, monkey
     (2, 1, 31, False, False), (8, 1, 31, False, False), (3, 2, 31, True, False), (2, 2, 63, True, True),
     (5, 3, 31, False, True), (3, 1, 5, False, True), (4, 2, 21, False, False)])
 def test_gpu_key_ranges_fused_select(fused, world, contigs, k, canonical, iupac, monkeypatch):
-    monkeypatch.setenv("GKM_RANGE_FUSED", fused)
+    monkeypatch.setitem(_native.options, "GKM_RANGE_FUSED", fused)
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
@@ -420,12 +421,49 @@ def test_gpu_key_ranges_resident_packed_copy(world, contigs, k, canonical, iupac
     test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 
+# Round 6: the ownership-digit histogram over the packed copy (own_hist_rsel_kernel) against numpy,
+# shares whose bounds are not multiples of 32, stops from contig ends and non-ACGT runs
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [3, 5, 16, 31, 32])
+@pytest.mark.parametrize("iupac", [False, True])
+def test_gpu_shard_histogram_packed_copy_vs_numpy(k, iupac, monkeypatch):
+    from genome_kmers import _native
+
+    monkeypatch.setenv("GKM_PACK_MIN", "0")
+    monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
+    sba, seg = _random_sba(150_000 + 13, 41 + k, 3)
+    if iupac:
+        sba[7000:7100] = ord("N")
+        sba[60_000:60_040:3] = ord("R")
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    ob = min(12, 2 * k)
+    code = np.full(256, 255, dtype=np.int64)
+    for i, ch in enumerate(b"ACGT"):
+        code[ch] = i
+    c = code[sba]
+    L = len(sba)
+    for lo, hi in [(0, L), (37, 70_001), (64, 64 + 32 * 7), (99_999, L), (5, 6)]:
+        h, bits = e.shard_histogram(lo, hi, k, canonical=False)
+        assert bits == ob
+        p = np.arange(lo, min(hi, L - k + 1))
+        ok = np.ones(len(p), dtype=bool)
+        dig = np.zeros(len(p), dtype=np.int64)
+        for j in range(k):
+            cj = c[p + j]
+            ok &= cj != 255
+            if 2 * j < ob:
+                dig = (dig << 2) | np.where(cj == 255, 0, cj)
+        want = np.bincount(dig[ok], minlength=1 << ob)
+        np.testing.assert_array_equal(np.asarray(h, dtype=np.int64)[:1 << ob], want)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,k,canonical", [(2, 31, False), (2, 63, True)])
 def test_gpu_key_ranges_fused_packed_l0(world, k, canonical, monkeypatch):
-    monkeypatch.setenv("GKM_RANGE_FUSED", "1")
-    monkeypatch.setenv("GKM_TEST_P88", "1")
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_RANGE_FUSED", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     test_gpu_key_ranges_concatenate_to_single_sort(world, 1, k, canonical, False)
 
 
@@ -433,7 +471,7 @@ def test_gpu_key_ranges_fused_packed_l0(world, k, canonical, monkeypatch):
 @pytest.mark.parametrize("world,contigs,k,canonical,iupac", [(2, 1, 31, False, False), (3, 2, 31, True, False),
                                                              (2, 2, 63, True, True)])
 def test_gpu_shards_packed_pairs(world, contigs, k, canonical, iupac, monkeypatch):
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     test_gpu_shards_concatenate_to_single_sort(world, contigs, k, canonical, iupac)
 
 

@@ -150,7 +150,7 @@ def test_canonical_split_complementary_homopolymer_runs(k):
 # the bits fit, so these sizes run the pair and compact levels with their canonical tie phases
 @pytest.mark.parametrize("k", [32, 63])
 def test_canonical_pair_levels_vs_oracle(k, monkeypatch):
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(500 + k)
     mixed = [("m" + name, s) for name, s in genome_with_rc_repeats(rng, [200_000], b"ACGT")]
     check_canonical(genome_with_rc_repeats(rng, [900_000, 300_000], b"AC") + mixed, k)

@@ -100,9 +100,11 @@ def _full_size_check(sba, seg, k, canonical, product_keys, expect_n):
         starts_ptr, n2 = eng.device_starts()
     assert n2 == n
     chk = devcheck.SortedOutputCheck(sba, k, bits, canonical=canonical)
-    groups, hist = chk.check_sorted(starts_ptr, n, keys_ptr=keys_ptr if product_keys else 0,
-                                    key_words=words if product_keys else 0, max_counts_bin=64,
-                                    unique=(gs_ptr, cnt_ptr, n_unique))
+    # multi-word keys (C5: 4 words, 99 GB of product keys): recomputed one word at a time
+    check = chk.check_sorted_wordwise if chk.words > 1 else chk.check_sorted
+    groups, hist = check(starts_ptr, n, keys_ptr=keys_ptr if product_keys else 0,
+                         key_words=words if product_keys else 0, max_counts_bin=64,
+                         unique=(gs_ptr, cnt_ptr, n_unique))
     del chk
     _log(f"device property checks done ({time.time() - t0:.1f} s): {groups:,} groups")
     assert groups == n_unique
@@ -124,17 +126,15 @@ def test_c3_full_size_properties():
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("k,canonical", [(31, False), (63, True)], ids=["c4_k31", "c5_k63_canonical"])
-def test_grch38_surrogate_full_size_properties(k, canonical, monkeypatch):
-    # canonical k = 63 checks the order without the product keys: since round 5 the split sort's
-    # merge writes them (4 words, 99 GB), which does not fit beside the property check's own
-    # per-position keys -- test_c5_full_size_merge_keys_windows checks them at this size
-    if canonical:
-        monkeypatch.setenv("GKM_NO_MERGE_KEYS", "1")
+def test_grch38_surrogate_full_size_properties(k, canonical):
+    # canonical k = 63: the product's own keys -- the 4-bit words the split sort's merge writes
+    # from the packed sequence (the default path) -- against keys recomputed one word at a time
+    # (devcheck.check_sorted_wordwise: 25 GB per word beside the product's 99 GB)
     _log("GRCh38 surrogate: generating")
     sba, seg = synthetic.grch38_surrogate(2)
     assert len(seg) == 24
     expect = sum(max(0, n - k + 1) for n in synthetic.GRCH38_LENGTHS)
-    _full_size_check(sba, seg, k, canonical, not canonical, expect)
+    _full_size_check(sba, seg, k, canonical, True, expect)
 
 
 @pytest.mark.timeout(900)
@@ -162,8 +162,8 @@ def test_c5_full_size_merge_keys_windows():
 # ---------------------------------------------------------------------------------------------
 @pytest.fixture
 def small_chunks(monkeypatch):
-    monkeypatch.setenv("GKM_TEST_CHUNK_TILES", "2")
-    monkeypatch.setenv("GKM_TEST_SCAN_CHUNK", "1024")
+    monkeypatch.setitem(_native.options, "GKM_TEST_CHUNK_TILES", "2")
+    monkeypatch.setitem(_native.options, "GKM_TEST_SCAN_CHUNK", "1024")
 
 
 def _oracle_sorted(seqs, k, canonical=False):
@@ -210,7 +210,7 @@ def test_small_chunks_acgt_vs_oracle(small_chunks, k):
 
 
 def test_small_chunks_low_entropy_levels_vs_oracle(small_chunks, monkeypatch):
-    monkeypatch.setenv("GKM_LEVEL_BITS", "8,6")
+    monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", "8,6")
     _oracle_sorted(_genome(6, [600_000], alphabet=b"AACGTT", rep_len=5000, copies=20), 31)
 
 

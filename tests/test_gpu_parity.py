@@ -197,7 +197,7 @@ def test_homopolymer_genome_all_ties():
 # (the random cases above finish after L0 / L1), at every level digit width (GKM_LEVEL_BITS)
 @pytest.mark.parametrize("level_bits", ["8", "8,7", "8,6", "8,7,8", "7,8,8"])
 def test_low_entropy_deep_levels_vs_oracle(level_bits, monkeypatch):
-    monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(11)
     # 1 bit per base: L0 leaves 16 buckets of ~150K, L1 ~10K each, L2 below the local limit
     oracle_check(random_genome(rng, [1_600_000, 800_000], alphabet=b"AC"), 31, 31)
@@ -205,7 +205,7 @@ def test_low_entropy_deep_levels_vs_oracle(level_bits, monkeypatch):
 
 @pytest.mark.parametrize("level_bits", ["8", "8,7,8", "7,8,8"])
 def test_sparse_variation_all_levels_vs_oracle(level_bits, monkeypatch):
-    monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(12)
     # mostly 'A' with a random base every ~40: huge equal-prefix buckets down to the last key bit,
     # exhausted (all-equal) buckets far above the local limit, long runs of ties
@@ -222,7 +222,7 @@ def test_sparse_variation_all_levels_vs_oracle(level_bits, monkeypatch):
 @pytest.mark.parametrize("compact", [True, False])
 def test_compact_level_with_big_sub_buckets_vs_oracle(compact, monkeypatch):
     if not compact:
-        monkeypatch.setenv("GKM_NO_COMPACT", "1")
+        monkeypatch.setitem(_native.options, "GKM_NO_COMPACT", "1")
     rng = np.random.default_rng(21)
     seqs = random_genome(rng, [1_500_000, 400_000])
     seqs.append(("periodic", "ACGT" * 30_000 + "AACCGGTT" * 8_000))
@@ -250,7 +250,7 @@ def test_compact_level_with_big_sub_buckets_vs_oracle(compact, monkeypatch):
 # buckets of ~490 k-mers for msd_wave_kernel<8> (C3's ~370 are in the same class), plus a periodic
 # run whose sub-buckets outgrow the rank-by-count limit and are re-listed with rebuilt keys.
 def test_compact_wave_class_vs_oracle(monkeypatch):
-    monkeypatch.setenv("GKM_LEVEL_BITS", "7,6,8")
+    monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", "7,6,8")
     rng = np.random.default_rng(22)
     seqs = random_genome(rng, [3_000_000, 1_000_000])
     seqs.append(("periodic", "ACGTTGCA" * 5_000 + "AACCGGTTAC" * 3_000))
@@ -745,7 +745,7 @@ def test_split_keys_with_homopolymers(k, canonical):
 # random, repeat-heavy and multi-contig inputs, bit-exact against the oracle
 @pytest.mark.parametrize("case", ["random", "block32", "repeats", "contigs", "homopolymer"])
 def test_wide_l0_vs_oracle(case, monkeypatch):
-    monkeypatch.setenv("GKM_WIDE_L0", "1")
+    monkeypatch.setitem(_native.options, "GKM_WIDE_L0", "1")
     rng = np.random.default_rng(21)
     if case == "random":
         seqs = random_genome(rng, [1_500_000])
@@ -763,7 +763,7 @@ def test_wide_l0_vs_oracle(case, monkeypatch):
 
 @pytest.mark.parametrize("k", [12, 20, 32])
 def test_wide_l0_k_sweep_vs_oracle(k, monkeypatch):
-    monkeypatch.setenv("GKM_WIDE_L0", "1")
+    monkeypatch.setitem(_native.options, "GKM_WIDE_L0", "1")
     rng = np.random.default_rng(k)
     oracle_check(random_genome(rng, [700_000, 12_345]), k, k)
 
@@ -776,8 +776,8 @@ def test_wide_l0_k_sweep_vs_oracle(k, monkeypatch):
 @pytest.mark.parametrize("level_bits,k", [("8", 31), ("8,6", 31), ("7,8,8", 31), ("7,8,8", 24), ("8", 32)])
 def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
     # k = 24 / 32: 33 / 48 key bits left behind the pair level (the two ends of its range)
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
-    monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(31)
     seqs = random_genome(rng, [1_600_000, 800_000], alphabet=b"AC")
     seqs.append(("mixed", random_genome(rng, [300_000])[0][1]))
@@ -798,11 +798,11 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
 @pytest.mark.parametrize("alphabet,k,level_bits", [(b"AC", 31, None), (b"AC", 24, None), (b"ACGT", 31, None),
                                                    (b"AC", 31, "8,8,8"), (b"AC", 32, "8,8,8")])
 def test_packed_l0_vs_oracle(pairs, alphabet, k, level_bits, monkeypatch):
-    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
     if pairs:
-        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+        monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     if level_bits:
-        monkeypatch.setenv("GKM_LEVEL_BITS", level_bits)
+        monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(k + len(alphabet))
     seqs = random_genome(rng, [1_600_000, 700_000], alphabet=alphabet)
     seqs.append(("mixed", random_genome(rng, [250_000])[0][1]))
@@ -814,9 +814,9 @@ def test_packed_l0_vs_oracle(pairs, alphabet, k, level_bits, monkeypatch):
 @pytest.mark.parametrize("pairs", [True, False], ids=["l1_pairs", "l1_plain"])
 def test_packed_l0_canonical_vs_oracle(pairs, monkeypatch):
     # canonical 64-bit first words (k = 32): the 8-bit L0 leaves 56 bits, 48 of them in the pair
-    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
     if pairs:
-        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+        monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(5)
     s = np.frombuffer(b"ACG", dtype=np.uint8)[rng.integers(0, 3, 1_500_000)].copy()
     seg = np.array([0], dtype=np.uint32)
@@ -838,9 +838,9 @@ def test_packed_l0_canonical_vs_oracle(pairs, monkeypatch):
 @pytest.mark.parametrize("k", [45, 63])
 @pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
 def test_packed_l0_multiword_vs_oracle(pairs, k, canonical, monkeypatch):
-    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
     if pairs:
-        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+        monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(k + 2 * canonical)
     s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 1_200_000)].copy()
     rep = s[1000:1000 + 4000].copy()
@@ -862,8 +862,8 @@ def test_packed_l0_multiword_vs_oracle(pairs, k, canonical, monkeypatch):
 @pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
 def test_packed_l0_split_vs_oracle(canonical, monkeypatch):
     # an N run: 4-bit keys, the ACGT-only class sorted on 2-bit keys (63 symbols: two words)
-    monkeypatch.setenv("GKM_TEST_P88", "1")
-    monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(11 + canonical)
     s = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, 900_000)].copy()
     s[300_000:300_500] = ord("N")
@@ -912,7 +912,7 @@ def test_split_merge_packed_keys_vs_oracle(k, canonical, transfer, monkeypatch):
     keys = oracle.canonical_keys(s, want, k, 4) if canonical else oracle.encode_keys(s, want, *oracle.key_spec(False, k, k))
     np.testing.assert_array_equal(got, keys.reshape(got.shape))
     # the same keys through the re-encode after the sort
-    monkeypatch.setenv("GKM_NO_MERGE_KEYS", "1")
+    monkeypatch.setitem(_native.options, "GKM_NO_MERGE_KEYS", "1")
     e2 = _native.Engine()
     e2.set_sequence(s, seg)
     e2.enumerate(k)
@@ -932,9 +932,9 @@ def test_split_merge_packed_keys_vs_oracle(k, canonical, transfer, monkeypatch):
                                                   (b"ACGT", 3, 64)])
 def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
     if path == "msd":
-        monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")
+        monkeypatch.setitem(_native.options, "GKM_MSD_KEYS_MIN", "2048")
     else:
-        monkeypatch.setenv("GKM_SORT_KEYS_LSD", "1")
+        monkeypatch.setitem(_native.options, "GKM_SORT_KEYS_LSD", "1")
     rng = np.random.default_rng(min_k * 7 + (max_k or 0))
     rep = rng.choice(np.frombuffer(alphabet, dtype=np.uint8), 3000).astype(np.uint8)
     oracle_check(random_genome(rng, [60_000, 20_000, 7_000, 40], alphabet=alphabet, repeat=rep, copies=3),
@@ -946,9 +946,9 @@ def test_sort_keys_paths_vs_oracle(path, alphabet, min_k, max_k, monkeypatch):
 @pytest.mark.parametrize("path", ["msd", "lsd"])
 def test_doubling_user_starts_vs_oracle(path, monkeypatch):
     if path == "msd":
-        monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2048")
+        monkeypatch.setitem(_native.options, "GKM_MSD_KEYS_MIN", "2048")
     else:
-        monkeypatch.setenv("GKM_SORT_KEYS_LSD", "1")
+        monkeypatch.setitem(_native.options, "GKM_SORT_KEYS_LSD", "1")
     rng = np.random.default_rng(77)
     rep = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 2000).astype(np.uint8)
     seqs = random_genome(rng, [30_000, 9_000, 300], repeat=rep, copies=4)
@@ -966,7 +966,7 @@ def test_doubling_user_starts_vs_oracle(path, monkeypatch):
 # cover most of them (round-4 advice); the encode stage then sees the user's starts, not every position
 @pytest.mark.parametrize("max_k", [30, 41, 64])
 def test_bounded_user_subset_keeps_direct_keys(max_k, monkeypatch):
-    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    monkeypatch.setitem(_native.options, "GKM_MSD_KEYS_MIN", "2")
     rng = np.random.default_rng(max_k)
     sc = SequenceCollection(sequence_list=random_genome(rng, [40_000, 9_000, 300]))
     km = gk.Kmers(sc, min_kmer_len=20, max_kmer_len=max_k)
@@ -989,7 +989,7 @@ def test_bounded_user_subset_keeps_direct_keys(max_k, monkeypatch):
 # from the sorted starts when asked for, as on small arrays (round-4 advice)
 @pytest.mark.parametrize("case", [c for c in CASES if c["max_kmer_len"] is not None], ids=lambda c: c["name"])
 def test_encoded_keys_on_large_array_routes(case, monkeypatch):
-    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    monkeypatch.setitem(_native.options, "GKM_MSD_KEYS_MIN", "2")
     km, a = make(case)
     km.sort()
     words, bits, symbols = km._engine.key_layout()
@@ -1006,7 +1006,7 @@ def test_encoded_keys_on_large_array_routes(case, monkeypatch):
 # answers
 @pytest.mark.parametrize("case", CASES, ids=CASE_IDS)
 def test_golden_on_large_array_routes(case, monkeypatch):
-    monkeypatch.setenv("GKM_MSD_KEYS_MIN", "2")
+    monkeypatch.setitem(_native.options, "GKM_MSD_KEYS_MIN", "2")
     km, a = make(case)
     km.sort()
     np.testing.assert_array_equal(km.kmer_sba_start_indices, a["starts_stable"])

@@ -87,9 +87,9 @@ def test_prefetched_sort_matches_plain(k, L, regions, monkeypatch):
 def test_prefetch_packed_l0(mode, alphabet, monkeypatch):
     # the regions write the packed L0 form (GKM_TEST_P88=1); the first level from their pieces reads
     # it when it writes packed pairs (GKM_TEST_PAIRS=1), else the pieces are expanded first
-    monkeypatch.setenv("GKM_TEST_P88", "1")
+    monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
     if mode == "p88_pairs":
-        monkeypatch.setenv("GKM_TEST_PAIRS", "1")
+        monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
     rng = np.random.default_rng(len(alphabet) + len(mode))
     L = 900_000
     sba = np.frombuffer(alphabet, dtype=np.uint8)[rng.integers(0, len(alphabet), L)].copy()
@@ -119,14 +119,14 @@ def test_prefetch_multi_chunk_region_scans(chunk_tiles, monkeypatch):
     # regions of 5 tiles in column-scan chunks of 1-3 tiles, the last region shorter (fewer chunks
     # than the others: its tables sit at the same stride) -- the multi-chunk scan branch that only
     # full-size inputs reach with the default 256-tile chunks
-    monkeypatch.setenv("GKM_TEST_CHUNK_TILES", chunk_tiles)
+    monkeypatch.setitem(_native.options, "GKM_TEST_CHUNK_TILES", chunk_tiles)
     rng = np.random.default_rng(int(chunk_tiles))
     L = 32 * 24576 + 1234
     sba = genome(rng, L, repeat=2000, copies=7)
     seg = np.zeros(1, dtype=np.uint32)
     _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=7)
     assert "prefetch_l0" in rep and "msd_pass_l0" not in rep
-    monkeypatch.delenv("GKM_TEST_CHUNK_TILES")
+    monkeypatch.delitem(_native.options, "GKM_TEST_CHUNK_TILES")
     _, want, _ = run(sba, seg, 31, monkeypatch, False)
     same(got, want)
     np.testing.assert_array_equal(got[0], oracle.quicksort(sba, np.arange(L - 30, dtype=np.uint32), 31, 31,

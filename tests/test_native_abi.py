@@ -32,3 +32,15 @@ def test_engine_fails_loudly_without_gpu():
         pytest.skip("a GPU is visible")
     with pytest.raises(_native.GkError, match="no CPU fallback"):
         _native.Engine()
+
+
+def test_options_are_explicit_overrides():
+    """gk_set_option: GKM_* test/tuning overrides set and cleared through _native.options; other
+    names are refused (no compute call: runs without a GPU)."""
+    lib = _native.load_library()
+    assert lib.gk_set_option(b"NOT_A_KNOB", b"1") == _native.GK_E_ARG
+    _native.options["GKM_TEST_PAIRS"] = "1"
+    assert _native.options.get("GKM_TEST_PAIRS") == "1"
+    del _native.options["GKM_TEST_PAIRS"]
+    assert "GKM_TEST_PAIRS" not in _native.options
+    assert lib.gk_set_option(b"GKM_TEST_PAIRS", None) == _native.GK_OK  # clearing an unset one is fine

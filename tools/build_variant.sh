@@ -1,5 +1,6 @@
 # Build a compile-time variant of libgkm.so for A/B runs (tuning only):
 #   bash tools/build_variant.sh NAME "-DGKM_X=1 ..."   -> abl/libgkm_NAME.so
+#   experiments that write wrong output on purpose (GKM_EXP_*, GKM_L0_PROF) need -DGKM_EXPERIMENTS
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 N=$1; F=$2

@@ -8,7 +8,7 @@
 #                         unprofiled bench, the SAME command under rocprofv3 --kernel-trace --stats,
 #                         --pmc passes (SQ mix, FETCH_SIZE, WRITE_SIZE: one pass each), rocm-smi after,
 #                         and tools/trace_summary.py (steady-state kernel times vs the bench's stages)
-#     ab=CFG              interleaved A/B over $LIBS ("abl/x.so intree env:VAR=1 ..."), $REPS rounds
+#     ab=CFG              interleaved A/B over $LIBS ("abl/x.so intree env:VAR=1 opt:GKM_X=1 ..."), $REPS rounds
 #     emu=CFG             tools/range_emulate.py (multi-GPU per-rank emulation) -> emu_CFG.json
 #     cmd=SHELL           any other command (its own 600 s limit)
 set -o pipefail
@@ -75,14 +75,15 @@ for task in "$@"; do
       for rep in $(seq 1 ${REPS:-2}); do
         for lib in ${LIBS}; do
           unset GKM_LIB
-          envs=()
+          envs=(); extra=()
           case "$lib" in
             intree) ;;
             env:*) envs=("${lib#env:}") ;;
+            opt:*) envs=(GKM_AB_OPT=1); extra=(--opt "${lib#opt:}") ;;
             *) export GKM_LIB=$lib ;;
           esac
           timeout -k 10 300 env "${envs[@]}" python bench.py --config "$arg" --steps ${AB_STEPS:-5} --warmup 1 \
-            --no-cpu-baseline --no-boundary > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; die ab; }
+            --no-cpu-baseline --no-boundary "${extra[@]}" > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; die ab; }
           python3 tools/line_brief.py gpurun_out/ab.json --label "$lib" | tee -a gpurun_out/ab_$arg.txt
         done
       done ;;

@@ -1104,16 +1104,232 @@ __global__ __launch_bounds__(kRselW * 64) void msd0_rsel_kernel(L0Args a, Dig d0
     if (lane == 0 && g0 < ngroups) wave_cnt[gw] = (uint32_t)run;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Key-range ranks' L0, compaction first (round 6): the fused select of msd0_pipe_kernel<..., OWN>
+// ranked, staged and keyed EVERY position of the sequence to store the ~1/N it keeps (7.7 ms over
+// C3 at any N).  These two kernels test the positions with the SWAR range test of msd0_rsel_kernel
+// (forward 2-bit keys of <= 32 symbols, packed copy), compact the kept ones per tile in position
+// order, and only then rank, stage and store them -- the L0 partition of the rank's k-mers
+// straight from the sequence: no select pass, no 13-byte round trip, no level from pieces.
+// Tiles are the L0's (kP0Tile = 768 groups of 32 positions, l0_count's tables); threads < 768
+// take one group each in the test, the kept elements then spread over all 1,024 threads in the
+// partition's wave-major item order (stable: items of a wave in order, waves in order).
+// ---------------------------------------------------------------------------------------------
+constexpr int kOwnT = 1024, kOwnG = kP0Tile / 32;  // threads, groups per tile
+constexpr int kOwnI = kP0Tile / kOwnT;             // items per thread (capacity: every position)
+static_assert(kOwnG <= kOwnT && kOwnI * kOwnT == kP0Tile, "one group per thread; every position fits");
+
+struct OwnTest {
+    uint32_t lo_w, spm1_w;  // the range shifted to the top of a 32-bit window (msd0_rsel_kernel)
+};
+
+// keep mask of the group at position P (bit 31 - j = position P + j): in [a.lo, a.hi), no stop in
+// [j, j + S), ownership digit in range; W0 / W1 / D0 / D1 the group's and the next group's words.
+// Wave-uniform call (a ballot inside).
+__device__ __forceinline__ uint32_t own_keep(const L0Args &a, OwnTest ot, uint64_t P, uint64_t W0, uint64_t W1,
+                                             uint32_t D0, uint32_t D1, bool live) {
+    const uint32_t x0 = (uint32_t)(W0 >> 32), x1 = (uint32_t)W0, x2 = (uint32_t)(W1 >> 32);
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int r = (2 * j) & 31;
+        const uint32_t hi = j < 16 ? x0 : x1, lo = j < 16 ? x1 : x2;
+        const uint32_t win = r ? __builtin_amdgcn_alignbit(hi, lo, 32 - r) : hi;
+        m = (m << 1) | (uint32_t)(win - ot.lo_w <= ot.spm1_w);
+    }
+    if (__ballot(live && (D0 | D1) != 0)) {
+        uint64_t sm = ((uint64_t)D0 << 32) | D1;
+        int len = 1;
+#pragma unroll
+        for (int s = 1; s < 32; s <<= 1) {
+            if (2 * len <= a.symbols) {
+                sm |= sm << len;
+                len *= 2;
+            }
+        }
+        if (len < a.symbols) sm |= sm << (a.symbols - len);
+        m &= ~(uint32_t)(sm >> 32);
+    }
+    const uint64_t jb = a.lo > P ? a.lo - P : 0, je = a.hi > P ? min(a.hi - P, (uint64_t)32) : 0;
+    m &= jb < je ? (uint32_t)((0xFFFFFFFFull >> jb) & ~(0xFFFFFFFFull >> je)) : 0u;
+    return live ? m : 0u;
+}
+
+// the B-bit key of position j of a group (j in [0, 32))
+__device__ __forceinline__ uint64_t group_key(uint64_t W0, uint64_t W1, uint32_t j, int B) {
+    const uint32_t s = 2 * j;
+    const uint64_t T = s ? (W0 << s) | (W1 >> (64 - s)) : W0;
+    return T >> (64 - B);
+}
+
+// count pass: per-tile histograms of the kept k-mers' L0 digits (R bits)
+template <int R>
+__global__ __launch_bounds__(kOwnT) void own_count_kernel(L0Args a, Dig d0, OwnTest ot, uint32_t *__restrict__ tile_hist,
+                                                           uint32_t ntiles) {
+    constexpr int RADIX = 1 << R, NC = 4;
+    __shared__ uint32_t s_hist[RADIX * NC];
+    const int t = threadIdx.x;
+    const uint64_t g_end = (a.hi + 31) / 32;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = t; i < RADIX * NC; i += kOwnT) s_hist[i] = 0;
+        __syncthreads();
+        if (t < kOwnG) {
+            const uint64_t g = a.lo / 32 + (uint64_t)tile * kOwnG + t;
+            const bool live = g < g_end;
+            const uint64_t gc = live ? g : g_end - 1;
+            const uint64_t W0 = a.pk_code[gc], W1 = a.pk_code[gc + 1];
+            uint32_t m = own_keep(a, ot, gc * 32, W0, W1, a.pk_dol[gc], a.pk_dol[gc + 1], live);
+            while (m) {
+                const uint32_t j = __clz(m);
+                m ^= 0x80000000u >> j;
+                atomicAdd(&s_hist[dg_of(group_key(W0, W1, j, a.total_bits), d0) * NC + (t & (NC - 1))], 1u);
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < RADIX; i += kOwnT) {
+            uint32_t h = 0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) h += s_hist[i * NC + c];
+            tile_hist[(uint64_t)tile * RADIX + i] = h;
+        }
+    }
+}
+
+// partition pass: the kept k-mers of each tile compacted, ranked by their L0 digit (R bits), staged
+// and stored at the tile's digit offsets -- (key, start, next digit) or the packed L0 form (P88)
+template <int R, bool P88>
+__global__ __launch_bounds__(kOwnT) void own_part_kernel(L0Args a, Dig d0, OwnTest ot,
+                                                          const uint32_t *__restrict__ tile_off,
+                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                          uint32_t ntiles, NextDigits nd) {
+    constexpr int RADIX = 1 << R, NW = kOwnT / 64;
+    __shared__ uint16_t s_pos[kP0Tile];             // kept positions in order, then in digit order
+    __shared__ uint64_t s_code[kOwnG + 1];
+    __shared__ uint32_t s_wc[NW * RADIX];
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint32_t s_start[RADIX + 1];
+    __shared__ uint32_t s_toff[RADIX];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t g_end = (a.hi + 31) / 32;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t g0 = a.lo / 32 + (uint64_t)tile * kOwnG;
+        if (t < RADIX) s_toff[t] = tile_off[(uint64_t)tile * RADIX + t];
+        uint32_t *wc = s_wc + wave * RADIX;
+#pragma unroll
+        for (int u = 0; u < (RADIX + 63) / 64; ++u)
+            if (u * 64 + lane < RADIX) wc[u * 64 + lane] = 0;
+        // 1. test: keep mask and count of this thread's group; its code words into LDS
+        uint32_t m = 0;
+        if (t < kOwnG) {
+            const uint64_t g = g0 + t;
+            const bool live = g < g_end;
+            const uint64_t gc = live ? g : g_end - 1;
+            const uint64_t W0 = a.pk_code[gc], W1 = a.pk_code[gc + 1];
+            m = own_keep(a, ot, gc * 32, W0, W1, a.pk_dol[gc], a.pk_dol[gc + 1], live);
+            s_code[t] = W0;
+            if (t == kOwnG - 1) s_code[kOwnG] = W1;
+        }
+        const uint32_t cnt = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan(cnt);
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t pre = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t v = s_wsum[w];
+            pre += w < wave ? v : 0u;
+            total += v;
+        }
+        // 2. compaction: the kept positions (tile-relative) in position order
+        {
+            uint32_t j = pre + incl - cnt;
+            while (m) {
+                const uint32_t b = __clz(m);
+                m ^= 0x80000000u >> b;
+                s_pos[j++] = (uint16_t)(t * 32 + b);
+            }
+        }
+        __syncthreads();
+        // 3. rank: element e = wave * kOwnI * 64 + i * 64 + lane (wave-major, position order)
+        uint32_t dr[kOwnI];
+        uint16_t pp[kOwnI];
+        const uint32_t e0 = wave * (kOwnI * 64);
+#pragma unroll
+        for (int i = 0; i < kOwnI; ++i) {
+            dr[i] = ~0u;
+            pp[i] = 0;
+            if (e0 + i * 64 < total) {  // (wave-uniform)
+                const uint32_t e = e0 + i * 64 + lane;
+                const bool valid = e < total;
+                const uint32_t p = s_pos[valid ? e : 0];
+                const uint32_t dig = dg_of(l0_key<2>(s_code, p, a.total_bits), d0);
+                const uint32_t rk = rank_atomic(wc, dig, valid);
+                dr[i] = valid ? dig | (rk << 8) : ~0u;
+                pp[i] = (uint16_t)p;
+            }
+        }
+        __syncthreads();  // ranks final; every compacted position read
+        // 4. digit starts: per-digit totals over the waves, their scan
+        uint32_t dtot = 0, dincl = 0;
+        if (t < RADIX) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t v = s_wc[w * RADIX + t];
+                s_wc[w * RADIX + t] = dtot;
+                dtot += v;
+            }
+            dincl = wave_incl_scan(dtot);
+            if (lane == 63) s_wsum[wave] = dincl;
+        }
+        __syncthreads();
+        if (t < RADIX) {
+            uint32_t p2 = 0;
+            for (int w = 0; w < wave; ++w) p2 += s_wsum[w];
+            const uint32_t st = p2 + dincl - dtot;
+            s_start[t] = st;
+            s_toff[t] -= st;
+        }
+        __syncthreads();
+        // 5. stage in digit order (over the compacted positions: all were read in 3)
+#pragma unroll
+        for (int i = 0; i < kOwnI; ++i) {
+            if (dr[i] != ~0u) {
+                const uint32_t dg = dr[i] & 0xFFu;
+                s_pos[s_start[dg] + wc[dg] + (dr[i] >> 8)] = pp[i];
+            }
+        }
+        __syncthreads();
+        // 6. store: runs of each digit at the tile's offsets
+        const uint64_t P0 = g0 * 32;
+        for (uint32_t s = t; s < total; s += kOwnT) {
+            const uint32_t p = s_pos[s];
+            const uint64_t key = l0_key<2>(s_code, p, a.total_bits);
+            const uint64_t o = (uint64_t)s_toff[dg_of(key, d0)] + s;
+            const uint32_t st = (uint32_t)(P0 + p);
+            if (P88) {
+                const int shi = nd.pshi;
+                kout[o] = (key << shi) | (st >> (32 - shi));
+                nd.out16[o] = (uint16_t)(st & ((1u << (32 - shi)) - 1));
+            } else {
+                kout[o] = key;
+                vout[o] = st;
+            }
+            nd.out[o] = (uint8_t)dg_of(key, nd.d);
+        }
+        __syncthreads();  // the staging and the codes are read before the next tile's
+    }
+}
+
 // The same histogram from the packed copy, SWAR (round 6; forward 2-bit keys of <= 32 symbols, as
 // msd0_rsel_kernel): one 32-position group per lane, the digit of position j the top own_bits bits
 // of the 32-bit window at bit 2 j of the group's codes; positions that start no k-mer (a stop in
-// [j, j + S), or outside [lo, hi)) count into a second table (bins 4096 + digit) instead of being
-// branched around.  One 8,192-bin LDS table per workgroup, its waves walking the chunk together.
+// [j, j + S), or outside [lo, hi)) count into junk bins (4096 + 64 j + lane: conflict-free) instead
+// of being branched around.  One LDS table per workgroup, its waves walking the chunk together.
 __global__ __launch_bounds__(kRselW * 64) void own_hist_rsel_kernel(L0Args a, uint64_t gpb,
                                                                      uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t s_hist[8192];
+    __shared__ uint32_t s_hist[4096 + 64 * 32];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 8192; i += kRselW * 64) s_hist[i] = 0;
+    for (int i = threadIdx.x; i < 4096 + 64 * 32; i += kRselW * 64) s_hist[i] = 0;
     __syncthreads();
     const uint64_t G0 = a.lo / 32, G1 = (a.hi + 31) / 32;
     const uint64_t g0 = G0 + blockIdx.x * gpb, g1 = min(g0 + gpb, G1);
@@ -1148,7 +1364,9 @@ __global__ __launch_bounds__(kRselW * 64) void own_hist_rsel_kernel(L0Args a, ui
             const int r = (2 * j) & 31;
             const uint32_t hi = j < 16 ? x0 : x1, lo = j < 16 ? x1 : x2;
             const uint32_t win = r ? __builtin_amdgcn_alignbit(hi, lo, 32 - r) : hi;
-            const uint32_t bin = (win >> osh) | (((inv >> (31 - j)) & 1u) << 12);
+            // (an invalid position's bin depends on the lane only: the N runs of a mixed sba would
+            // otherwise send a whole wave to one address, serialising the atomic)
+            const uint32_t bin = ((inv >> (31 - j)) & 1u) ? 4096u + 64u * j + (uint32_t)lane : win >> osh;
             atomicAdd(&s_hist[bin], 1u);
         }
     }
@@ -2992,6 +3210,36 @@ struct MsdDriver {
             return;
         }
         const bool pk = !count && nd_ && ndg.out16 != nullptr;  // the packed L0 (P88)
+        // a key-range rank's L0 over the packed copy: test, compact, then rank only the kept k-mers
+        if (ks.bits == 2 && !CANON && a.own_span != 0xFFFFFFFFu && a.own_span != 0 && a.pk_code &&
+            ks.symbols <= 32 && a.own_bits <= 32 && (w0 == 7 || w0 == kGR) && (count || nd_) &&
+            !opt("GKM_OWN_L0_TILE")) {
+            const int sh = 32 - a.own_bits;
+            const OwnTest ot{(uint32_t)((uint64_t)a.own_lo << sh),
+                             (uint32_t)(((uint64_t)std::min<uint64_t>(a.own_span, 1ull << a.own_bits) << sh) - 1)};
+            auto grid = [&](const void *k) {
+                int per_cu = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kOwnT, 0) != hipSuccess || per_cu < 1)
+                    per_cu = 1;
+                return dim3(std::min<unsigned>(nt0, cus * (unsigned)per_cu));
+            };
+#define GK_OWN(R_)                                                                                             \
+    do {                                                                                                       \
+        if (count)                                                                                             \
+            hipLaunchKernelGGL(own_count_kernel<R_>, grid((const void *)own_count_kernel<R_>), dim3(kOwnT), 0,   \
+                               c->stream, a, d0, ot, tile_hist, nt0);                                         \
+        else if (pk)                                                                                           \
+            hipLaunchKernelGGL((own_part_kernel<R_, true>), grid((const void *)own_part_kernel<R_, true>),       \
+                               dim3(kOwnT), 0, c->stream, a, d0, ot, tile_hist, kout, vout, nt, ndg);         \
+        else                                                                                                   \
+            hipLaunchKernelGGL((own_part_kernel<R_, false>), grid((const void *)own_part_kernel<R_, false>),     \
+                               dim3(kOwnT), 0, c->stream, a, d0, ot, tile_hist, kout, vout, nt, ndg);         \
+    } while (0)
+            if (w0 == 7) GK_OWN(7);
+            else GK_OWN(kGR);
+#undef GK_OWN
+            return;
+        }
         if (!count && ks.bits == 2 && nd_ && a.own_span != 0xFFFFFFFFu) {  // a key-range rank's fused select
             if (w0 == 7) {
                 if (pk) l0_launch<2, 7, true, CANON, true, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
@@ -4377,6 +4625,8 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
             if (rp != GK_OK) return rp;
         }
         c->pk_fresh = false;
+        d.pk_code = a.pk_code;  // (the fused L0 reads it too)
+        d.pk_dol = a.pk_dol;
     } else if (c->res_pk && ks.bits == 2 && (c->acgt || ks.acgt_only)) {  // the transfer's packed copy
         a.pk_code = c->res_code;
         a.pk_dol = c->res_dol;
@@ -4392,7 +4642,10 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     {
         const int ob = range_own_bits(ks);
         const uint32_t span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
-        bool fused = ks.bits == 2 && span > 0 && (uint64_t)span * kFusedMaxRanks >= (1ull << ob);
+        // (with the compacting L0 -- forward keys of <= 32 symbols over the packed copy, own_part_kernel
+        // -- the fused path is taken at any share)
+        const bool compacting = !ks.canonical && ks.symbols <= 32 && d.pk_code && !opt("GKM_OWN_L0_TILE");
+        bool fused = ks.bits == 2 && span > 0 && (compacting || (uint64_t)span * kFusedMaxRanks >= (1ull << ob));
         if (const char *e = opt("GKM_RANGE_FUSED")) fused = ks.bits == 2 && span > 0 && e[0] == '1';
         if (fused) {
             c->n = 0;

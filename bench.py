@@ -603,8 +603,9 @@ def main():
     if args.no_boundary:
         pass
     elif dist is None:
-        # the sort hint applies to the fixed-length forward sort of a single-contig ACGT sequence (C3)
-        hint = k if (not canonical and 8 <= k <= 32 and len(seg) == 1) else 0
+        # the sort hint applies to the fixed-length forward sort of an ACGT sequence (C3; any number of
+        # contigs since round 6 -- a non-ACGT sequence drops it as the transfer packs its first such byte)
+        hint = k if (not canonical and 8 <= k <= 32) else 0
         e2e = end_to_end(torch, eng, sba, seg, step, log, args.e2e_reps, hint)
         e2e_ms = e2e["e2e_ms"]
     else:  # ranks: each loads the whole sba; the slowest transfer + the step (max over ranks)

@@ -537,7 +537,7 @@ extern "C" int gk_set_sequence(gk_ctx *c, const uint8_t *sba, uint64_t len, cons
             if (int rc = ensure_elems(c, len, 1)) return rc;
         // a sort hint (gk_sort_hint): the L0 pass of gk_sort(k) runs as the sequence lands
         L0Prefetch *pf = nullptr;
-        if (c->hint_k && nseg == 1 && !internal)
+        if (c->hint_k && !internal)
             if (int rc = prefetch_plan(c, len, &pf)) return rc;
         if (int rc = packed_transfer(c, sba, len, &h[0], &dollars, pf)) return rc;
         h[1] = (uint32_t)dollars;

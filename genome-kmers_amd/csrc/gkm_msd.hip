@@ -3211,9 +3211,11 @@ struct MsdDriver {
         }
         const bool pk = !count && nd_ && ndg.out16 != nullptr;  // the packed L0 (P88)
         // a key-range rank's L0 over the packed copy: test, compact, then rank only the kept k-mers
+        // (GKM_OWN_L0_COMPACT=1, measured slower than the select + level from pieces at N >= 4 and
+        // equal to the tile L0 at N = 2: own_part_kernel)
         if (ks.bits == 2 && !CANON && a.own_span != 0xFFFFFFFFu && a.own_span != 0 && a.pk_code &&
             ks.symbols <= 32 && a.own_bits <= 32 && (w0 == 7 || w0 == kGR) && (count || nd_) &&
-            !opt("GKM_OWN_L0_TILE")) {
+            opt("GKM_OWN_L0_COMPACT")) {
             const int sh = 32 - a.own_bits;
             const OwnTest ot{(uint32_t)((uint64_t)a.own_lo << sh),
                              (uint32_t)(((uint64_t)std::min<uint64_t>(a.own_span, 1ull << a.own_bits) << sh) - 1)};
@@ -4187,7 +4189,8 @@ int msd_sort(gk_ctx *c, const KeySpec &ks) {
 // to the sorted product in HBM -- is the packed transfer (host-bound: ~20 ms for 3.1 Gb) followed
 // by the sort, whose first pass (L0 count + partition, ~14 ms at C3) needs only the sequence.  With
 // a hint, gk_set_sequence runs that pass while the sequence streams in: the k-mer starts [0, n) of
-// a single-contig ACGT sba are cut into regions of whole L0 tiles; as soon as the transfer has
+// an ACGT sba (any number of contigs: the '$' separators are stops of the L0 pass, round 6) are cut
+// into regions of whole L0 tiles of positions; as soon as the transfer has
 // unpacked a region's bytes (and its last tile's halo) on the context's stream, the region is
 // counted, scanned and partitioned on the prefetch stream into keys[1] / vals[1] / the digit bytes
 // at output indices from its first position (MsdDriver::l0_region), and its 2^w0 buckets become
@@ -4226,13 +4229,13 @@ static KeySpec hint_spec(uint32_t k) {
 bool prefetch_matches(const gk_ctx *c, const KeySpec &ks) {
     return c->pre_valid && c->enumerated && ks.bits == 2 && ks.symbols == (int)c->pre_k &&
            ks.min_len == ks.symbols && ks.words == 1 && ks.lenbits == 0 && !ks.canonical && !ks.acgt_only &&
-           c->nseg == 1 && c->n + ks.symbols - 1 == c->sba_len;
+           c->n + ks.symbols - 1 <= c->sba_len;
 }
 
 int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
     *out = nullptr;
     const uint32_t k = c->hint_k;
-    if (k < 8 || k > 32 || c->nseg != 1 || len < (uint64_t)k + kP0Tile) return GK_OK;
+    if (k < 8 || k > 32 || len < (uint64_t)k + kP0Tile) return GK_OK;
     const KeySpec ks = hint_spec(k);
     MsdDriver d(c, ks);
     if (d.width(0) != 7 && d.width(0) != kGR) return GK_OK;  // (the wide L0 has its own tiles)
@@ -4642,10 +4645,7 @@ int msd_sort_range(gk_ctx *c, const KeySpec &ks, uint32_t digit_lo, uint32_t dig
     {
         const int ob = range_own_bits(ks);
         const uint32_t span = digit_hi > digit_lo ? digit_hi - digit_lo : 0;
-        // (with the compacting L0 -- forward keys of <= 32 symbols over the packed copy, own_part_kernel
-        // -- the fused path is taken at any share)
-        const bool compacting = !ks.canonical && ks.symbols <= 32 && d.pk_code && !opt("GKM_OWN_L0_TILE");
-        bool fused = ks.bits == 2 && span > 0 && (compacting || (uint64_t)span * kFusedMaxRanks >= (1ull << ob));
+        bool fused = ks.bits == 2 && span > 0 && (uint64_t)span * kFusedMaxRanks >= (1ull << ob);
         if (const char *e = opt("GKM_RANGE_FUSED")) fused = ks.bits == 2 && span > 0 && e[0] == '1';
         if (fused) {
             c->n = 0;

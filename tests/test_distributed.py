@@ -460,6 +460,19 @@ def test_gpu_shard_histogram_packed_copy_vs_numpy(k, iupac, monkeypatch):
         np.testing.assert_array_equal(np.asarray(h, dtype=np.int64)[:1 << ob], want)
 
 
+# Round 6: the compacting rank L0 (own_count_kernel / own_part_kernel: test, compact, then rank the
+# kept k-mers only), opt-in (GKM_OWN_L0_COMPACT=1), at fused and select-sized shares
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,contigs,k,iupac", [(2, 1, 31, False), (8, 2, 31, False), (5, 3, 31, True),
+                                                   (3, 1, 12, False), (4, 2, 32, True), (16, 1, 31, False)])
+def test_gpu_key_ranges_compacting_l0(world, contigs, k, iupac, monkeypatch):
+    monkeypatch.setitem(_native.options, "GKM_OWN_L0_COMPACT", "1")
+    monkeypatch.setitem(_native.options, "GKM_RANGE_FUSED", "1")
+    monkeypatch.setenv("GKM_PACK_MIN", "0")
+    monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
+    test_gpu_key_ranges_concatenate_to_single_sort(world, contigs, k, False, iupac)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,k,canonical", [(2, 31, False), (2, 63, True)])
 def test_gpu_key_ranges_fused_packed_l0(world, k, canonical, monkeypatch):

@@ -1,12 +1,12 @@
 """The sort hint (gk_sort_hint): gk_set_sequence runs the L0 pass of gk_sort(k) over regions of a
-single-contig A/C/G/T sequence while the packed transfer lands them, and the next gk_sort(k) of the
+A/C/G/T sequence (one or many contigs) while the packed transfer lands them, and the next gk_sort(k) of the
 whole enumeration starts from the regions' buckets (gkm_msd.hip, L0Prefetch).
 
 The result must be bit-identical to the sort without the hint -- sorted starts, keys, head flags
 (through the unique counts) -- and to the oracle's break_ties=True order; the tests also check that
 the prefetched pass was the one used (profile stages), and that every other use of the k-mer
-buffers, another k, canonical sorts, user-given starts, multi-contig and non-ACGT sequences fall
-back to the plain sort.  Small chunk and region sizes (GKM_PACK_BLOCKS, GKM_PREFETCH_REGIONS) put
+buffers, another k, canonical sorts, user-given starts and non-ACGT sequences fall back to the
+plain sort.  Small chunk and region sizes (GKM_PACK_BLOCKS, GKM_PREFETCH_REGIONS) put
 many regions, partial tiles and region edges into test-sized inputs."""
 
 import numpy as np
@@ -209,21 +209,51 @@ def test_prefetch_consumed_once_and_dropped_by_other_calls(monkeypatch):
     np.testing.assert_array_equal(got[0], ref)
 
 
-@pytest.mark.parametrize("kind", ["contigs", "N"])
-def test_no_prefetch_outside_single_contig_acgt(kind, monkeypatch):
+def contigs(rng, lengths, repeat=0, copies=0):
+    """'$'-joined random ACGT contigs (the reference's forward_sba layout) and their starts."""
+    parts = [genome(rng, n, min(repeat, n // 2), copies) for n in lengths]
+    seg = np.cumsum([0] + [n + 1 for n in lengths[:-1]]).astype(np.uint32)
+    sba = np.concatenate([np.concatenate([p, np.frombuffer(b"$", dtype=np.uint8)]) for p in parts])[:-1]
+    return np.ascontiguousarray(sba), seg
+
+
+# Round 6: multi-contig ACGT sequences prefetch too (the '$' separators are stops of the region
+# passes, their blocks cross the link raw); bit-identical to the plain sort and to the oracle
+@pytest.mark.parametrize("k", [12, 31, 32])
+@pytest.mark.parametrize("lengths,regions", [
+    ([70_000, 80_000], 4),
+    ([30_000 + 997 * i for i in range(24)], 9),             # 24 contigs: separators in many regions
+    ([100, 40_000, 31, 32, 33, 90_000, 24_576, 12], 6),    # contigs of k bases, tile-sized ones
+])
+def test_prefetch_multi_contig(k, lengths, regions, monkeypatch):
+    rng = np.random.default_rng(len(lengths) + k)
+    # (the reference rejects min_kmer_len > the shortest sequence: the contigs shorter than k drop out)
+    sba, seg = contigs(rng, [n for n in lengths if n >= k], repeat=600, copies=3)
+    _, got, rep = run(sba, seg, k, monkeypatch, True, regions=regions)
+    assert "prefetch_l0" in rep and "msd_pass_l0" not in rep, sorted(rep)
+    _, want, rep0 = run(sba, seg, k, monkeypatch, False, regions=regions)
+    assert "prefetch_l0" not in rep0
+    same(got, want)
+    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, oracle.enumerate_starts(sba, seg, k), k, k,
+                                                           break_ties=True))
+
+
+@pytest.mark.parametrize("kind", ["N", "N_contigs", "iupac_late"])
+def test_no_prefetch_outside_acgt(kind, monkeypatch):
     rng = np.random.default_rng(12)
     L = 150_000
     sba = genome(rng, L)
-    if kind == "contigs":
-        sba[70_000] = ord("$")
-        seg = np.array([0, 70_001], dtype=np.uint32)
-    else:
+    seg = np.zeros(1, dtype=np.uint32)
+    if kind == "N":
         sba[90_000:90_050] = ord("N")
-        seg = np.zeros(1, dtype=np.uint32)
+    elif kind == "N_contigs":  # 24 contigs with N runs (the GRCh38 shape)
+        sba, seg = contigs(rng, [6_000 + 50 * i for i in range(24)])
+        for at in range(1_000, len(sba) - 200, 9_000):
+            sba[at:at + 120] = ord("N")
+    else:  # one IUPAC letter in the last chunk: regions before it have run, the prefetch is dropped
+        sba[L - 40] = ord("R")
     _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=4)
-    if kind == "contigs":  # never planned
-        assert "prefetch_l0" not in rep
-    # (an N block drops the prefetch when its chunk lands: regions before it may have run, unused)
+    # (a non-ACGT byte drops the prefetch when its chunk is packed: regions before it may have run, unused)
     _, want, _ = run(sba, seg, 31, monkeypatch, False, regions=4)
     same(got, want)
     np.testing.assert_array_equal(got[0], oracle.quicksort(sba, oracle.enumerate_starts(sba, seg, 31), 31, 31,

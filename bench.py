@@ -618,7 +618,7 @@ def main():
     # per-stage algorithmic bytes per work unit (k-mer), DESIGN.md section 4.  The L0 passes read
     # the sequence: its resident 2-bit packed copy when gk_set_sequence left one (0.375 B per
     # position: a u64 of codes and a u32 of stop flags per 32 positions), else the ASCII bytes
-    packed_in = eng.resident_packed() and eng.is_acgt()
+    packed_in = eng.resident_packed()  # (an ACGT sba's L0, or the class-A L0 of a mixed one)
     seq_positions = L if dist is None or args.exchange == "range" else job.hi - job.lo
     seq_bytes = seq_positions * (0.375 if packed_in else 1.0)
 

@@ -3451,7 +3451,10 @@ struct MsdDriver {
         c_first = tab;  // (the region's table: nc_max entries each, then misc)
         c_ntiles = tab + nc_max;
         const uint32_t *misc = tab + 2 * nc_max;
-        const L0Args a{c->sba, lo, hi, ks.symbols, B, 0};
+        // (acgt_only: every byte other than A/C/G/T ends k-mers -- on an ACGT sba exactly the '$'
+        // separators, so this is the plain sort's L0 there, and the class-A L0 of a mixed sba's
+        // split sort elsewhere)
+        const L0Args a{c->sba, lo, hi, ks.symbols, B, 1};
         const int w0 = width(0);
         const Dig d0 = dig_at(B, 0, w0);
         l0_dispatch(true, w0, false, a, d0, nt, nullptr, nullptr, 0, 0, NextDigits{});
@@ -4228,8 +4231,8 @@ static KeySpec hint_spec(uint32_t k) {
 
 bool prefetch_matches(const gk_ctx *c, const KeySpec &ks) {
     return c->pre_valid && c->enumerated && ks.bits == 2 && ks.symbols == (int)c->pre_k &&
-           ks.min_len == ks.symbols && ks.words == 1 && ks.lenbits == 0 && !ks.canonical && !ks.acgt_only &&
-           c->n + ks.symbols - 1 <= c->sba_len;
+           ks.min_len == ks.symbols && ks.words == 1 && ks.lenbits == 0 && !ks.canonical &&
+           c->n + ks.symbols - 1 <= c->sba_len;  // (acgt_only: the class A of a mixed sba, gkm_split.hip)
 }
 
 int prefetch_plan(gk_ctx *c, uint64_t len, L0Prefetch **out) {
@@ -4376,8 +4379,8 @@ int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
     d.B = ks.total_bits;
     if (d.width(0) != c->pre_w0 || d.width(1) != c->pre_w1) return msd_sort(c, ks);  // (widths changed)
     d.allow_c79 = opt("GKM_NO_PAIRS") == nullptr;
-    d.wkeys = 1;  // one-word keys end final in keys[0]
-    c->msd_keys_final = true;
+    d.wkeys = (!ks.acgt_only || c->msd_force_keys) ? 1 : 0;  // one-word keys end final in keys[0] (as msd_sort)
+    c->msd_keys_final = d.wkeys != 0;
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;

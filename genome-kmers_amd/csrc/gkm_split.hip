@@ -959,17 +959,27 @@ int split_sort(gk_ctx *c, const KeySpec &ks, bool *used, const SplitRange *rg) {
         c->n = nA + nB;
     } else {
         // both key buffers at the final key width before the A sort (which uses word 0 of each):
-        // nothing is freed or re-allocated between the A sort and the merge
+        // nothing is freed or re-allocated between the A sort and the merge -- except with a
+        // prefetched class-A L0 (gk_sort_hint) in keys[1] / vals[1]: keys[1] grows after the A sort,
+        // whose result is in buffer 0 (keys[1] is its scratch by then)
+        c->n = nA;
+        const bool pre = nA > 0 && prefetch_matches(c, ka);
+        c->n = n;
         if (WK) {
             if (!a_packed)
                 if (int r = grow_key_buffer(c, 0, WK)) return r;
-            if (int r = grow_key_buffer(c, 1, WK)) return r;
+            if (!pre)
+                if (int r = grow_key_buffer(c, 1, WK)) return r;
         }
         c->n = nA;
-        rc = nA > 0 ? msd_sort(c, ka) : GK_OK;
+        rc = nA > 0 ? (pre ? msd_sort_prefetched(c, ka) : msd_sort(c, ka)) : GK_OK;
         c->msd_force_keys = false;
         c->n = n;
         if (rc != GK_OK) return rc;
+        if (pre && WK) {
+            if (c->cur != 0) return fail(c, GK_E_STATE, "split sort: the prefetched A sort did not end in buffer 0");
+            if (int r = grow_key_buffer(c, 1, WK)) return r;
+        }
         a_keys = a_packed ? nullptr : c->keys[0];
     }
     if (nA == 0) {  // all B: the B order is the order

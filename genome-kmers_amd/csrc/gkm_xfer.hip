@@ -460,9 +460,6 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
     for (int i = 0; i < S; ++i) free_slots.push_back(i);
     std::atomic<uint32_t> cls{0};
     std::atomic<uint64_t> dol{0};
-    // a packed chunk held an IUPAC / N byte: the sequence is not ACGT, the prefetched plain L0 is not
-    // the sort it will get (set as soon as a worker's census sees one)
-    std::atomic<bool> nonacgt{false};
 
     auto worker = [&]() {
         Census cen;
@@ -481,7 +478,6 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             bool whole = false;
             const uint64_t u = pack_chunk(sba + at, m, c->xfer_host + (uint64_t)slot * c->xfer_slot_bytes, cen, &whole);
             _mm_sfence();  // the chunk's streaming stores are globally visible before it is queued
-            if (cen.cls_or & 2u) nonacgt.store(true, std::memory_order_relaxed);
             {
                 std::lock_guard<std::mutex> lk(mu);
                 used[slot] = u;
@@ -546,9 +542,8 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
             chunk_issued[k] = 1;
         }
         // prefetch: the in-order prefix of enqueued unpacks has grown -- launch the L0 regions it covers
-        // (chunks with raw blocks -- '$' separators of a multi-contig sequence -- are unpacked on the
-        // same stream; a non-ACGT byte anywhere ends the prefetch: that sequence gets another sort)
-        if (pf_ok && nonacgt.load(std::memory_order_relaxed)) pf_ok = false;
+        // (chunks with raw blocks -- '$' separators, N runs, IUPAC letters -- are unpacked on the same
+        // stream; the region passes stop k-mers at every non-ACGT byte: a mixed sba's class A)
         if (pf_ok && err == hipSuccess && prefix < C && chunk_issued[prefix]) {
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -634,7 +629,7 @@ int packed_transfer(gk_ctx *c, const uint8_t *sba, uint64_t len, uint32_t *cls_o
         if (err == hipSuccess) c->res_pk = true;  // (gk_set_sequence keeps it for an ACGT census)
     }
     if (pf) {
-        const int rc = prefetch_finish(c, pf, pf_ok && !nonacgt.load() && err == hipSuccess && prefix == C);
+        const int rc = prefetch_finish(c, pf, pf_ok && err == hipSuccess && prefix == C);
         if (err == hipSuccess && rc != GK_OK) return rc;
     }
     if (pf_rc != GK_OK) return pf_rc;  // (prefetch_launch's own error; it set the message)

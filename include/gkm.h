@@ -125,10 +125,12 @@ int gk_set_sequence(gk_ctx *ctx, const uint8_t *sba, uint64_t len, const uint32_
 int gk_copy_sequence(gk_ctx *ctx, uint8_t *dst, uint64_t len);
 /* Sort hint (no reference counterpart: the reference has no transfer; Kmers(sc, k, k) followed by
  * Kmers.sort(), kmers.py:656-760, 1624-1652, is the call pattern it serves).  While k != 0, every
- * later gk_set_sequence of a single-contig sba that crosses the link packed (pure A/C/G/T) also runs
- * the first pass of gk_sort(k) -- the L0 partition by the top key bits -- over regions of the
- * sequence as they land, on a stream of its own; the next gk_enumerate(k) + gk_sort(k, 0) of the
- * whole enumeration then starts from its buckets (same result, less time after the transfer).
+ * later gk_set_sequence that crosses the link packed (>= GKM_PACK_MIN bytes, any number of contigs)
+ * also runs the first pass of gk_sort(k) -- the L0 partition of the A/C/G/T-only k-mers by their top
+ * key bits -- over regions of the sequence as they land, on a stream of its own; the next
+ * gk_enumerate(k) + gk_sort(k, 0) of the whole enumeration then starts from its buckets (same
+ * result, less time after the transfer): on an A/C/G/T sba they are the sort's own L0, on a mixed
+ * one (N runs, IUPAC letters) the L0 of the split sort's A/C/G/T-only class.
  * Any other call that uses the k-mer buffers drops the prefetched pass.  k = 0 clears the hint;
  * flags must be 0.  Hints outside 8 <= k <= 32 are ignored. */
 int gk_sort_hint(gk_ctx *ctx, uint32_t k, uint32_t flags);

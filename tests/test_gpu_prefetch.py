@@ -5,8 +5,8 @@ whole enumeration starts from the regions' buckets (gkm_msd.hip, L0Prefetch).
 The result must be bit-identical to the sort without the hint -- sorted starts, keys, head flags
 (through the unique counts) -- and to the oracle's break_ties=True order; the tests also check that
 the prefetched pass was the one used (profile stages), and that every other use of the k-mer
-buffers, another k, canonical sorts, user-given starts and non-ACGT sequences fall back to the
-plain sort.  Small chunk and region sizes (GKM_PACK_BLOCKS, GKM_PREFETCH_REGIONS) put
+buffers, another k, canonical sorts and user-given starts fall back to the plain sort; on a mixed sba
+(N runs, IUPAC letters) the prefetched pass is the class-A L0 of the split sort.  Small chunk and region sizes (GKM_PACK_BLOCKS, GKM_PREFETCH_REGIONS) put
 many regions, partial tiles and region edges into test-sized inputs."""
 
 import numpy as np
@@ -238,8 +238,11 @@ def test_prefetch_multi_contig(k, lengths, regions, monkeypatch):
                                                            break_ties=True))
 
 
+# Round 6: a mixed sba (N runs, IUPAC letters) prefetches its class-A L0 (the region passes stop
+# k-mers at every non-ACGT byte) and the split sort's A sort starts from it (gkm_split.hip)
+@pytest.mark.parametrize("k", [16, 31])
 @pytest.mark.parametrize("kind", ["N", "N_contigs", "iupac_late"])
-def test_no_prefetch_outside_acgt(kind, monkeypatch):
+def test_prefetch_mixed_alphabet(kind, k, monkeypatch):
     rng = np.random.default_rng(12)
     L = 150_000
     sba = genome(rng, L)
@@ -252,11 +255,12 @@ def test_no_prefetch_outside_acgt(kind, monkeypatch):
             sba[at:at + 120] = ord("N")
     else:  # one IUPAC letter in the last chunk: regions before it have run, the prefetch is dropped
         sba[L - 40] = ord("R")
-    _, got, rep = run(sba, seg, 31, monkeypatch, True, regions=4)
-    # (a non-ACGT byte drops the prefetch when its chunk is packed: regions before it may have run, unused)
-    _, want, _ = run(sba, seg, 31, monkeypatch, False, regions=4)
+    _, got, rep = run(sba, seg, k, monkeypatch, True, regions=4)
+    assert "prefetch_l0" in rep and "split_merge" in rep and "msd_pass_l0" not in rep, sorted(rep)
+    _, want, rep0 = run(sba, seg, k, monkeypatch, False, regions=4)
+    assert "prefetch_l0" not in rep0 and "split_merge" in rep0
     same(got, want)
-    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, oracle.enumerate_starts(sba, seg, 31), 31, 31,
+    np.testing.assert_array_equal(got[0], oracle.quicksort(sba, oracle.enumerate_starts(sba, seg, k), k, k,
                                                            break_ties=True))
 
 

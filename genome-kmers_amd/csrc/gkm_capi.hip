@@ -1339,7 +1339,9 @@ extern "C" int gk_profile_report(gk_ctx *c, char *buf, uint64_t buflen) {
 // multi-GPU shards
 // ---------------------------------------------------------------------------------------------
 static int shard_spec(gk_ctx *c, uint32_t k, uint32_t flags, KeySpec *ks) {
-    if (flags & ~GK_SORT_CANONICAL) return fail(c, GK_E_ARG, "unknown shard flags");
+    if (flags & ~(GK_SORT_CANONICAL | GK_SHARD_STARTS_ONLY)) return fail(c, GK_E_ARG, "unknown shard flags");
+    if ((flags & GK_SHARD_STARTS_ONLY) && ((flags & GK_SORT_CANONICAL) || !c->acgt || k > 32))
+        return fail(c, GK_E_UNSUPPORTED, "starts-only shards: forward keys of an A/C/G/T sba with k <= 32");
     const int bits = c->acgt ? 2 : 4;
     if (k == 0 || k > 64) return fail(c, GK_E_ARG, "shard k-mers must have 1 <= k <= 64");
     *ks = KeySpec{};
@@ -1357,7 +1359,8 @@ extern "C" int gk_shard_bucket_bits(void) { return gkm::msd_radix_bits(); }
 
 extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *d_keys,
                                   uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out) {
-    if (!c || !d_keys || !d_starts || !h_hist || !n_out) return GK_E_ARG;
+    const bool starts_only = (flags & GK_SHARD_STARTS_ONLY) != 0;
+    if (!c || (!d_keys && !starts_only) || !d_starts || !h_hist || !n_out) return GK_E_ARG;
     pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (lo % 32) return fail(c, GK_E_ARG, "shard lo must be a multiple of 32");
@@ -1366,7 +1369,8 @@ extern "C" int gk_shard_partition(gk_ctx *c, uint64_t lo, uint64_t hi, uint32_t 
     KeySpec ks;
     int rc = shard_spec(c, k, flags, &ks);
     if (rc != GK_OK) return rc;
-    return msd_shard_partition(c, ks, lo, std::max(hi, lo), d_keys, d_starts, cap, h_hist, n_out);
+    return msd_shard_partition(c, ks, lo, std::max(hi, lo), starts_only ? nullptr : d_keys, d_starts, cap, h_hist,
+                               n_out);
 }
 
 // Key-range shards of a mixed sba (N runs, IUPAC letters; k >= 4): the ranges are top-7-bit
@@ -1515,7 +1519,9 @@ static int shard_sort_range_impl(gk_ctx *c, uint32_t k, uint32_t flags, uint32_t
 extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *d_starts, uint64_t n, uint32_t k,
                              uint32_t flags, const uint64_t *h_piece_off, const uint64_t *h_piece_len,
                              const uint32_t *h_piece_bucket, uint32_t npieces) {
-    if (!c || (n && (!d_keys || !d_starts || !h_piece_off || !h_piece_len || !h_piece_bucket))) return GK_E_ARG;
+    const bool starts_only = (flags & GK_SHARD_STARTS_ONLY) != 0;
+    if (!c || (n && ((!d_keys && !starts_only) || !d_starts || !h_piece_off || !h_piece_len || !h_piece_bucket)))
+        return GK_E_ARG;
     pre_drop(c);  // (the k-mer buffers: a prefetched L0 does not survive)
     GK_TRY_HIP(c, hipSetDevice(c->device));
     if (n > 0xFFFFFFFFull) return fail(c, GK_E_ARG, "more k-mers than uint32 start indices can address");
@@ -1533,7 +1539,8 @@ extern "C" int gk_shard_sort(gk_ctx *c, const uint64_t *d_keys, const uint32_t *
     c->starts_materialized = true;
     c->sorted = c->keys_valid = c->unique_valid = c->heads_valid = c->canonical = c->enum_sorted = false;
     if (n > 0) {
-        rc = msd_shard_sort(c, ks, d_keys, d_starts, h_piece_off, h_piece_len, h_piece_bucket, npieces);
+        rc = msd_shard_sort(c, ks, starts_only ? nullptr : d_keys, d_starts, h_piece_off, h_piece_len, h_piece_bucket,
+                            npieces);
         if (rc != GK_OK) return rc;
     } else {
         c->cur = 0;

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(T) void msd0_pipe_kernel(L0Args a, Dig d0, const ui
             nd.out16[o] = (uint16_t)(st & ((1u << (32 - shi)) - 1));
             nd.out[o] = (uint8_t)dg_of(key, nd.d);
         } else {
-            kout[o] = key;
+            if (kout) kout[o] = key;  // (none: a starts-only shard send, GK_SHARD_STARTS_ONLY)
             vout[o] = (uint32_t)(pP0 + p);
             if (ND) nd.out[o] = (uint8_t)dg_of(key, nd.d);
         }
@@ -4417,6 +4417,24 @@ int msd_sort_prefetched(gk_ctx *c, const KeySpec &ks) {
     return rc;
 }
 
+// starts-only shards (GK_SHARD_STARTS_ONLY): key of the k-mer at every received start from the 2-bit
+// packed copy (B <= 64 bits: the first word), and its next-level digit byte
+__global__ __launch_bounds__(256) void keys_from_starts_kernel(const uint64_t *__restrict__ pk,
+                                                                const uint32_t *__restrict__ vin, uint64_t n, int B,
+                                                                Dig dn, uint64_t *__restrict__ kout,
+                                                                uint8_t *__restrict__ nd) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t s = vin[i], q = s >> 5, sh = (s & 31) * 2;
+        const uint64_t A = pk[q];
+        const uint64_t T = sh ? (A << sh) | (pk[q + 1] >> (64 - sh)) : A;
+        const uint64_t key = T >> (64 - B);
+        kout[i] = key;
+        nd[i] = (uint8_t)dg_of(key, dn);
+    }
+}
+
+static unsigned grid_of_n_msd(uint64_t n) { return (unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 16); }
+
 // multi-GPU send side: k-mers starting in [lo, hi) partitioned by their top kGR key bits
 int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, uint64_t *kout, uint32_t *vout,
                         uint64_t cap, uint64_t *hist, uint64_t *count) {
@@ -4447,6 +4465,29 @@ int msd_shard_sort(gk_ctx *c, const KeySpec &ks, const uint64_t *kin, const uint
     timer_begin(c, "msd_total", &d.total_slot);
     int rc = d.init(c->n);
     if (rc != GK_OK) return rc;
+    if (!kin) {
+        // starts only (GK_SHARD_STARTS_ONLY): every received k-mer's key from the rank's own packed copy
+        // of the sequence (a sender's piece holds ascending starts of one position range, so the
+        // words read stay close), with the level-1 digit byte its count pass reads
+        const uint64_t *pk = nullptr;
+        const uint32_t *pd = nullptr;
+        if (c->res_pk && c->acgt) {
+            pk = c->res_code;
+        } else {
+            int rp = pack_sequence(c, &pk, &pd);
+            if (rp != GK_OK) return rp;
+        }
+        GK_TRY_HIP(c, scratch(c, "msd_nd", c->n + 64, &d.nd));
+        int slot;
+        timer_begin(c, "shard_keys", &slot);
+        timer_units(c, slot, c->n);
+        hipLaunchKernelGGL(keys_from_starts_kernel, dim3(grid_of_n_msd(c->n)), dim3(256), 0, c->stream, pk, vin, c->n,
+                           d.B, dig_at(d.B, kGR, d.width(1)), c->keys[1], d.nd);
+        GK_TRY_HIP(c, hipGetLastError());
+        timer_end(c, slot);
+        kin = c->keys[1];
+        d.nd_ready = true;
+    }
     rc = d.first_level_from_pieces(kin, vin, poff, plen, pbucket, np);
     if (rc != GK_OK) return rc;
     rc = d.levels(2, kGR + d.width(1), 0);

@@ -61,6 +61,7 @@ EXPORTED = (
 
 SORT_CANONICAL = 1  # GK_SORT_CANONICAL
 SORT_QUICKSORT_ORDER = 2  # GK_SORT_QUICKSORT_ORDER
+SHARD_STARTS_ONLY = 4  # GK_SHARD_STARTS_ONLY
 
 
 class GkFilter(ctypes.Structure):
@@ -465,27 +466,31 @@ class Engine:
     def shard_bucket_bits(self) -> int:
         return int(self.lib.gk_shard_bucket_bits())
 
-    def shard_partition(self, lo: int, hi: int, k: int, keys, starts, canonical: bool = False):
+    def shard_partition(self, lo: int, hi: int, k: int, keys, starts, canonical: bool = False,
+                        starts_only: bool = False):
         """Encode + partition the k-mers starting in [lo, hi) into the device tensors ``keys``
-        (int64) / ``starts`` (int32); returns (bucket sizes as a numpy uint64 array, count)."""
+        (int64) / ``starts`` (int32); returns (bucket sizes as a numpy uint64 array, count).
+        starts_only (GK_SHARD_STARTS_ONLY): ``keys`` may be None, only the starts are written."""
         hist = np.zeros(1 << self.shard_bucket_bits(), dtype=np.uint64)
         n = ctypes.c_uint64(0)
-        cap = min(keys.numel(), starts.numel())
-        self._check(self.lib.gk_shard_partition(self.ctx, lo, hi, k, SORT_CANONICAL if canonical else 0,
-                                                keys.data_ptr(), starts.data_ptr(), cap,
-                                                _ptr(hist, ctypes.c_uint64), ctypes.byref(n)))
+        cap = starts.numel() if keys is None else min(keys.numel(), starts.numel())
+        flags = (SORT_CANONICAL if canonical else 0) | (SHARD_STARTS_ONLY if starts_only else 0)
+        self._check(self.lib.gk_shard_partition(self.ctx, lo, hi, k, flags, None if keys is None else keys.data_ptr(),
+                                                starts.data_ptr(), cap, _ptr(hist, ctypes.c_uint64), ctypes.byref(n)))
         return hist, n.value
 
     def shard_sort(self, keys, starts, n: int, k: int, piece_off: np.ndarray, piece_len: np.ndarray,
-                   piece_bucket: np.ndarray, canonical: bool = False):
-        """Sort n received (key, start) pairs held in device tensors, given as bucket pieces."""
+                   piece_bucket: np.ndarray, canonical: bool = False, starts_only: bool = False):
+        """Sort n received (key, start) pairs held in device tensors, given as bucket pieces.
+        starts_only (GK_SHARD_STARTS_ONLY): ``keys`` may be None, the keys are re-derived from the
+        resident sequence."""
         off = np.ascontiguousarray(piece_off, dtype=np.uint64)
         ln = np.ascontiguousarray(piece_len, dtype=np.uint64)
         bk = np.ascontiguousarray(piece_bucket, dtype=np.uint32)
-        self._check(self.lib.gk_shard_sort(self.ctx, keys.data_ptr() if n else None, starts.data_ptr() if n else None,
-                                           n, k, SORT_CANONICAL if canonical else 0, _ptr(off, ctypes.c_uint64),
-                                           _ptr(ln, ctypes.c_uint64),
-                                           _ptr(bk, ctypes.c_uint32), len(bk)))
+        flags = (SORT_CANONICAL if canonical else 0) | (SHARD_STARTS_ONLY if starts_only else 0)
+        self._check(self.lib.gk_shard_sort(self.ctx, keys.data_ptr() if n and keys is not None else None,
+                                           starts.data_ptr() if n else None, n, k, flags, _ptr(off, ctypes.c_uint64),
+                                           _ptr(ln, ctypes.c_uint64), _ptr(bk, ctypes.c_uint32), len(bk)))
         self.n = n
 
     def shard_histogram(self, lo: int, hi: int, k: int, canonical: bool = False):

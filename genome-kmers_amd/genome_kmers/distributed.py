@@ -16,8 +16,11 @@ selects its k-mers from the whole resident sequence and sorts them.
    partitions them stably by the top ``bits`` (8) key bits into a torch-owned send buffer;
 2. ``all_gather`` of the 256-bucket histograms: every rank derives the same split of the buckets
    into N contiguous ranges of about n/N k-mers each (``split_buckets``);
-3. the exchange: every rank sends each other rank the buckets it owns, keys and starts, as one
-   group of point-to-point messages (ncclSend / ncclRecv over xGMI under RCCL);
+3. the exchange: every rank sends each other rank the buckets it owns as one group of
+   point-to-point messages (ncclSend / ncclRecv over xGMI under RCCL) -- keys and starts, or (round
+   6, ``starts_only``: forward keys of an A/C/G/T sequence with k <= 32, the default there) the
+   starts alone, 4 B per k-mer instead of 12: every rank holds the whole sequence, so the receiver
+   re-derives each key from its own copy (GK_SHARD_STARTS_ONLY);
 4. ``shard_sort``: the received buckets are sorted by the MSD levels below the top bits.  A bucket
    arrives as one piece per source rank; pieces are listed in source-rank order, and ranks own
    ascending positions, so equal keys stay in ascending start order.
@@ -86,7 +89,7 @@ class ShardedKmerSort:
 
     def __init__(self, sba: np.ndarray, seg_starts: np.ndarray, k: int, rank: int, world: int, device: int = 0,
                  engine=None, torch_device=None, group=None, chunk: int = None, canonical: bool = False,
-                 stage_host: bool = None):
+                 stage_host: bool = None, starts_only: bool = None):
         import torch
         import torch.distributed as dist
 
@@ -107,8 +110,13 @@ class ShardedKmerSort:
         self.lo, self.hi = bounds[rank], bounds[rank + 1]
         self.total_kmers = count_kmers(len(sba), seg_starts, k)
         self.nb = 1 << self.engine.shard_bucket_bits()
+        # only the starts cross the exchange where the receiver can re-derive the keys (the same
+        # decision on every rank: the same sequence, k and flag)
+        if starts_only is None:
+            starts_only = not canonical and k <= 32 and self.engine.is_acgt()
+        self.starts_only = starts_only
         cap = self.hi - self.lo + 64
-        self.send_k = torch.empty(cap, dtype=torch.int64, device=self.dev)
+        self.send_k = None if starts_only else torch.empty(cap, dtype=torch.int64, device=self.dev)
         self.send_v = torch.empty(cap, dtype=torch.int32, device=self.dev)
         self.recv_k = torch.empty(0, dtype=torch.int64, device=self.dev)
         self.recv_v = torch.empty(0, dtype=torch.int32, device=self.dev)
@@ -123,9 +131,10 @@ class ShardedKmerSort:
         self.stage_host = stage_host
 
     def _ensure_recv(self, n: int):
-        if self.recv_k.numel() < n + 64:
+        if self.recv_v.numel() < n + 64:
             size = n + n // 8 + 64
-            self.recv_k = self.torch.empty(size, dtype=self.torch.int64, device=self.dev)
+            if not self.starts_only:
+                self.recv_k = self.torch.empty(size, dtype=self.torch.int64, device=self.dev)
             self.recv_v = self.torch.empty(size, dtype=self.torch.int32, device=self.dev)
 
     # bytes per point-to-point message: RCCL mis-copies messages of 2^31 bytes and more (measured
@@ -168,7 +177,7 @@ class ShardedKmerSort:
         """One sort; returns this rank's number of distinct k-mers."""
         torch, dist = self.torch, self.dist
         hist, n = self.engine.shard_partition(self.lo, self.hi, self.k, self.send_k, self.send_v,
-                                              canonical=self.canonical)
+                                              canonical=self.canonical, starts_only=self.starts_only)
         h = torch.from_numpy(np.asarray(hist, dtype=np.int64)).to("cpu" if self.stage_host else self.dev)
         gathered = [torch.empty_like(h) for _ in range(self.world)]
         dist.all_gather(gathered, h, group=self.group)
@@ -181,12 +190,14 @@ class ShardedKmerSort:
         recv_counts = [int(H[s, b0:b1].sum()) for s in range(self.world)]
         R = sum(recv_counts)
         self._ensure_recv(R)
-        self._exchange(self.send_k, self.recv_k, send_counts, recv_counts)
+        if not self.starts_only:
+            self._exchange(self.send_k, self.recv_k, send_counts, recv_counts)
         self._exchange(self.send_v, self.recv_v, send_counts, recv_counts)
         off, ln, bk = receive_pieces(H, b0, b1, recv_counts)
-        if self.recv_k.is_cuda:  # the engine works on its own stream: the exchange must be done
+        if self.recv_v.is_cuda:  # the engine works on its own stream: the exchange must be done
             torch.cuda.current_stream(self.dev).synchronize()
-        self.engine.shard_sort(self.recv_k, self.recv_v, R, self.k, off, ln, bk, canonical=self.canonical)
+        self.engine.shard_sort(None if self.starts_only else self.recv_k, self.recv_v, R, self.k, off, ln, bk,
+                               canonical=self.canonical, starts_only=self.starts_only)
         self.local_kmers = R
         self.engine.materialize_keys()
         return self.engine.unique_count_only()

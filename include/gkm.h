@@ -233,6 +233,12 @@ int gk_shard_bucket_bits(void);
  */
 int gk_shard_partition(gk_ctx *ctx, uint64_t lo, uint64_t hi, uint32_t k, uint32_t flags, uint64_t *d_keys,
                        uint32_t *d_starts, uint64_t cap, uint64_t *h_hist, uint64_t *n_out);
+/* Shard flag (round 6): only the start indices cross the exchange -- 4 B per k-mer instead of 12.
+ * gk_shard_partition writes d_starts only (d_keys may be NULL); gk_shard_sort ignores d_keys and
+ * re-derives every received k-mer's key from its own resident copy of the sequence (every rank holds
+ * the whole sba, as the key-range shards do).  Forward keys of an A/C/G/T sba with k <= 32 only
+ * (GK_E_UNSUPPORTED otherwise); the same flag on every rank. */
+#define GK_SHARD_STARTS_ONLY 4u
 /*
  * Receive side: sort n received (key, start) pairs in DEVICE buffers, given as npieces pieces
  * (offset, length, bucket) listed in ascending bucket order; the pieces of one bucket are listed

@@ -67,21 +67,25 @@ class NumpyShardEngine:
     def shard_bucket_bits(self):
         return self.bits
 
-    def shard_partition(self, lo, hi, k, keys_t, starts_t, canonical=False):
+    def shard_partition(self, lo, hi, k, keys_t, starts_t, canonical=False, starts_only=False):
         assert not canonical
+        assert (keys_t is None) == starts_only, "a starts-only send has no key buffer"
         s = _valid_starts(self.sba, self.seg, k, lo, hi)
         key = _keys(self.sba, s, k)
         top = (key >> np.uint64(2 * k - self.bits)).astype(np.int64)
         order = np.argsort(top, kind="stable")
         n = len(s)
-        keys_t[:n] = __import__("torch").from_numpy(key[order].view(np.int64))
+        if not starts_only:
+            keys_t[:n] = __import__("torch").from_numpy(key[order].view(np.int64))
         starts_t[:n] = __import__("torch").from_numpy(s[order].astype(np.int32))
         return np.bincount(top, minlength=1 << self.bits).astype(np.uint64), n
 
-    def shard_sort(self, keys_t, starts_t, n, k, off, ln, bk, canonical=False):
+    def shard_sort(self, keys_t, starts_t, n, k, off, ln, bk, canonical=False, starts_only=False):
         assert np.all(np.diff(bk.astype(np.int64)) >= 0), "pieces must come in bucket order"
-        key = keys_t[:n].numpy().view(np.uint64)
+        assert (keys_t is None) == starts_only, "a starts-only receive has no key buffer"
         st = starts_t[:n].numpy().astype(np.int64)
+        # (starts only: the keys re-derived from the resident sequence, as the engine does)
+        key = _keys(self.sba, st, k) if starts_only else keys_t[:n].numpy().view(np.uint64)
         idx = np.concatenate([np.arange(o, o + m) for o, m in zip(off.astype(np.int64), ln.astype(np.int64))]) \
             if len(off) else np.zeros(0, dtype=np.int64)
         key, st = key[idx], st[idx]
@@ -169,7 +173,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, sba, seg, k, q, chunk, scheme="a2a"):
+def _worker(rank, world, port, sba, seg, k, q, chunk, scheme="a2a", starts_only=None):
     import torch
     import torch.distributed as dist
 
@@ -182,16 +186,17 @@ def _worker(rank, world, port, sba, seg, k, q, chunk, scheme="a2a"):
                                      torch_device=torch.device("cpu"))
         else:
             job = D.ShardedKmerSort(sba, seg, k, rank, world, engine=NumpyShardEngine(),
-                                    torch_device=torch.device("cpu"), chunk=chunk)
+                                    torch_device=torch.device("cpu"), chunk=chunk, starts_only=starts_only)
         n_unique = job.run()
         q.put((rank, job.engine.starts.tolist(), n_unique, job.total_kmers, job.local_kmers))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scheme,contigs,chunk", [("a2a", 1, None), ("a2a", 3, None), ("a2a", 1, 5000),
-                                                  ("range", 1, None), ("range", 3, None)])
-def test_gloo_world2_matches_oracle(scheme, contigs, chunk):
+@pytest.mark.parametrize("scheme,contigs,chunk,starts_only", [
+    ("a2a", 1, None, None), ("a2a", 3, None, None), ("a2a", 1, 5000, None), ("a2a", 3, 5000, False),
+    ("a2a", 1, None, False), ("range", 1, None, None), ("range", 3, None, None)])
+def test_gloo_world2_matches_oracle(scheme, contigs, chunk, starts_only):
     import torch.multiprocessing as mp
 
     from oracle import oracle
@@ -203,7 +208,8 @@ def test_gloo_world2_matches_oracle(scheme, contigs, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sba, seg, K, q, chunk, scheme)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sba, seg, K, q, chunk, scheme, starts_only))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in procs)
@@ -334,6 +340,78 @@ def test_gpu_shards_concatenate_to_single_sort(world, contigs, k, canonical, iup
     ref.sort(k, canonical=canonical)
     np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
     assert uniq == ref.unique_count_only()
+
+
+# Round 6: starts-only shards (GK_SHARD_STARTS_ONLY): the send holds no keys, the receiver re-derives
+# them from its own copy of the sequence -- with and without the transfer's resident packed copy
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True], ids=["packed_now", "resident"])
+@pytest.mark.parametrize("world,contigs,k", [(2, 1, 31), (3, 4, 31), (8, 1, 31), (4, 2, 12), (5, 3, 32), (2, 1, 5)])
+def test_gpu_shards_starts_only(world, contigs, k, packed, monkeypatch):
+    import torch
+
+    from genome_kmers import _native
+
+    if packed:
+        monkeypatch.setenv("GKM_PACK_MIN", "0")
+        monkeypatch.setenv("GKM_PACK_BLOCKS", "1")
+    sba, seg = _random_sba(200_000 + 17, 5 + world, contigs)
+    sba[150_100:151_000] = sba[1000:1900]  # repeats across ranks (inside a contig)
+    engines = [_native.Engine(0) for _ in range(world)]
+    bounds = D.position_ranges(len(sba), world)
+    dev = torch.device("cuda", 0)
+    sends, hists = [], []
+    for r, e in enumerate(engines):
+        e.set_sequence(sba, seg)
+        assert e.resident_packed() == packed
+        sv = torch.empty(bounds[r + 1] - bounds[r] + 64, dtype=torch.int32, device=dev)
+        hist, n = e.shard_partition(bounds[r], bounds[r + 1], k, None, sv, starts_only=True)
+        sends.append(sv)
+        hists.append(np.asarray(hist, dtype=np.int64))
+    H = np.stack(hists)
+    bb = D.split_buckets(H.sum(axis=0), world)
+    got, keys, uniq = [], [], 0
+    for r, e in enumerate(engines):
+        parts_v, recv_counts = [], []
+        for s in range(world):
+            lo = int(H[s, :bb[r]].sum())
+            m = int(H[s, bb[r]:bb[r + 1]].sum())
+            parts_v.append(sends[s][lo:lo + m])
+            recv_counts.append(m)
+        R = sum(recv_counts)
+        rv = torch.cat(parts_v + [torch.empty(64, dtype=torch.int32, device=dev)])
+        off, ln, bk = D.receive_pieces(H, bb[r], bb[r + 1], recv_counts)
+        torch.cuda.current_stream(dev).synchronize()
+        e.shard_sort(None, rv, R, k, off, ln, bk, starts_only=True)
+        got.append(e.copy_starts())
+        keys.append(e.copy_keys())
+        uniq += e.unique_count_only()
+    ref = _native.Engine(0)
+    ref.set_sequence(sba, seg)
+    ref.enumerate(k)
+    ref.sort(k)
+    np.testing.assert_array_equal(np.concatenate(got), ref.copy_starts())
+    np.testing.assert_array_equal(np.concatenate(keys), ref.copy_keys())
+    assert uniq == ref.unique_count_only()
+
+
+@pytest.mark.gpu
+def test_gpu_shards_starts_only_refuses_what_it_cannot_rederive():
+    import torch
+
+    from genome_kmers import _native
+
+    sba, seg = _random_sba(50_000, 3, 1)
+    sv = torch.empty(60_000, dtype=torch.int32, device=torch.device("cuda", 0))
+    e = _native.Engine(0)
+    e.set_sequence(sba, seg)
+    for k, canonical in [(33, False), (31, True)]:
+        with pytest.raises(_native.GkError, match="starts-only"):
+            e.shard_partition(0, len(sba), k, None, sv, canonical=canonical, starts_only=True)
+    sba[100:110] = ord("N")
+    e.set_sequence(sba, seg)
+    with pytest.raises(_native.GkError, match="starts-only"):
+        e.shard_partition(0, len(sba), 31, None, sv, starts_only=True)
 
 
 @pytest.mark.gpu

@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--worlds", type=str, default="8,4,2")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--keys", action="store_true",
+                    help="a2a: exchange (key, start) pairs (12 B) even where the starts alone (4 B, "
+                         "GK_SHARD_STARTS_ONLY, the default for forward ACGT k <= 32) would do")
     ap.add_argument("--b-scan", action="store_true",
                     help="mixed sba: every rank scans the whole sequence for its class-B k-mers (round-2 path)")
     args = ap.parse_args()
@@ -190,13 +193,15 @@ def main():
             import torch
 
             dev = torch.device("cuda", 0)
+            so = not args.keys and not canonical and k <= 32 and e.is_acgt()  # (as ShardedKmerSort)
+            wire = 4 if so else 12  # bytes per k-mer over xGMI
             sends, hists, part_ms = [], [], []
             for r in range(world):
                 cap = pb[r + 1] - pb[r] + 64
-                sk = torch.empty(cap, dtype=torch.int64, device=dev)
+                sk = None if so else torch.empty(cap, dtype=torch.int64, device=dev)
                 sv = torch.empty(cap, dtype=torch.int32, device=dev)
                 ms, (hist, n) = best_of(lambda _l, r=r, sk=sk, sv=sv: e.shard_partition(
-                    pb[r], pb[r + 1], k, sk, sv, canonical=canonical), args.reps, e.sync)
+                    pb[r], pb[r + 1], k, sk, sv, canonical=canonical, starts_only=so), args.reps, e.sync)
                 sends.append((sk, sv))
                 hists.append(np.asarray(hist, dtype=np.int64))
                 part_ms.append(ms)
@@ -207,17 +212,18 @@ def main():
                 parts_k, parts_v = [], []
                 for s in range(world):
                     lo = int(H[s, :bb[r]].sum())
-                    parts_k.append(sends[s][0][lo:lo + to[s, r]])
+                    if not so:
+                        parts_k.append(sends[s][0][lo:lo + to[s, r]])
                     parts_v.append(sends[s][1][lo:lo + to[s, r]])
                 R = int(to[:, r].sum())
-                rk = torch.cat(parts_k + [torch.empty(64, dtype=torch.int64, device=dev)])
+                rk = None if so else torch.cat(parts_k + [torch.empty(64, dtype=torch.int64, device=dev)])
                 rv = torch.cat(parts_v + [torch.empty(64, dtype=torch.int32, device=dev)])
                 off, ln, bk = D.receive_pieces(H, bb[r], bb[r + 1], list(to[:, r]))
                 torch.cuda.synchronize()
 
                 def rank(last, r=r, rk=rk, rv=rv, R=R, off=off, ln=ln, bk=bk):
                     e.profile_enable(last)
-                    e.shard_sort(rk, rv, R, k, off, ln, bk, canonical=canonical)
+                    e.shard_sort(rk, rv, R, k, off, ln, bk, canonical=canonical, starts_only=so)
                     e.materialize_keys()
                     u = e.unique_count_only()
                     rep = e.profile_report() if last else None
@@ -225,11 +231,12 @@ def main():
                     return u, rep
                 ms, (u, rep) = best_of(rank, args.reps, e.sync)
                 peers = [d for d in range(world) if d != r]
-                x_bytes = 12 * max([int(to[r, d]) for d in peers] + [int(to[s, r]) for s in peers] + [0])
+                x_bytes = wire * max([int(to[r, d]) for d in peers] + [int(to[s, r]) for s in peers] + [0])
                 x_ms = x_bytes / (LINK_GBS * 1e9) * 1e3
                 extra.append({"partition_ms": round(part_ms[r], 2), "sort_ms": round(ms, 2),
                               "exchange_link_bound_ms": round(x_ms, 2),
-                              "sent_gb": round(12 * (int(to[r].sum()) - int(to[r, r])) / 1e9, 3)})
+                              "sent_gb": round(wire * (int(to[r].sum()) - int(to[r, r])) / 1e9, 3),
+                              "wire_bytes_per_kmer": wire})
                 record(part_ms[r] + x_ms + ms, rep)
                 uniq += u
                 kept += R

@@ -3342,7 +3342,9 @@ struct MsdDriver {
         timer_units(c, slot, count);
         // the sort's own L0 also writes the level-1 digits (shard sends are re-counted after the
         // exchange, so they do not)
-        const bool with_nd = (kout == c->keys[0] || kout == c->keys[1]) && !opt("GKM_L0_NO_ND");  // (tuning knob)
+        // (a starts-only shard send has no key output: kout == nullptr, which a context whose key
+        // buffers are not allocated yet must not mistake for one of them)
+        const bool with_nd = kout && (kout == c->keys[0] || kout == c->keys[1]) && !opt("GKM_L0_NO_ND");  // (tuning knob)
         NextDigits ndg{dig_at(B, w0, width(1)), nullptr};
         if (with_nd && p88) {  // the packed L0: digit bytes and low start bits in the free start buffer
             p88_place(vout == c->vals[0] ? 0 : 1);
@@ -4442,6 +4444,10 @@ int msd_shard_partition(gk_ctx *c, const KeySpec &ks, uint64_t lo, uint64_t hi, 
     d.B = ks.bits * std::min(ks.symbols, 64 / ks.bits);  // the first key word (see msd_sort)
     d.wsched[0] = kGR;  // the exchange splits by kGR-bit buckets (msd_radix_bits)
     GK_TRY_HIP(c, msd_tables());
+    if (c->res_pk && c->acgt && ks.bits == 2) {  // both L0 passes read the transfer's packed copy
+        d.pk_code = c->res_code;
+        d.pk_dol = c->res_dol;
+    }
     int rc = d.run_l0(lo, hi, kout, vout, cap, count);
     if (rc != GK_OK) return rc;
     std::vector<uint32_t> hc(kGRadix);

@@ -3053,7 +3053,7 @@ struct MsdDriver {
         }
         for (; l < kMaxLevels; ++l) wsched[l] = w;
         if (ks.bits != 2) wsched[0] = kGR;
-        wsched[0] = std::max(wsched[0], 7);
+        wsched[0] = std::max(wsched[0], ks.canonical ? 7 : 6);  // (6: forward 2-bit L0 only)
     }
 
     Lists lists(int g, int bigsel) {
@@ -3256,6 +3256,10 @@ struct MsdDriver {
             if (pk) l0_launch<2, 7, true, CANON, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else if (nd_) l0_launch<2, 7, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else l0_launch<2, 7, false, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+        } else if (ks.bits == 2 && w0 == 6 && !CANON) {  // (A/B, GKM_LEVEL_BITS=6,...: half the L0's write streams)
+            if (pk) l0_launch<2, 6, true, false, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else if (nd_) l0_launch<2, 6, true, false>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
+            else l0_launch<2, 6, false, false>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
         } else if (ks.bits == 2) {
             if (pk) l0_launch<2, kGR, true, CANON, true>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
             else if (nd_) l0_launch<2, kGR, true, CANON>(count, a, d0, nt0, kout, vout, nt, sink, ndg);
@@ -3396,7 +3400,7 @@ struct MsdDriver {
     bool p88_wanted() const {
         if (opt("GKM_NO_P88") || !allow_c79 || ks.bits != 2 || phase != 0 || no_compact()) return false;
         const int w0 = width(0), w1 = width(1), w2 = width(2), rem = B - w0;
-        if ((w0 != 7 && w0 != kGR) || w1 != 8 || rem - 8 < 33 || rem - 8 > 48) return false;
+        if ((w0 != 6 && w0 != 7 && w0 != kGR) || w1 != 8 || rem - 8 < 33 || rem - 8 > 48) return false;
         if (opt("GKM_TEST_P88")) return true;
         const uint64_t m1 = (n >> w0) >> w1;  // mean L1 sub-bucket
         const int rem2 = rem - w1 - w2;

@@ -195,7 +195,7 @@ def test_homopolymer_genome_all_ties():
 
 # MSD depth: inputs whose buckets stay above the local limit (4096) for several global levels
 # (the random cases above finish after L0 / L1), at every level digit width (GKM_LEVEL_BITS)
-@pytest.mark.parametrize("level_bits", ["8", "8,7", "8,6", "8,7,8", "7,8,8"])
+@pytest.mark.parametrize("level_bits", ["8", "8,7", "8,6", "8,7,8", "7,8,8", "6,8,8"])
 def test_low_entropy_deep_levels_vs_oracle(level_bits, monkeypatch):
     monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", level_bits)
     rng = np.random.default_rng(11)
@@ -773,7 +773,8 @@ def test_wide_l0_k_sweep_vs_oracle(k, monkeypatch):
 # buckets the pair level sends to the finishing classes and a next level that is not compact get
 # (key, start) back first (expand_pair_*).  At test sizes GKM_TEST_PAIRS=1 makes every level whose
 # remaining bits fit write pairs; the low-entropy input keeps buckets big for several levels.
-@pytest.mark.parametrize("level_bits,k", [("8", 31), ("8,6", 31), ("7,8,8", 31), ("7,8,8", 24), ("8", 32)])
+@pytest.mark.parametrize("level_bits,k", [("8", 31), ("8,6", 31), ("7,8,8", 31), ("7,8,8", 24), ("8", 32),
+                                          ("6,8,8", 31), ("6,8,8", 27)])
 def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
     # k = 24 / 32: 33 / 48 key bits left behind the pair level (the two ends of its range)
     monkeypatch.setitem(_native.options, "GKM_TEST_PAIRS", "1")
@@ -796,7 +797,8 @@ def test_packed_pair_levels_vs_oracle(level_bits, k, monkeypatch):
 # random input sends most L0 buckets to the local classes.
 @pytest.mark.parametrize("pairs", [True, False], ids=["l1_pairs", "l1_plain"])
 @pytest.mark.parametrize("alphabet,k,level_bits", [(b"AC", 31, None), (b"AC", 24, None), (b"ACGT", 31, None),
-                                                   (b"AC", 31, "8,8,8"), (b"AC", 32, "8,8,8")])
+                                                   (b"AC", 31, "8,8,8"), (b"AC", 32, "8,8,8"), (b"AC", 31, "6,8,8"),
+                                                   (b"ACGT", 31, "6,8,8")])
 def test_packed_l0_vs_oracle(pairs, alphabet, k, level_bits, monkeypatch):
     monkeypatch.setitem(_native.options, "GKM_TEST_P88", "1")
     if pairs:

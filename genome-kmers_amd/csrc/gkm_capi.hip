@@ -231,6 +231,14 @@ hipError_t launch_rank_scatter(gk_ctx *c, const uint32_t *vals, const uint32_t *
     return hipGetLastError();
 }
 
+hipError_t read_back(gk_ctx *c, const void *dev, size_t bytes, void *host) {
+    if (bytes > 8 * (size_t)kHostPinWords) return hipErrorInvalidValue;
+    hipError_t e = hipMemcpyAsync(c->hpin, dev, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) std::memcpy(host, c->hpin, bytes);
+    return e;
+}
+
 }  // namespace gkm
 
 using namespace gkm;
@@ -450,7 +458,8 @@ extern "C" int gk_create(gk_ctx **out, int device) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counters, 4 * 64) != hipSuccess || hipMalloc(&c->hist, 4 * 256 * kMaxWords * 8) != hipSuccess ||
-        hipMalloc(&c->offsets, 4 * 256 * kMaxWords * 8) != hipSuccess || hipMalloc(&c->scalars, 8 * 64) != hipSuccess) {
+        hipMalloc(&c->offsets, 4 * 256 * kMaxWords * 8) != hipSuccess || hipMalloc(&c->scalars, 8 * 64) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&c->hpin), 8 * kHostPinWords, hipHostMallocDefault) != hipSuccess) {
         gk_destroy(c);
         return GK_E_HIP;
     }
@@ -464,6 +473,7 @@ extern "C" void gk_destroy(gk_ctx *c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->pre_stream) hipStreamSynchronize(c->pre_stream);
     xfer_release(c);
+    if (c->hpin) hipHostFree(c->hpin);
     for (hipEvent_t e : c->pre_ev) hipEventDestroy(e);
     if (c->pre_done) hipEventDestroy(c->pre_done);
     if (c->pre_stream) hipStreamDestroy(c->pre_stream);

@@ -319,11 +319,7 @@ static hipError_t ensure_tile_sums(gk_ctx *c, uint64_t ntiles) {
                   4 * (ntiles + 16 + ntiles / 1024 + 16));
 }
 
-static hipError_t read_total(gk_ctx *c, uint64_t *count) {
-    hipError_t e = hipMemcpyAsync(count, c->scalars, 8, hipMemcpyDeviceToHost, c->stream);
-    if (e != hipSuccess) return e;
-    return hipStreamSynchronize(c->stream);
-}
+static hipError_t read_total(gk_ctx *c, uint64_t *count) { return read_back(c, c->scalars, 8, count); }
 
 hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count) {
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
@@ -933,6 +929,14 @@ hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uin
     return scan_u32_exclusive(c, in, n, out, total);
 }
 
+// two exclusive scans of n entries, no read-back (the caller knows the totals)
+hipError_t scan_u32_exclusive_pair_launch(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
+                                          uint32_t *out2, uint64_t n) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = scan_u32_exclusive_launch(c, in1, n, out1);
+    return e == hipSuccess ? scan_u32_exclusive_launch(c, in2, n, out2) : e;
+}
+
 // two exclusive scans of n entries with one host round trip for both totals (scalars[62..63])
 hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
                                    uint32_t *out2, uint64_t n, uint64_t *total1, uint64_t *total2) {
@@ -945,8 +949,7 @@ hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out
     if (e == hipSuccess) e = scan_u32_exclusive_launch(c, in2, n, out2);
     if (e == hipSuccess) e = hipMemcpyAsync(c->scalars + 62, c->scalars, 8, hipMemcpyDeviceToDevice, c->stream);
     uint64_t t[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpyAsync(t, c->scalars + 62, 16, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = read_back(c, c->scalars + 62, 16, t);
     *total1 = t[1];
     *total2 = t[0];
     return e;

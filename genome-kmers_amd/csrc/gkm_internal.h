@@ -133,6 +133,9 @@ struct gk_ctx {
     uint32_t *tile_sums = nullptr;
     uint64_t tile_sums_cap = 0;
     uint64_t *scalars = nullptr;    // small device scratch [64]
+    // pinned host words [kHostPinWords] for the sort's small read-backs (list counters, scan totals):
+    // a copy into pageable memory goes through a staging buffer and costs a second blit
+    uint64_t *hpin = nullptr;
     int64_t *dhist = nullptr;
     uint64_t dhist_cap = 0;
     uint8_t *mask = nullptr;
@@ -209,6 +212,10 @@ inline const char *exp_opt(const char *) { return nullptr; }
 #endif
 
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
+constexpr int kHostPinWords = 64;
+// copy `bytes` (<= 8 * kHostPinWords) from device memory to `host` through the context's pinned
+// words, after everything enqueued on c->stream before it (synchronises the stream)
+hipError_t read_back(gk_ctx *c, const void *dev, size_t bytes, void *host);
 // pack2_kernel (gkm_msd.hip) over nwords words of 32 bytes from `from`
 hipError_t launch_pack2(const uint8_t *from, uint64_t nwords, uint64_t *code, uint32_t *dol, hipStream_t s);
 // grow-only named device scratch buffer of at least `bytes` (contents not preserved on growth)

@@ -1550,7 +1550,16 @@ __device__ __forceinline__ uint32_t wave_append(bool flag, uint32_t *counter, in
 }
 
 // list counters (device, one array): next global level, done, then the local classes
-enum { kCtrBig = 0, kCtrDone = 1, kCtrLoc = 2, kLists = kCtrLoc + kLocal, kCtrN = 8 + 2 };
+enum { kCtrBig = 0, kCtrDone = 1, kCtrLoc = 2, kLists = kCtrLoc + kLocal, kCtrNbCopy = kLists, kCtrN = 8 + 2 };
+// (kCtrNbCopy: the big list's count kept while its counter restarts, MsdDriver::drop_uniform_dev)
+// element sums per list, then the next global level's tile and chunk totals (its tile tables'
+// sizes, known with the list counts so that planning the level needs no read-back of its own)
+enum { kSumTiles = kLists, kSumChunks = kLists + 1, kSumN = kLists + 2 };
+
+__host__ __device__ inline uint32_t tiles_of(uint32_t len, uint32_t tile) { return (len + tile - 1) / tile; }
+__host__ __device__ inline uint32_t chunks_of(uint32_t len, uint32_t tile, uint32_t ctiles) {
+    return (tiles_of(len, tile) + ctiles - 1) / ctiles;
+}
 
 struct Lists {
     uint32_t *nb_start, *nb_len;                 // buckets for the next global level
@@ -1630,11 +1639,13 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
                                                            const uint32_t *__restrict__ seg_cnt, uint64_t nsub, int hi,
                                                            int B, int parity, Lists L, uint32_t *__restrict__ ctr,
                                                            unsigned long long *__restrict__ sums, uint32_t min_size,
-                                                           const uint64_t *__restrict__ ppref, int pw, int compact) {
+                                                           const uint64_t *__restrict__ ppref, int pw, int compact,
+                                                           uint32_t tile, uint32_t ctiles) {
     constexpr int NW = kClassT / 64;
     __shared__ uint32_t s_cnt[kLists][NW];
     __shared__ uint32_t s_elems[kLists][NW];
     __shared__ uint32_t s_base[kLists];
+    __shared__ uint32_t s_tc[2][NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kClassT + tid;
     const uint32_t size = i < nsub ? seg_cnt[i] : 0, st = i < nsub ? seg_base[i] : 0;
@@ -1655,7 +1666,24 @@ __global__ __launch_bounds__(kClassT) void classify_kernel(const uint32_t *__res
             s_elems[l][wave] = e;
         }
     }
+    {
+        uint32_t tl = li == kCtrBig ? tiles_of(size, tile) : 0, ch = li == kCtrBig ? chunks_of(size, tile, ctiles) : 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            tl += __shfl_xor(tl, off);
+            ch += __shfl_xor(ch, off);
+        }
+        if (lane == 0) {
+            s_tc[0][wave] = tl;
+            s_tc[1][wave] = ch;
+        }
+    }
     __syncthreads();
+    if (tid >= 64 && tid < 66) {  // (another wave than the list totals below)
+        unsigned long long t = 0;
+        for (int w = 0; w < NW; ++w) t += s_tc[tid - 64][w];
+        if (t) atomicAdd(&sums[kSumTiles + tid - 64], t);
+    }
     if (tid < kLists) {
         uint32_t tot = 0;
         unsigned long long el = 0;
@@ -1801,7 +1829,9 @@ __global__ __launch_bounds__(256) void expand_compact_kernel(const uint32_t *__r
                                                              const uint32_t *__restrict__ blen,
                                                              const uint64_t *__restrict__ bpref, int hi, int B,
                                                              const uint8_t *__restrict__ nd,
-                                                             uint64_t *__restrict__ kio, uint32_t *__restrict__ vout) {
+                                                             uint64_t *__restrict__ kio, uint32_t *__restrict__ vout,
+                                                             const uint32_t *__restrict__ nb_dev = nullptr) {
+    if (nb_dev && blockIdx.x >= *nb_dev) return;  // (a grid sized by a bound: the count is on the device)
     const uint64_t st = bst[blockIdx.x];
     const uint32_t len = blen[blockIdx.x];
     const uint64_t pf = bpref[blockIdx.x];
@@ -1858,6 +1888,46 @@ __global__ __launch_bounds__(256) void seg_counts_kernel(const uint32_t *__restr
     const uint32_t nt = (s_len[s] + tile - 1) / tile;
     ntiles[s] = nt;
     nchunks[s] = (nt + ctiles - 1) / ctiles;
+}
+
+// seg_counts_kernel and the exclusive scans of both counts in ONE workgroup, for the level's
+// bucket list of up to kSegScanMax entries (C3: 128 / 32 K buckets; the deep levels of a repeat-rich
+// genome: tens): one launch instead of seven, the totals already known from the list counters
+constexpr uint32_t kSegScanMax = 1u << 16;
+__global__ __launch_bounds__(1024) void seg_tiles_scan_kernel(const uint32_t *__restrict__ s_len, uint32_t nseg,
+                                                              uint32_t tile, uint32_t ctiles,
+                                                              uint32_t *__restrict__ tfirst,
+                                                              uint32_t *__restrict__ cfirst,
+                                                              uint32_t *__restrict__ nchunks) {
+    __shared__ uint32_t s_w[2][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t carry_t = 0, carry_c = 0;
+    for (uint32_t b0 = 0; b0 < nseg; b0 += 1024) {  // (block-uniform)
+        const uint32_t s = b0 + tid;
+        const uint32_t nt = s < nseg ? tiles_of(s_len[s], tile) : 0, nc = (nt + ctiles - 1) / ctiles;
+        const uint32_t it = wave_incl_scan(nt), ic = wave_incl_scan(nc);
+        if (lane == 63) {
+            s_w[0][wave] = it;
+            s_w[1][wave] = ic;
+        }
+        __syncthreads();
+        uint32_t pt = carry_t, pc = carry_c;
+        for (int w = 0; w < 16; ++w) {
+            const uint32_t a = s_w[0][w], d = s_w[1][w];
+            if (w < wave) {
+                pt += a;
+                pc += d;
+            }
+            carry_t += a;
+            carry_c += d;
+        }
+        if (s < nseg) {
+            tfirst[s] = pt + it - nt;
+            cfirst[s] = pc + ic - nc;
+            nchunks[s] = nc;
+        }
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2786,7 +2856,11 @@ __global__ __launch_bounds__(256) void tie_encode_list_kernel(const uint8_t *__r
 __global__ __launch_bounds__(256) void uniform_flag_kernel(const uint32_t *__restrict__ bst,
                                                            const uint32_t *__restrict__ blen,
                                                            const uint64_t *__restrict__ keys,
-                                                           uint32_t *__restrict__ mixed) {
+                                                           uint32_t *__restrict__ mixed,
+                                                           const uint32_t *__restrict__ nb_dev = nullptr,
+                                                           uint32_t *__restrict__ nb_copy = nullptr) {
+    if (nb_copy && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *nb_copy = *nb_dev;
+    if (nb_dev && blockIdx.x >= *nb_dev) return;
     const uint64_t st = bst[blockIdx.x];
     const uint32_t len = blen[blockIdx.x];
     const uint64_t k0 = keys[st];
@@ -2800,12 +2874,16 @@ __global__ __launch_bounds__(256) void route_uniform_kernel(const uint32_t *__re
                                                             const uint64_t *__restrict__ bpref, uint32_t nb,
                                                             const uint32_t *__restrict__ mixed, Lists L, int parity,
                                                             uint32_t *__restrict__ ctr,
-                                                            unsigned long long *__restrict__ sums) {
+                                                            unsigned long long *__restrict__ sums, uint32_t tile,
+                                                            uint32_t ctiles, const uint32_t *__restrict__ nb_dev = nullptr) {
+    if (nb_dev) nb = *nb_dev;
     for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < nb; b += gridDim.x * 256) {
         if (mixed[b]) {
             const uint32_t at = atomicAdd(&ctr[kCtrBig], 1u);
             put_entry(L, kCtrBig, at, bst[b], blen[b], 0, parity, bpref ? bpref[b] : 0);
             atomicAdd(&sums[kCtrBig], (unsigned long long)blen[b]);
+            atomicAdd(&sums[kSumTiles], (unsigned long long)tiles_of(blen[b], tile));
+            atomicAdd(&sums[kSumChunks], (unsigned long long)chunks_of(blen[b], tile, ctiles));
         } else {
             put_entry(L, kCtrDone, atomicAdd(&ctr[kCtrDone], 1u), bst[b], blen[b], 0, parity);
         }
@@ -2869,6 +2947,8 @@ static int grid_n(uint64_t n) { return (int)std::max<uint64_t>((n + 255) / 256, 
 hipError_t scan_u32_exclusive_pub(gk_ctx *c, const uint32_t *in, uint64_t n, uint32_t *out, uint64_t *total);
 hipError_t scan_u32_exclusive_pair(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
                                    uint32_t *out2, uint64_t n, uint64_t *total1, uint64_t *total2);
+hipError_t scan_u32_exclusive_pair_launch(gk_ctx *c, const uint32_t *in1, uint32_t *out1, const uint32_t *in2,
+                                          uint32_t *out2, uint64_t n);
 hipError_t select_flags(gk_ctx *c, const uint8_t *flags, uint64_t n, uint32_t *out_idx, uint64_t *count);
 
 // grow a device array to hold `need` entries, keeping the first `keep` entries
@@ -2979,7 +3059,7 @@ struct MsdDriver {
     unsigned cus, pgrid;
     int slot = -1, total_slot = -1;
     uint32_t *ctr = nullptr, h[kCtrN] = {0};
-    unsigned long long *sums = nullptr, hs[kLists] = {0};
+    unsigned long long *sums = nullptr, hs[kSumN] = {0};  // (one device block: ctr, then sums at byte 64)
     uint32_t *big_start[2], *big_len[2];
     uint64_t *big_pref[2];         // prefixes of the big-list buckets (Lists::nb_pref)
     uint64_t *loc_pref[kLocal];    // prefixes of generation 0's local entries (Lists::loc_pref)
@@ -3067,8 +3147,11 @@ struct MsdDriver {
     int init(uint64_t n_) {
         n = n_;
         GK_TRY_HIP(c, msd_tables());
-        GK_TRY_HIP(c, scratch(c, "msd_ctr", kCtrN, &ctr));
-        GK_TRY_HIP(c, scratch(c, "msd_sums", kLists, &sums));
+        static_assert(4 * kCtrN <= 64 && 64 + 8 * kSumN <= 8 * kHostPinWords, "list counter block");
+        uint64_t *cs;
+        GK_TRY_HIP(c, scratch(c, "msd_ctr_sums", 8 + kSumN, &cs));
+        ctr = reinterpret_cast<uint32_t *>(cs);
+        sums = reinterpret_cast<unsigned long long *>(cs + 8);
         GK_TRY_HIP(c, hipMemsetAsync(ctr, 0, 4 * kCtrN, c->stream));
         const uint64_t max_big = n / kBlockMax + 2;
         GK_TRY_HIP(c, scratch(c, "big_start0", max_big, &big_start[0]));
@@ -3086,10 +3169,12 @@ struct MsdDriver {
         return GK_OK;
     }
 
+    // the list counters and sums: one copy into pinned host memory
     int read_ctr() {
-        GK_TRY_HIP(c, hipMemcpyAsync(h, ctr, 4 * kLists, hipMemcpyDeviceToHost, c->stream));
-        GK_TRY_HIP(c, hipMemcpyAsync(hs, sums, 8 * kLists, hipMemcpyDeviceToHost, c->stream));
-        GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+        uint64_t buf[8 + kSumN];
+        GK_TRY_HIP(c, read_back(c, ctr, sizeof(buf), buf));
+        std::memcpy(h, buf, 4 * kCtrN);
+        std::memcpy(hs, buf + 8, 8 * kSumN);
         return GK_OK;
     }
 
@@ -3494,7 +3579,7 @@ struct MsdDriver {
     // ppref / pw / compact: see classify_kernel
     int classify(uint64_t nsub, int hi, int parity, int bigsel, const uint32_t *base = nullptr,
                  const uint32_t *cnt = nullptr, uint32_t min_size = 1, const uint64_t *ppref = nullptr, int pw = 0,
-                 int compact = 0) {
+                 int compact = 0, bool read = true) {
         if (!base) base = seg_base;
         if (!cnt) cnt = seg_cnt;
         for (int k = 0; k < kLocal; ++k)
@@ -3505,13 +3590,18 @@ struct MsdDriver {
         GK_TRY_HIP(c, grow_keep(c, "dn_len", ndone + nsub, ndone, &dn_len));
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nsub, ndone, &dn_par));
         GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
-        GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * kLists, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums, 0, 8 * kSumN, c->stream));
         timer_begin(c, "msd_classify", &slot);
         hipLaunchKernelGGL(classify_kernel, dim3((unsigned)((nsub + kClassT - 1) / kClassT)), dim3(kClassT), 0,
                            c->stream, base, cnt, nsub, hi, B, parity, lists(0, bigsel), ctr, sums, min_size, ppref, pw,
-                           compact);
+                           compact, (uint32_t)kPTile, ctiles);
         GK_TRY_HIP(c, hipGetLastError());
         timer_end(c, slot);
+        return read ? classify_counts() : GK_OK;
+    }
+
+    // the lists classify wrote (and drop_uniform_dev re-routed), to the host
+    int classify_counts() {
         int r = read_ctr();
         if (r != GK_OK) return r;
         for (int k = 0; k < kLocal; ++k) {
@@ -3522,6 +3612,34 @@ struct MsdDriver {
         nbig = h[kCtrBig];
         big_elems = hs[kCtrBig];
         return GK_OK;
+    }
+
+    // drop_uniform with no read-back of its own, behind a classify that did not read its lists
+    // either (the deep levels of a repeat-rich genome: one host round trip per level instead of
+    // two): the next-level list's count stays on the device; `bound` >= that count sizes the grids
+    // (the blocks past the count return at once).  Ends with classify_counts.
+    int drop_uniform_dev(int out, uint32_t bound) {
+        const uint32_t *nb_dev = ctr + kCtrBig;
+        const unsigned split = bucket_split(bound);
+        if (compact_now)
+            hipLaunchKernelGGL(expand_compact_kernel, dim3(bound, split), dim3(256), 0, c->stream, big_start[cur_big],
+                               big_len[cur_big], big_pref[cur_big], compact_hi, B, nd, c->keys[out], c->vals[out],
+                               nb_dev);
+        uint32_t *mixed;
+        GK_TRY_HIP(c, scratch(c, "uni_mixed", bound, &mixed));
+        GK_TRY_HIP(c, hipMemsetAsync(mixed, 0, 4ull * bound, c->stream));
+        hipLaunchKernelGGL(uniform_flag_kernel, dim3(bound, split), dim3(256), 0, c->stream, big_start[cur_big],
+                           big_len[cur_big], c->keys[out], mixed, nb_dev, ctr + kCtrNbCopy);
+        // (the done list has room: classify grew it by every sub-bucket, and each goes to one list)
+        GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums + kCtrBig, 0, 8, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums + kSumTiles, 0, 16, c->stream));
+        hipLaunchKernelGGL(route_uniform_kernel, dim3(grid_n(bound)), dim3(256), 0, c->stream, big_start[cur_big],
+                           big_len[cur_big], big_pref[cur_big], bound, mixed, lists(0, cur_big ^ 1), out, ctr, sums,
+                           (uint32_t)kPTile, ctiles, ctr + kCtrNbCopy);
+        GK_TRY_HIP(c, hipGetLastError());
+        cur_big ^= 1;
+        return classify_counts();
     }
 
     // one global partition level (R-bit digits below the top hi bits) over tiles already in
@@ -3906,8 +4024,10 @@ struct MsdDriver {
         GK_TRY_HIP(c, grow_keep(c, "dn_par", ndone + nbig, ndone, &dn_par));
         GK_TRY_HIP(c, hipMemsetAsync(ctr + kCtrBig, 0, 4, c->stream));
         GK_TRY_HIP(c, hipMemsetAsync(sums + kCtrBig, 0, 8, c->stream));
+        GK_TRY_HIP(c, hipMemsetAsync(sums + kSumTiles, 0, 16, c->stream));
         hipLaunchKernelGGL(route_uniform_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_start[cur_big],
-                           big_len[cur_big], big_pref[cur_big], nbig, mixed, lists(0, cur_big ^ 1), out, ctr, sums);
+                           big_len[cur_big], big_pref[cur_big], nbig, mixed, lists(0, cur_big ^ 1), out, ctr, sums,
+                           (uint32_t)kPTile, ctiles);
         GK_TRY_HIP(c, hipGetLastError());
         cur_big ^= 1;
         int r = read_ctr();
@@ -3929,11 +4049,28 @@ struct MsdDriver {
             GK_TRY_HIP(c, scratch(c, "s_nchunks", nbig, &nch));
             GK_TRY_HIP(c, scratch(c, "s_tfirst", nbig, &tfirst));
             GK_TRY_HIP(c, scratch(c, "s_cfirst", nbig, &cfirst));
-            hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big], nbig,
-                               (uint32_t)kPTile, ctiles, ntl, nch);
-            GK_TRY_HIP(c, hipGetLastError());
-            uint64_t T = 0, C = 0;
-            GK_TRY_HIP(c, scan_u32_exclusive_pair(c, ntl, tfirst, nch, cfirst, nbig, &T, &C));
+            // the tile / chunk totals came with the list counters (classify, route_uniform)
+            const uint64_t T = hs[kSumTiles], C = hs[kSumChunks];
+            if (nbig <= kSegScanMax && !opt("GKM_TEST_SEG_SCAN_MULTI")) {
+                hipLaunchKernelGGL(seg_tiles_scan_kernel, dim3(1), dim3(1024), 0, c->stream, big_len[cur_big], nbig,
+                                   (uint32_t)kPTile, ctiles, tfirst, cfirst, nch);
+                GK_TRY_HIP(c, hipGetLastError());
+            } else {
+                hipLaunchKernelGGL(seg_counts_kernel, dim3(grid_n(nbig)), dim3(256), 0, c->stream, big_len[cur_big],
+                                   nbig, (uint32_t)kPTile, ctiles, ntl, nch);
+                GK_TRY_HIP(c, hipGetLastError());
+                GK_TRY_HIP(c, scan_u32_exclusive_pair_launch(c, ntl, tfirst, nch, cfirst, nbig));
+            }
+            if (opt("GKM_TEST_CHECK_TILES")) {  // (tests: the totals against the scans' own)
+                uint32_t last[4];
+                GK_TRY_HIP(c, hipMemcpyAsync(&last[0], tfirst + nbig - 1, 4, hipMemcpyDeviceToHost, c->stream));
+                GK_TRY_HIP(c, hipMemcpyAsync(&last[1], cfirst + nbig - 1, 4, hipMemcpyDeviceToHost, c->stream));
+                GK_TRY_HIP(c, hipMemcpyAsync(&last[2], nch + nbig - 1, 4, hipMemcpyDeviceToHost, c->stream));
+                GK_TRY_HIP(c, hipMemcpyAsync(&last[3], big_len[cur_big] + nbig - 1, 4, hipMemcpyDeviceToHost, c->stream));
+                GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
+                if (last[0] + tiles_of(last[3], (uint32_t)kPTile) != T || last[1] + last[2] != C)
+                    return fail(c, GK_E_HIP, "msd: level tile totals disagree with the bucket scan");
+            }
             uint32_t *t_start, *t_count;
             GK_TRY_HIP(c, scratch(c, "t_start", T, &t_start));
             GK_TRY_HIP(c, scratch(c, "t_count", T, &t_count));
@@ -3942,17 +4079,28 @@ struct MsdDriver {
             hipLaunchKernelGGL(tile_table_kernel, dim3((unsigned)std::max<uint64_t>((std::max(T, C) + 255) / 256, 1)), dim3(256), 0,
                                c->stream, big_start[cur_big], big_len[cur_big], tfirst, cfirst, nbig,
                                (uint32_t)kPTile, (uint32_t)T, (uint32_t)C, ctiles, t_start, t_count, c_first, c_ntiles);
+            const uint64_t in_big = big_elems;
             rc = level_pass(level, hi, t_start, t_count, T, C, cfirst, nch, big_start[cur_big], nbig, c->keys[in],
                             c->vals[in], out);
             if (rc != GK_OK) return rc;
             cur_big ^= 1;
             uint64_t before[kLocal];
             for (int k = 0; k < kLocal; ++k) before[k] = nloc[k];
-            rc = classify((uint64_t)nbig << width(level), hi + width(level), out, cur_big, nullptr, nullptr, 1,
-                          big_pref[cur_big ^ 1], width(level), compact_now ? 1 : 0);
-            if (rc == GK_OK && c79_out) rc = expand_pair_locals(before, out);
-            if (rc == GK_OK) rc = expand_big(out);
-            if (rc == GK_OK && !c79_out) rc = drop_uniform(level, out);  // (pairs: keys not comparable)
+            const uint64_t nsub = (uint64_t)nbig << width(level);
+            // the level's input already small: its output's uniform buckets are dropped behind
+            // the classify with one read-back for both (drop_uniform's rule, on the input's size)
+            const bool fuse = !c79_out && level >= 1 && in_big * 64 <= std::max<uint64_t>(c->n, 1) &&
+                              !opt("GKM_NO_FUSED_UNIFORM");
+            rc = classify(nsub, hi + width(level), out, cur_big, nullptr, nullptr, 1, big_pref[cur_big ^ 1],
+                          width(level), compact_now ? 1 : 0, !fuse);
+            if (fuse) {
+                const uint64_t bound = std::min<uint64_t>(nsub, in_big / ((uint64_t)kBlockMax + 1));
+                if (rc == GK_OK) rc = bound ? drop_uniform_dev(out, (uint32_t)bound) : classify_counts();
+            } else {
+                if (rc == GK_OK && c79_out) rc = expand_pair_locals(before, out);
+                if (rc == GK_OK) rc = expand_big(out);
+                if (rc == GK_OK && !c79_out) rc = drop_uniform(level, out);  // (pairs: keys not comparable)
+            }
             if (rc != GK_OK) return rc;
             ++level;
             hi += width(level - 1);

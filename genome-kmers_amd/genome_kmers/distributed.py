@@ -47,17 +47,47 @@ def position_ranges(sba_len: int, world: int) -> list[int]:
 
 
 def split_buckets(totals: np.ndarray, world: int) -> list[int]:
-    """world + 1 bucket boundaries: rank r receives buckets [b_r, b_r+1), each range holding about
-    sum(totals) / world k-mers (b_r = first bucket whose exclusive prefix reaches r/world)."""
-    totals = np.asarray(totals, dtype=np.int64)
-    excl = np.concatenate(([0], np.cumsum(totals)[:-1]))
-    n = int(totals.sum())
-    nb = len(totals)
-    bounds = [0]
-    for r in range(1, world):
-        target = n * r // world
-        b = int(np.searchsorted(excl, target, side="left"))
-        bounds.append(min(max(b, bounds[-1]), nb))
+    """world + 1 bucket boundaries: rank r receives buckets [b_r, b_r+1).  The largest range is as
+    small as contiguous ranges allow (binary search on the capacity; a greedy fill decides whether
+    a capacity fits), and each boundary is the one nearest an even share of what is left that keeps
+    the rest within that capacity -- so one heavy bucket (the N runs' digit of an assembly) costs
+    its own rank alone, where cutting at the prefixes r/world of the total gave that rank the whole
+    bucket on top of its share."""
+    t = np.asarray(totals, dtype=np.int64)
+    nb = len(t)
+    P = np.concatenate(([0], np.cumsum(t)))  # P[i]: the buckets before i
+    n = int(P[-1])
+    if world <= 1 or n == 0:
+        return [0] * world + [nb]
+
+    def last_fit(s, cap):  # the furthest boundary e with buckets [s, e) holding <= cap
+        return int(np.searchsorted(P, P[s] + cap, side="right")) - 1
+
+    def fits(s, ranks, cap):  # buckets [s, nb) in `ranks` ranges of <= cap
+        for _ in range(ranks):
+            if s >= nb:
+                return True
+            s = last_fit(s, cap)
+        return s >= nb
+
+    lo, hi = max(-(-n // world), int(t.max())), n
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if fits(0, world, mid):
+            hi = mid
+        else:
+            lo = mid + 1
+    cap = lo
+    bounds, s = [0], 0
+    for r in range(world - 1):
+        left = world - r
+        want = P[s] + (n - P[s]) / left
+        e_max = last_fit(s, cap)
+        near = int(np.searchsorted(P, want, side="left"))
+        cands = sorted({min(near, e_max), min(max(near - 1, s), e_max)}, key=lambda e: abs(P[e] - want))
+        e = next(e for e in cands + [e_max] if fits(e, left - 1, cap))
+        bounds.append(e)
+        s = e
     bounds.append(nb)
     return bounds
 

@@ -23,6 +23,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and libgkm.so")
 
 
+@pytest.fixture(autouse=True)
+def _check_level_tile_totals(request, monkeypatch):
+    """GPU tests: every MSD level re-reads its bucket scan and compares it with the tile / chunk
+    totals the list counters carried (the product plans levels from those totals alone)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from genome_kmers import _native
+
+    try:
+        monkeypatch.setitem(_native.options, "GKM_TEST_CHECK_TILES", "1")
+    except Exception:  # no library on this machine: the test itself reports that
+        pass
+    yield
+
+
 def load_manifest():
     with open(GOLDEN / "manifest.json") as fh:
         return json.load(fh)["cases"]

@@ -150,6 +150,25 @@ def test_split_buckets_balanced_and_contiguous(world):
     assert max(share) <= totals.sum() / world + totals.max() + 1
 
 
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_split_buckets_min_max(world):
+    # one heavy bucket (an assembly's N-run digit) between light ones: the largest range is the
+    # smallest any contiguous split reaches (brute force over all boundaries at this size)
+    import itertools
+
+    rng = np.random.default_rng(10 + world)
+    totals = rng.integers(0, 100, 14)
+    totals[int(rng.integers(0, 14))] = 600
+    b = D.split_buckets(totals, world)
+    P = np.concatenate(([0], np.cumsum(totals)))
+    got = max(P[b[r + 1]] - P[b[r]] for r in range(world))
+    best = min(max(P[c[r + 1]] - P[c[r]] for r in range(world))
+               for mid in itertools.combinations_with_replacement(range(15), world - 1)
+               for c in [(0,) + mid + (14,)])
+    assert got == best
+    assert b[0] == 0 and b[-1] == 14 and all(b[i] <= b[i + 1] for i in range(world))
+
+
 def test_split_buckets_skewed():
     totals = np.zeros(256, dtype=np.int64)
     totals[7] = 10_000

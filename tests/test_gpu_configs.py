@@ -209,9 +209,39 @@ def test_small_chunks_acgt_vs_oracle(small_chunks, k):
     _oracle_sorted(_genome(5, [900_000, 300_000]), k)
 
 
-def test_small_chunks_low_entropy_levels_vs_oracle(small_chunks, monkeypatch):
+@pytest.mark.parametrize("fused_uniform", [True, False])
+def test_small_chunks_low_entropy_levels_vs_oracle(small_chunks, monkeypatch, fused_uniform):
+    # deep levels: the uniform-bucket drop behind the classify's read-back (default) or its own
+    if not fused_uniform:
+        monkeypatch.setitem(_native.options, "GKM_NO_FUSED_UNIFORM", "1")
     monkeypatch.setitem(_native.options, "GKM_LEVEL_BITS", "8,6")
     _oracle_sorted(_genome(6, [600_000], alphabet=b"AACGTT", rep_len=5000, copies=20), 31)
+
+
+@pytest.mark.parametrize("fused_uniform", [True, False])
+def test_deep_levels_identical_repeats_vs_oracle(monkeypatch, fused_uniform):
+    # buckets of > 8,192 copies of one k-mer (uniform: dropped) beside near-identical ones (another
+    # level each) several levels down -- the deep levels of a repeat-rich genome
+    if not fused_uniform:
+        monkeypatch.setitem(_native.options, "GKM_NO_FUSED_UNIFORM", "1")
+    rng = np.random.default_rng(11)
+    s = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 1_500_000).astype(np.uint8)
+    s[100_000:140_000] = np.frombuffer(b"CA" * 20_000, dtype=np.uint8)  # (CA)n: two uniform buckets
+    unit = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 60).astype(np.uint8)
+    for j in range(9000):  # 9,000 copies of a 60-mer, one substitution each at a late position
+        u = unit.copy()
+        u[40 + j % 20] = b"ACGT"[(j // 20) % 4]
+        s[200_000 + 61 * j:200_000 + 61 * j + 60] = u
+    _oracle_sorted([("c0", s.tobytes().decode())], 31)
+
+
+@pytest.mark.parametrize("k", [21, 31])
+def test_level_bucket_scan_multi_launch_vs_oracle(small_chunks, monkeypatch, k):
+    # the level tables' bucket scans as seg_counts + two device-wide scans (the branch for more
+    # than 65,536 big buckets, which no parity-size input reaches), totals cross-checked
+    monkeypatch.setitem(_native.options, "GKM_TEST_SEG_SCAN_MULTI", "1")
+    _oracle_sorted(_genome(5, [900_000, 300_000]), k)
+    _oracle_sorted(_genome(6, [600_000], alphabet=b"AACGTT", rep_len=5000, copies=20), k)
 
 
 @pytest.mark.parametrize("k", [31, 63])

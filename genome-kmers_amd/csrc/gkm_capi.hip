@@ -28,7 +28,7 @@ std::map<std::string, std::string> g_opts;
 // tracing); everything else needs gk_set_option
 const char *const kEnvKnobs[] = {"GKM_RANK_BALLOT", "GKM_PACK_IMPL",       "GKM_PACK_MIN",        "GKM_PACK_BLOCKS",
                                  "GKM_XFER_THREADS", "GKM_XFER_HYBRID",    "GKM_XFER_NUMA",       "GKM_NO_RESIDENT_PACK",
-                                 "GKM_PREFETCH_REGIONS", "GKM_MSD_TRACE"};
+                                 "GKM_PREFETCH_REGIONS", "GKM_MSD_TRACE",   "GKM_VMM_CHUNK_MB"};
 }  // namespace
 
 const char *opt(const char *name) {
@@ -42,16 +42,115 @@ const char *opt(const char *name) {
     return nullptr;
 }
 
+// Large device buffers (the k-mer arrays, the sort's scratch): hipMalloc, or -- GKM_VMM_CHUNK_MB=N,
+// opt-in -- an address range mapped from physical allocations of N MiB each (hipMemAddressReserve /
+// hipMemCreate / hipMemMap).  The scatter passes ran faster on mapped 1-4 GiB chunks: C3 69.8-70.0 ->
+// 64.7-64.9 ms with 2 GiB chunks on one box (the L1 pass 18.5 -> 15.3 ms, L2 14.5 -> 13.4-13.7, the
+// wave-local one 15.8 -> 15.1), 68.4 -> 64.7-65.4 ms with 1-4 GiB on another; chunks of 2-64 MiB or
+// of the whole array were no better than hipMalloc (profiles/r6/ab_vmm_*.txt).  Not the default: a
+// full-size C4 sort through the Python API (sort hint, prefetched class-A L0) hit an illegal address
+// with it, whose cause is not found.  A failed mapping falls back to hipMalloc.
+namespace {
+constexpr size_t kVmmMin = 256ull << 20;  // smaller buffers: hipMalloc
+struct VmmAlloc {
+    size_t size, chunk;
+    std::vector<hipMemGenericAllocationHandle_t> h;
+};
+std::mutex g_vmm_mu;
+std::map<void *, VmmAlloc> g_vmm;
+
+void vmm_release(void *base, const VmmAlloc &a) {
+    for (size_t i = 0; i < a.h.size(); ++i) {
+        (void)hipMemUnmap(static_cast<char *>(base) + i * a.chunk, a.chunk);
+        (void)hipMemRelease(a.h[i]);
+    }
+    (void)hipMemAddressFree(base, a.size);
+}
+
+hipError_t vmm_alloc(void **p, size_t bytes, size_t want) {
+    int dev = 0;
+    hipError_t r = hipGetDevice(&dev);
+    if (r != hipSuccess) return r;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    r = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (r != hipSuccess) return r;
+    if (gran == 0) gran = 2ull << 20;
+    const size_t whole = (bytes + gran - 1) / gran * gran;
+    const size_t chunk = std::min(std::max(want, gran) / gran * gran, whole);
+    VmmAlloc a{(bytes + chunk - 1) / chunk * chunk, chunk, {}};
+    void *base = nullptr;
+    r = hipMemAddressReserve(&base, a.size, gran, nullptr, 0);
+    if (r != hipSuccess) return r;
+    for (size_t off = 0; off < a.size && r == hipSuccess; off += chunk) {
+        hipMemGenericAllocationHandle_t h{};
+        r = hipMemCreate(&h, chunk, &prop, 0);
+        if (r != hipSuccess) break;
+        a.h.push_back(h);
+        r = hipMemMap(static_cast<char *>(base) + off, chunk, 0, h, 0);
+        if (r != hipSuccess) {  // (this handle is not mapped: release it alone)
+            (void)hipMemRelease(h);
+            a.h.pop_back();
+        }
+    }
+    if (r == hipSuccess) {
+        hipMemAccessDesc d{};
+        d.location = prop.location;
+        d.flags = hipMemAccessFlagsProtReadWrite;
+        r = hipMemSetAccess(base, a.size, &d, 1);
+    }
+    // zero-filled, as the driver hands out fresh hipMalloc memory
+    if (r == hipSuccess) r = hipMemset(base, 0, a.size);
+    if (r != hipSuccess) {
+        vmm_release(base, a);
+        return r;
+    }
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    g_vmm[base] = std::move(a);
+    *p = base;
+    return hipSuccess;
+}
+}  // namespace
+
+hipError_t dev_alloc(void **p, size_t bytes) {
+    const char *e = opt("GKM_VMM_CHUNK_MB");
+    const size_t want = e ? (size_t)std::strtoull(e, nullptr, 10) << 20 : 0;
+    const char *tm = opt("GKM_TEST_VMM_MIN_KB");  // (tests: mapped buffers at parity-test sizes)
+    const size_t vmin = tm ? (size_t)std::strtoull(tm, nullptr, 10) << 10 : kVmmMin;
+    if (want == 0 || bytes < vmin) return hipMalloc(p, bytes);
+    if (vmm_alloc(p, bytes, want) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();  // (the mapping's error: hipMalloc decides)
+    return hipMalloc(p, bytes);
+}
+
+hipError_t dev_free(void *p) {
+    if (!p) return hipSuccess;
+    VmmAlloc a{};
+    {
+        std::lock_guard<std::mutex> g(g_vmm_mu);
+        auto it = g_vmm.find(p);
+        if (it == g_vmm.end()) return hipFree(p);
+        a = std::move(it->second);
+        g_vmm.erase(it);
+    }
+    (void)hipDeviceSynchronize();  // (hipFree's own semantics: no kernel may still use it)
+    vmm_release(p, a);
+    return hipSuccess;
+}
+
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes) {
     if (bytes == 0) bytes = 16;
     if (*p && *cap >= bytes) return hipSuccess;
     if (*p) {
-        hipError_t e = hipFree(*p);
+        hipError_t e = dev_free(*p);
         if (e != hipSuccess) return e;
         *p = nullptr;
         *cap = 0;
     }
-    hipError_t e = hipMalloc(p, bytes);
+    hipError_t e = dev_alloc(p, bytes);
     if (e != hipSuccess) {
         *p = nullptr;
         return e;
@@ -250,14 +349,14 @@ int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
     // vals[0] / vals[1] hold data that must survive when only keys grow; grow both together
     if (n > c->elem_cap) {
         uint32_t *nv[2] = {nullptr, nullptr};
-        for (int b = 0; b < 2; ++b) GK_TRY_HIP(c, hipMalloc(&nv[b], 4 * (n + 64)));
+        for (int b = 0; b < 2; ++b) GK_TRY_HIP(c, dev_alloc(reinterpret_cast<void **>(&nv[b]), 4 * (n + 64)));
         if (c->have_starts && c->elem_cap > 0)
             GK_TRY_HIP(c, hipMemcpyAsync(nv[c->cur], c->vals[c->cur], 4 * c->n, hipMemcpyDeviceToDevice, c->stream));
         GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
         for (int b = 0; b < 2; ++b) {
-            if (c->vals[b]) hipFree(c->vals[b]);
+            if (c->vals[b]) dev_free(c->vals[b]);
             c->vals[b] = nv[b];
-            if (c->keys[b]) hipFree(c->keys[b]);
+            if (c->keys[b]) dev_free(c->keys[b]);
             c->keys[b] = nullptr;
         }
         c->elem_cap = n;
@@ -268,9 +367,9 @@ int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
     if (words > c->key_words_cap) {
         for (int b = 0; b < 2; ++b) {
             if (c->key_words_b[b] >= words) continue;
-            if (c->keys[b]) hipFree(c->keys[b]);
+            if (c->keys[b]) dev_free(c->keys[b]);
             c->keys[b] = nullptr;
-            GK_TRY_HIP(c, hipMalloc(&c->keys[b], 8 * (uint64_t)words * (c->elem_cap + 64)));
+            GK_TRY_HIP(c, dev_alloc(reinterpret_cast<void **>(&c->keys[b]), 8 * (uint64_t)words * (c->elem_cap + 64)));
             c->key_words_b[b] = words;
         }
         c->key_words_cap = words;
@@ -290,9 +389,9 @@ int gkm::ensure_elems(gk_ctx *c, uint64_t n, int words) {
 int gkm::grow_key_buffer(gk_ctx *c, int b, int words) {
     if (c->key_words_b[b] >= words) return GK_OK;
     GK_TRY_HIP(c, hipStreamSynchronize(c->stream));
-    if (c->keys[b]) hipFree(c->keys[b]);
+    if (c->keys[b]) dev_free(c->keys[b]);
     c->keys[b] = nullptr;
-    GK_TRY_HIP(c, hipMalloc(&c->keys[b], 8 * (uint64_t)words * (c->elem_cap + 64)));
+    GK_TRY_HIP(c, dev_alloc(reinterpret_cast<void **>(&c->keys[b]), 8 * (uint64_t)words * (c->elem_cap + 64)));
     c->key_words_b[b] = words;
     c->key_words_cap = std::min(c->key_words_b[0], c->key_words_b[1]);
     return GK_OK;
@@ -481,9 +580,9 @@ extern "C" void gk_destroy(gk_ctx *c) {
                     c->hist, c->offsets, c->flags, c->idx_a, c->idx_b, c->ucount, c->cumk, c->tile_sums, c->scalars,
                     c->dhist, c->mask, c->hmask, c->ranks, c->ym, c->yoff, c->oy, c->ot, c->onum};
     for (void *b : bufs)
-        if (b) hipFree(b);
+        if (b) dev_free(b);
     for (auto &e : c->scratch)
-        if (e.second.first) hipFree(e.second.first);
+        if (e.second.first) dev_free(e.second.first);
     for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;

@@ -212,6 +212,10 @@ inline const char *exp_opt(const char *) { return nullptr; }
 #endif
 
 hipError_t ensure(void **p, uint64_t *cap, uint64_t bytes);
+// large device buffers (gkm_capi.hip): hipMalloc, or an address range mapped from physical
+// allocations (GKM_VMM_CHUNK_MB); dev_free releases either
+hipError_t dev_alloc(void **p, size_t bytes);
+hipError_t dev_free(void *p);
 constexpr int kHostPinWords = 64;
 // copy `bytes` (<= 8 * kHostPinWords) from device memory to `host` through the context's pinned
 // words, after everything enqueued on c->stream before it (synchronises the stream)
@@ -230,7 +234,7 @@ inline hipError_t scratch(gk_ctx *c, const char *name, uint64_t count, T **out) 
 inline void scratch_release(gk_ctx *c, const char *name) {
     auto it = c->scratch.find(name);
     if (it == c->scratch.end()) return;
-    if (it->second.first) (void)hipFree(it->second.first);
+    if (it->second.first) (void)dev_free(it->second.first);
     c->scratch.erase(it);
 }
 // re-encode keys[cur] from vals[cur] when the sort left them stale (gk_ctx::keys_stale)

@@ -2961,7 +2961,7 @@ static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t
     }
     void *np = nullptr;
     const uint64_t bytes = sizeof(T) * (need + need / 2 + 256);
-    hipError_t r = hipMalloc(&np, bytes);
+    hipError_t r = dev_alloc(&np, bytes);
     if (r != hipSuccess) return r;
     if (e.first && keep) {
         r = hipMemcpyAsync(np, e.first, sizeof(T) * keep, hipMemcpyDeviceToDevice, c->stream);
@@ -2969,7 +2969,7 @@ static hipError_t grow_keep(gk_ctx *c, const char *name, uint64_t need, uint64_t
         r = hipStreamSynchronize(c->stream);
         if (r != hipSuccess) return r;
     }
-    if (e.first) hipFree(e.first);
+    if (e.first) dev_free(e.first);
     e.first = np;
     e.second = bytes;
     *p = static_cast<T *>(np);

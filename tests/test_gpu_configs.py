@@ -244,6 +244,17 @@ def test_level_bucket_scan_multi_launch_vs_oracle(small_chunks, monkeypatch, k):
     _oracle_sorted(_genome(6, [600_000], alphabet=b"AACGTT", rep_len=5000, copies=20), k)
 
 
+@pytest.mark.parametrize("chunk_mb", ["0", "2", "6"])
+def test_mapped_buffers_vs_oracle(monkeypatch, chunk_mb):
+    # the k-mer arrays and scratch as address ranges mapped from 2 / 6 MiB physical allocations
+    # (many chunks per array, buffers regrown between the sorts), or plain hipMalloc ("0")
+    monkeypatch.setitem(_native.options, "GKM_VMM_CHUNK_MB", chunk_mb)
+    monkeypatch.setitem(_native.options, "GKM_TEST_VMM_MIN_KB", "64")
+    _oracle_sorted(_genome(12, [700_000, 200_000], n_runs=5), 31)
+    _oracle_sorted(_genome(13, [2_500_000]), 31)
+    _oracle_sorted(_genome(14, [600_000], n_runs=5), 63, canonical=True)
+
+
 @pytest.mark.parametrize("k", [31, 63])
 def test_small_chunks_split_n_runs_vs_oracle(small_chunks, k):
     _oracle_sorted(_genome(7, [500_000, 400_000], n_runs=40), k)
